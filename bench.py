@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: decoded codewords/s, wman N576 R3/4, 20 NMS iterations.
+
+One "step" = one decode of a resident batch (default B = 2^20 codewords per GPU, the
+BASELINE.json configs[1] workload) with FER/BER counters accumulated on the device.  The
+AWGN LLRs (3.5 dB, QMS q=5) are generated on the GPU before the timed region.
+``python bench.py --gpus N --steps K --warmup W``; N > 1 is launched by torch.distributed.run
+(one rank per GPU, weak scaling: every rank decodes its own B codewords).
+
+Prints ONE JSON line (rank 0).  Besides the driver's fields it carries:
+  roofline      dominant kernel vs HBM: achieved = SURVEY §8 d bytes/codeword x B / kernel
+                time (HIP events on the decode stream); traffic = PMC HBM bytes per launch
+                when profiles/traffic_<kernel>.json exists (see tools/profile.sh), else null
+  cpu_baseline  the dense TF-graph-equivalent numpy restatement of the reference decoder
+                (oracle/nms_dense.py) on the C1 sample (B=120, T=20, 3.5 dB), rank 0, N=1
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
+GRAPH = "wman_N0576_R34_z24"
+WEIGHTS = "C0_wman_N0576_R34_z24_Opt_Weight_End20.txt"
+
+
+def survey_bytes_per_cw(E, N, z, T, ucn=False):
+    """SURVEY.md §8 d: T * (3*E*z*4 + 4*N*z*4 + N*z/8 [+ N*z/8 with UCN])."""
+    return T * (3 * E * z * 4 + 4 * N * z * 4 + N * z // 8 + (N * z // 8 if ucn else 0))
+
+
+def load_problem(T=20):
+    from ldpc_error_floor_amd.code import CodeParams, TannerGraph, load_base_graph
+    from ldpc_error_floor_amd.weights import expand_weights, read_weight_file
+    data = os.path.join(ROOT, "ldpc_error_floor_amd", "data")
+    proto = load_base_graph(os.path.join(data, "BaseGraph", GRAPH + ".txt"))
+    g = TannerGraph(proto, 24)
+    wf = read_weight_file(os.path.join(data, "Weights", WEIGHTS))
+    W = expand_weights((3, 0, 3), {0: wf.blocks[0], 2: wf.blocks[2]}, T, g)
+    return proto, g, W, CodeParams(proto, 24)
+
+
+def cpu_baseline(proto, g, W, cp, B=120, T=20, snr=3.5):
+    """Dense TF-graph-equivalent numpy decoder on the C1 sample, all allowed host cores."""
+    from threadpoolctl import threadpool_limits
+    from ldpc_error_floor_amd.channel import create_mix_epoch
+    from oracle import nms_dense, nms_oracle
+    cores = min(16, len(os.sched_getaffinity(0)))
+    sigma = float(cp.sigma(snr))
+    wr, nr = np.random.RandomState(2044), np.random.RandomState(1076)
+    X, _ = create_mix_epoch([sigma], wr, nr, B, g.N, g.N - g.M, 24, [], True, 2, 0, 0, 0, 0, 5, 20.0)
+    X = X.reshape(B, -1).astype(np.float32)
+    dg = nms_dense.DenseGraph(proto, 24)
+    with threadpool_limits(limits=cores):
+        t0 = time.perf_counter()
+        nms_dense.decode(X, proto, 24, W.alpha, W.alpha_ucn, W.beta, T, 2, 5, graph=dg)
+        dt = time.perf_counter() - t0
+        sg = nms_oracle.lifted_edges(proto, 24)
+        t1 = time.perf_counter()
+        nms_oracle.decode(np.tile(X, (8, 1)), proto, 24, W.alpha, W.alpha_ucn, W.beta, T, 2, 5, graph=sg)
+        dt_sparse = time.perf_counter() - t1
+    cpu = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), cpu)
+    except OSError:
+        pass
+    return {"value": round(B / dt, 3), "unit": "codewords/s", "cores": cores, "kind": "port",
+            "sample": f"C1: wman QMS q5 T={T}, B={B} host-channel codewords at {snr} dB (seeds "
+                      f"2044/1076), dense TF-graph-equivalent numpy (oracle/nms_dense.py), "
+                      f"{dt:.1f} s",
+            "cpu_model": cpu,
+            "sparse_oracle_cw_s": round(8 * B / dt_sparse, 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU per step")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "flood", "fused"])
+    ap.add_argument("--snr", type=float, default=3.5)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--all-kernels", action="store_true",
+                    help="also time the non-default kernel and report it under 'kernels'")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    T = args.iters
+    proto, g, W, cp = load_problem(T)
+    sigma = float(cp.sigma(args.snr))
+    B = args.batch
+
+    def run(kernel):
+        dec = NMSDecoder(proto, 24, W, 2, 5, device=dev, kernel=kernel, B_max=B)
+        llr = dec.awgn(B, sigma, seed=1076, offset=rank * B)          # resident in HBM
+        counters = torch.zeros(4, dtype=torch.int64, device=dev)
+        name = dec.kernel_info(T)[1]
+        stream = torch.cuda.current_stream(dev)
+        for _ in range(args.warmup):
+            dec.decode(llr, T=T, app=False, counters=counters)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        counters.zero_()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(args.steps):
+            dec.decode(llr, T=T, app=False, counters=counters)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        cnt = counters.clone()
+        if world > 1:
+            dist.all_reduce(cnt)
+        kernel_ms = ev0.elapsed_time(ev1) / args.steps
+        return dict(name=name, elapsed=float(elapsed.item()), kernel_ms=kernel_ms,
+                    counters=cnt.cpu().tolist(), design_bytes=dec.kernel_info(T)[0])
+
+    primary = run(args.kernel)
+    extra = {}
+    if args.all_kernels:
+        for k in ("flood", "fused"):
+            if k != primary["name"]:
+                try:
+                    r = run(k)
+                    extra[r["name"]] = {"codewords_per_s": round(world * B * args.steps / r["elapsed"], 1),
+                                        "ms_per_step": round(1e3 * r["elapsed"] / args.steps, 3)}
+                except RuntimeError as e:
+                    extra[k] = {"error": str(e)}
+
+    t = primary["elapsed"]
+    value = world * B * args.steps / t
+    bytes_cw = survey_bytes_per_cw(g.E, g.N, 24, T)
+    achieved = bytes_cw * B / (primary["kernel_ms"] / 1e3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", f"traffic_{primary['name']}.json")
+    if os.path.exists(tf):
+        try:
+            with open(tf) as f:
+                tj = json.load(f)
+            if int(tj.get("batch", -1)) == B:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    c = primary["counters"]
+    n_frames = world * B * args.steps
+    out = {
+        "metric": "decoded codewords/sec, wman N576 R3/4, 20 NMS iters",
+        "value": round(value, 1),
+        "unit": "codewords/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * t / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if primary["name"] == "flood" else "i32",
+        "data": "synthetic (on-GPU Philox AWGN, all-zero codeword, 3.5 dB, QMS q=5 LLRs)",
+        "config": {"workload": f"{GRAPH} QMS q5 T={T} sharing [3,0,3] trained weights "
+                               f"({WEIGHTS}), B={B} codewords/GPU/step @ {args.snr} dB",
+                   "batch_per_gpu": B, "iterations": T, "kernel": primary["name"],
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic,
+                     "kernel": primary["name"], "kernel_ms": round(primary["kernel_ms"], 3),
+                     "algorithmic_bytes_per_cw": bytes_cw,
+                     "design_bytes_per_cw": int(primary["design_bytes"]),
+                     "note": "achieved = SURVEY 8d two-kernel fp32 bytes/codeword x B / decode "
+                             "time (HIP events); for the fused kernel this is an effective "
+                             "figure (its real HBM traffic is design_bytes_per_cw)"},
+        "fer_at_snr": {"frames": n_frames, "fer_last": c[1] / n_frames,
+                       "ber_last": c[0] / (n_frames * g.N * 24)},
+    }
+    if extra:
+        out["kernels"] = extra
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(proto, g, W, cp, T=T)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

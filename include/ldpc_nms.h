@@ -1,0 +1,119 @@
+/*
+ * ldpc_nms.h — C ABI of the MI355X neural min-sum (NMS / quantized NMS) LDPC decoder.
+ *
+ * The reference (ghy1228/LDPC_Error_Floor) has no FFI: its decoder is a TF1 graph built by
+ * build_neural_network (Main_Functions.py:157-385) and executed through
+ *     sess.run(fetches=net_dict["ya_output_all"] [, net_dict["lossa"]],
+ *              feed_dict={xa: X[B,N,z], ya: Y, etha: e, learn_rate: 0})
+ * (Print_Functions.py:147-151).  Each entry point below replaces one piece of that:
+ *
+ *   ldpc_graph_create   <- init_parameter + init_connecting_matrix (Main_Functions.py:8-150)
+ *   ldpc_weights_set    <- weight_init's var_{i}_{t} (Main_Functions.py:387-439), already
+ *                          expanded per iteration by the sharing rules (:167-174, :266-304)
+ *   ldpc_ctx_create     <- the placeholders' fixed batch size (main_Base.py:122-127)
+ *   ldpc_decode         <- sess.run of the T unrolled iterations; app_all == ya_output_all,
+ *                          counters == calc_ber_fer (Print_Functions.py:100-118) on device
+ *
+ * Conventions: LLRs are log(p1/p0) (Print_Functions.py:45-46), bit index j*z+g, proto edges
+ * in row-major order E(C).  All device pointers are owned by the caller (e.g. torch
+ * tensors); the library owns graph tables, weights and per-context scratch.  Every call
+ * returns LDPC_OK (0) or a negative status; no exception crosses the boundary.  A context
+ * must be used by one host thread / stream at a time; there is no global mutable state.
+ */
+#ifndef LDPC_NMS_H
+#define LDPC_NMS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDPC_NMS_ABI_VERSION 1
+
+typedef struct ldpc_graph ldpc_graph;
+typedef struct ldpc_ctx ldpc_ctx;
+
+enum ldpc_status {
+    LDPC_OK = 0,
+    LDPC_ERR_ARG = -1,          /* bad argument (null pointer, size, unsupported mode) */
+    LDPC_ERR_HIP = -2,          /* a HIP runtime call or kernel launch failed */
+    LDPC_ERR_OOM = -3,          /* device allocation failed */
+    LDPC_ERR_STATE = -4,        /* weights not set / B or T above the context limits */
+    LDPC_ERR_UNSUPPORTED = -5   /* valid request this build cannot serve */
+};
+
+enum ldpc_decoding_type {       /* decoding_type of main_Base.py:27 */
+    LDPC_DEC_MS = 1,            /* min-sum fp32, messages clipped to +-clip_llr */
+    LDPC_DEC_QMS = 2,           /* quantized min-sum on the q_bit grid */
+    LDPC_DEC_MS_NONUDGE = 3     /* min-sum without the 0 -> 1e-4 nudge */
+};
+
+enum ldpc_kernel {
+    LDPC_KERNEL_AUTO = 0,       /* fused when supported, else flooding */
+    LDPC_KERNEL_FLOOD = 1,      /* two edge-parallel kernels per iteration, state in HBM */
+    LDPC_KERNEL_FUSED = 2       /* all T iterations in one launch, state in LDS/registers */
+};
+
+typedef struct ldpc_decode_params {
+    int32_t T;                  /* iterations (training_iter_end), 1 <= T <= T_max */
+    int32_t decoding_type;      /* ldpc_decoding_type */
+    int32_t q_bit;              /* 6, 5, -5, 4 or 3 (QMS only) */
+    int32_t target_bits;        /* Nt*z: width of app_all and of the FER/BER bit range */
+    float clip_llr;             /* clip_LLR (20.0 in the reference) */
+    int32_t kernel;             /* ldpc_kernel */
+    int32_t reserved[2];
+} ldpc_decode_params;
+
+typedef struct ldpc_decode_outputs {
+    float* app_all;             /* [T][B][target_bits] f32 (== ya_output_all) or NULL */
+    uint32_t* hard_bits;        /* [T][B][ceil(N*z/32)] bit v%32 of word v/32, or NULL */
+    uint32_t* synd_bits;        /* [T][B][ceil(M*z/32)] syndrome of hard_bits[t], or NULL */
+    int64_t* counters;          /* [4] += {bit errors @T-1, frames wrong @T-1,
+                                   frames wrong at every t, 2*loss (loss_type 2, etha 0)}
+                                   for the all-zero codeword; or NULL */
+    uint8_t* frame_flags;       /* [B] bit0 wrong at every t (uncor), bit1 wrong @T-1; or NULL */
+} ldpc_decode_outputs;
+
+int ldpc_abi_version(void);
+const char* ldpc_status_string(int status);
+
+/* proto: host [M][N] row-major, -1 = no edge, else cyclic shift (taken mod z). */
+int ldpc_graph_create(const int32_t* proto, int32_t M, int32_t N, int32_t z, int32_t device,
+                      ldpc_graph** out);
+int ldpc_graph_destroy(ldpc_graph* g);
+/* dims[8] = {M, N, z, E, n_checks, n_vars, n_edges, max_check_degree} */
+int ldpc_graph_query(const ldpc_graph* g, int32_t* dims);
+
+/* Host tables, copied to the device: alpha [T][E] (E(C) order), alpha_ucn [T][E] or NULL
+   (UCN weighting off), beta [T][N]. */
+int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* alpha_ucn,
+                     const float* beta);
+
+int ldpc_ctx_create(ldpc_graph* g, int64_t B_max, int32_t T_max, ldpc_ctx** out);
+int ldpc_ctx_destroy(ldpc_ctx* c);
+
+/* llr_dev: device [B][N*z] f32 (natural bit order, log p1/p0).  stream: hipStream_t (NULL =
+   default stream).  Asynchronous: returns after enqueueing on the stream. */
+int ldpc_decode(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
+                const ldpc_decode_outputs* o, void* stream);
+
+/* Bytes of HBM traffic per codeword the selected kernel is designed to move (for the
+   roofline report), and a short kernel name.  Returns 0 if unsupported. */
+int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* bytes_per_cw,
+                     char* name, int32_t name_len);
+
+/* On-GPU AWGN channel for the all-zero codeword (create_mix_epoch, Print_Functions.py:29-72):
+   writes llr_dev [B][n_vars] f32 = Q(2(sigma*n - 1)/sigma^2) with punctured (1-based bits
+   punct_start..punct_end, 0 = none) -> 0 and shortened -> -clip_llr.  n ~ N(0,1) from a
+   counter-based Philox stream indexed by (seed, offset + b, element): shards generated with
+   their global codeword offset reproduce the single-GPU stream. */
+int ldpc_channel_awgn(float* llr_dev, int64_t B, int32_t n_vars, double sigma, uint64_t seed,
+                      int64_t offset, int32_t decoding_type, int32_t q_bit, int32_t punct_start,
+                      int32_t punct_end, int32_t short_start, int32_t short_end, float clip_llr,
+                      void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDPC_NMS_H */

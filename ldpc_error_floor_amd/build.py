@@ -1,0 +1,94 @@
+"""Build the native pieces in-tree (hipcc for gfx950; no JIT cache, no pip install).
+
+Artifacts (git-ignored, shipped to the GPU box with the snapshot):
+  ldpc_error_floor_amd/libldpc_nms.so          C ABI (include/ldpc_nms.h), HIP kernels
+  ldpc_error_floor_amd/_ldpc_nms<EXT_SUFFIX>    pybind11 binding, rpath $ORIGIN
+
+Usage: python -m ldpc_error_floor_amd.build [--force] [--jobs N]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+BUILD = os.path.join(PKG, "_build")
+ARCH = os.environ.get("LDPC_OFFLOAD_ARCH", "gfx950")
+
+HIP_SOURCES = ["ldpc_capi.hip", "ldpc_flood.hip", "ldpc_fused.hip", "ldpc_channel.hip"]
+HEADERS = ["ldpc_internal.h", "ldpc_fused.h"]
+LIB = os.path.join(PKG, "libldpc_nms.so")
+EXT = os.path.join(PKG, "_ldpc_nms" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _hipcc():
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm required to build the HIP extension)")
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build(force=False, jobs=4, verbose=False):
+    os.makedirs(BUILD, exist_ok=True)
+    hipcc = _hipcc()
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "ldpc_nms.h")]
+    flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+             "-I" + INCLUDE, "-I" + CSRC, "-Wall", "-Wno-unused-result"]
+    objs, jobs_list = [], []
+    for src in HIP_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, src.replace(".hip", ".o"))
+        objs.append(o)
+        if force or _newer(o, [s] + hdrs):
+            jobs_list.append([hipcc] + flags + ["-c", s, "-o", o])
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for r in ex.map(_run, jobs_list):
+            if verbose and r.stderr:
+                print(r.stderr, file=sys.stderr)
+    if force or _newer(LIB, objs):
+        _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs)
+    py_src = os.path.join(CSRC, "pybind_module.cpp")
+    if force or _newer(EXT, [py_src, LIB, os.path.join(INCLUDE, "ldpc_nms.h")]):
+        import pybind11
+        cxx = os.environ.get("CXX", "g++")
+        _run([cxx, "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
+              "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"],
+              "-I" + INCLUDE, py_src, "-o", EXT, "-L" + PKG, "-lldpc_nms",
+              "-Wl,-rpath,$ORIGIN"])
+    return LIB, EXT
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=4)
+    a = ap.parse_args()
+    lib, ext = build(force=a.force, jobs=a.jobs, verbose=True)
+    print(lib)
+    print(ext)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,474 @@
+// ldpc_capi.hip — C ABI (include/ldpc_nms.h): graph/weights/context management, decode
+// dispatch, and the small compat kernels (output export, FER/BER counter finalisation).
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "ldpc_internal.h"
+#include "ldpc_fused.h"
+
+using namespace ldpc;
+
+struct ldpc_graph {
+    int device = 0;
+    int M = 0, N = 0, z = 0, E = 0;
+    int max_cdeg = 0, max_vdeg = 0;
+    std::vector<int32_t> row_ptr, pe_row, pe_col, pe_shift, col_ptr, col_pe;
+    int32_t* d_tables = nullptr;
+    DevGraph dev{};
+    int T_w = 0;
+    float* d_alpha = nullptr;
+    float* d_alpha_ucn = nullptr;
+    float* d_beta = nullptr;
+};
+
+struct ldpc_ctx {
+    ldpc_graph* g = nullptr;
+    int64_t B_max = 0;
+    int T_max = 0;
+    int ntiles_max = 0;
+    // flooding workspace (allocated on first use)
+    float* ch = nullptr;
+    float* Tv = nullptr;
+    float* c2v = nullptr;
+    uint64_t* hd = nullptr;
+    // counters workspace (always)
+    uint64_t* wrong = nullptr;
+    uint64_t* anypos = nullptr;
+    int32_t* biterr = nullptr;
+    // fused workspace
+    FusedWorkspace fused{};
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+template <typename T>
+int dev_alloc(T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) return LDPC_OK;
+    if (hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)) != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+        return LDPC_ERR_OOM;
+    }
+    return LDPC_OK;
+}
+
+template <typename T>
+void dev_free(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+// ---- compat kernels --------------------------------------------------------------------
+__global__ void k_export_hard(Bufs p, uint32_t* __restrict__ out, int T, int nwords) {
+    const int64_t total = (int64_t)T * p.B * nwords;
+    for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
+         id += (int64_t)gridDim.x * blockDim.x) {
+        const int w = (int)(id % nwords);
+        const int64_t b = (id / nwords) % p.B;
+        const int t = (int)(id / ((int64_t)nwords * p.B));
+        const int64_t tile = b / TILE;
+        const int bl = (int)(b - tile * TILE);
+        const int lane = bl >> 2, q = bl & 3;
+        uint32_t word = 0;
+        for (int k = 0; k < 32; ++k) {
+            const int v = w * 32 + k;
+            if (v >= p.n_vars) break;
+            word |= (uint32_t)((p.hd[hd_index(p, t, tile, v) + q] >> lane) & 1) << k;
+        }
+        out[id] = word;
+    }
+}
+
+__global__ void k_export_synd(DevGraph g, Bufs p, uint32_t* __restrict__ out, int T, int nwords) {
+    const int64_t total = (int64_t)T * p.B * nwords;
+    for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
+         id += (int64_t)gridDim.x * blockDim.x) {
+        const int w = (int)(id % nwords);
+        const int64_t b = (id / nwords) % p.B;
+        const int t = (int)(id / ((int64_t)nwords * p.B));
+        const int64_t tile = b / TILE;
+        const int bl = (int)(b - tile * TILE);
+        const int lane = bl >> 2, q = bl & 3;
+        uint32_t word = 0;
+        for (int k = 0; k < 32; ++k) {
+            const int c = w * 32 + k;
+            if (c >= g.n_checks) break;
+            const int i = c / g.z, h = c - i * g.z;
+            uint32_t par = 0;
+            for (int pe = g.row_ptr[i]; pe < g.row_ptr[i + 1]; ++pe) {
+                const int s = h + g.pe_shift[pe];
+                const int v = g.pe_col[pe] * g.z + (s >= g.z ? s - g.z : s);
+                par ^= (uint32_t)((p.hd[hd_index(p, t, tile, v) + q] >> lane) & 1);
+            }
+            word |= par << k;
+        }
+        out[id] = word;
+    }
+}
+
+__global__ void k_finalize(Bufs p, int64_t* __restrict__ counters, uint8_t* __restrict__ flags) {
+    __shared__ unsigned long long red[4][256];
+    unsigned long long c[4] = {0, 0, 0, 0};
+    for (int64_t tile = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; tile < p.ntiles;
+         tile += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t wl[4], all[4], ap[4];
+        for (int q = 0; q < 4; ++q) {
+            uint64_t valid = 0;
+            for (int l = 0; l < 64; ++l)
+                if (tile * TILE + 4 * l + q < p.B) valid |= 1ull << l;
+            wl[q] = p.wrong[((size_t)(p.T - 1) * p.ntiles + tile) * 4 + q] & valid;
+            uint64_t a = valid;
+            for (int t = 0; t < p.T; ++t) a &= p.wrong[((size_t)t * p.ntiles + tile) * 4 + q];
+            all[q] = a;
+            ap[q] = p.anypos[(size_t)tile * 4 + q] & valid;
+            c[1] += __popcll(wl[q]);
+            c[2] += __popcll(all[q]);
+            c[3] += 2 * __popcll(ap[q]) + __popcll(wl[q] & ~ap[q]);
+        }
+        c[0] += (unsigned long long)p.biterr[tile];
+        if (flags) {
+            for (int bl = 0; bl < TILE; ++bl) {
+                const int64_t b = tile * TILE + bl;
+                if (b >= p.B) break;
+                const int lane = bl >> 2, q = bl & 3;
+                flags[b] = (uint8_t)(((all[q] >> lane) & 1) | (((wl[q] >> lane) & 1) << 1));
+            }
+        }
+    }
+    for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = c[k];
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s)
+            for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && counters)
+        for (int k = 0; k < 4; ++k)
+            if (red[k][0]) atomicAdd(reinterpret_cast<unsigned long long*>(counters + k), red[k][0]);
+}
+
+int ensure_counters(ldpc_ctx* c) {
+    if (c->wrong) return LDPC_OK;
+    const size_t nt = (size_t)c->ntiles_max;
+    int st = dev_alloc(&c->wrong, (size_t)c->T_max * nt * 4);
+    if (st == LDPC_OK) st = dev_alloc(&c->anypos, nt * 4);
+    if (st == LDPC_OK) st = dev_alloc(&c->biterr, nt);
+    return st;
+}
+
+int ensure_flood(ldpc_ctx* c) {
+    if (c->ch) return LDPC_OK;
+    const ldpc_graph* g = c->g;
+    const size_t nt = (size_t)c->ntiles_max;
+    const size_t nv = (size_t)g->N * g->z, ne = (size_t)g->E * g->z;
+    int st = dev_alloc(&c->ch, nt * nv * TILE);
+    if (st == LDPC_OK) st = dev_alloc(&c->Tv, nt * nv * TILE);
+    if (st == LDPC_OK) st = dev_alloc(&c->c2v, nt * ne * TILE);
+    if (st == LDPC_OK) st = dev_alloc(&c->hd, (size_t)(c->T_max + 1) * nt * nv * 4);
+    if (st != LDPC_OK) {
+        dev_free(c->ch); dev_free(c->Tv); dev_free(c->c2v); dev_free(c->hd);
+    }
+    return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ldpc_abi_version(void) { return LDPC_NMS_ABI_VERSION; }
+
+const char* ldpc_status_string(int status) {
+    switch (status) {
+        case LDPC_OK: return "ok";
+        case LDPC_ERR_ARG: return "invalid argument";
+        case LDPC_ERR_HIP: return "HIP runtime error";
+        case LDPC_ERR_OOM: return "device out of memory";
+        case LDPC_ERR_STATE: return "invalid state (weights not set or limits exceeded)";
+        case LDPC_ERR_UNSUPPORTED: return "unsupported configuration";
+        default: return "unknown status";
+    }
+}
+
+int ldpc_graph_create(const int32_t* proto, int32_t M, int32_t N, int32_t z, int32_t device,
+                      ldpc_graph** out) {
+    if (!out) return LDPC_ERR_ARG;
+    *out = nullptr;
+    if (!proto || M <= 0 || N <= 0 || z <= 0) return LDPC_ERR_ARG;
+    ldpc_graph* g = new (std::nothrow) ldpc_graph();
+    if (!g) return LDPC_ERR_OOM;
+    g->device = device;
+    g->M = M; g->N = N; g->z = z;
+    g->row_ptr.assign(M + 1, 0);
+    for (int i = 0; i < M; ++i)
+        for (int j = 0; j < N; ++j) {
+            const int32_t s = proto[(size_t)i * N + j];
+            if (s < -1) { delete g; return LDPC_ERR_ARG; }
+            if (s != -1) {
+                g->pe_row.push_back(i);
+                g->pe_col.push_back(j);
+                g->pe_shift.push_back(s % z);
+            }
+        }
+    g->E = (int)g->pe_row.size();
+    if (g->E == 0) { delete g; return LDPC_ERR_ARG; }
+    for (int e = 0; e < g->E; ++e) g->row_ptr[g->pe_row[e] + 1]++;
+    for (int i = 0; i < M; ++i) {
+        g->max_cdeg = std::max(g->max_cdeg, g->row_ptr[i + 1]);
+        g->row_ptr[i + 1] += g->row_ptr[i];
+    }
+    if (g->max_cdeg > 64) { delete g; return LDPC_ERR_UNSUPPORTED; }
+    g->col_ptr.assign(N + 1, 0);
+    for (int e = 0; e < g->E; ++e) g->col_ptr[g->pe_col[e] + 1]++;
+    for (int j = 0; j < N; ++j) {
+        g->max_vdeg = std::max(g->max_vdeg, g->col_ptr[j + 1]);
+        g->col_ptr[j + 1] += g->col_ptr[j];
+    }
+    g->col_pe.assign(g->E, 0);
+    {
+        std::vector<int32_t> fill(g->col_ptr.begin(), g->col_ptr.end() - 1);
+        for (int e = 0; e < g->E; ++e) g->col_pe[fill[g->pe_col[e]]++] = e;   // ascending row
+    }
+    // one device block: row_ptr | pe_row | pe_col | pe_shift | col_ptr | col_pe
+    std::vector<int32_t> host;
+    host.insert(host.end(), g->row_ptr.begin(), g->row_ptr.end());
+    host.insert(host.end(), g->pe_row.begin(), g->pe_row.end());
+    host.insert(host.end(), g->pe_col.begin(), g->pe_col.end());
+    host.insert(host.end(), g->pe_shift.begin(), g->pe_shift.end());
+    host.insert(host.end(), g->col_ptr.begin(), g->col_ptr.end());
+    host.insert(host.end(), g->col_pe.begin(), g->col_pe.end());
+    {
+        DeviceGuard dg(device);
+        if (dev_alloc(&g->d_tables, host.size()) != LDPC_OK) { delete g; return LDPC_ERR_OOM; }
+        if (hipMemcpy(g->d_tables, host.data(), host.size() * sizeof(int32_t),
+                      hipMemcpyHostToDevice) != hipSuccess) {
+            dev_free(g->d_tables);
+            delete g;
+            return LDPC_ERR_HIP;
+        }
+    }
+    DevGraph& d = g->dev;
+    d.M = M; d.N = N; d.z = z; d.E = g->E;
+    d.n_checks = M * z; d.n_vars = N * z; d.n_edges = g->E * z; d.max_cdeg = g->max_cdeg;
+    const int32_t* p = g->d_tables;
+    d.row_ptr = p; p += M + 1;
+    d.pe_row = p; p += g->E;
+    d.pe_col = p; p += g->E;
+    d.pe_shift = p; p += g->E;
+    d.col_ptr = p; p += N + 1;
+    d.col_pe = p;
+    *out = g;
+    return LDPC_OK;
+}
+
+int ldpc_graph_destroy(ldpc_graph* g) {
+    if (!g) return LDPC_ERR_ARG;
+    DeviceGuard dg(g->device);
+    dev_free(g->d_tables);
+    dev_free(g->d_alpha);
+    dev_free(g->d_alpha_ucn);
+    dev_free(g->d_beta);
+    delete g;
+    return LDPC_OK;
+}
+
+int ldpc_graph_query(const ldpc_graph* g, int32_t* dims) {
+    if (!g || !dims) return LDPC_ERR_ARG;
+    const int32_t v[8] = {g->M, g->N, g->z, g->E, g->M * g->z, g->N * g->z, g->E * g->z,
+                          g->max_cdeg};
+    std::memcpy(dims, v, sizeof(v));
+    return LDPC_OK;
+}
+
+int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* alpha_ucn,
+                     const float* beta) {
+    if (!g || T <= 0 || !alpha || !beta) return LDPC_ERR_ARG;
+    DeviceGuard dg(g->device);
+    dev_free(g->d_alpha);
+    dev_free(g->d_alpha_ucn);
+    dev_free(g->d_beta);
+    g->T_w = 0;
+    const size_t ne = (size_t)T * g->E, nn = (size_t)T * g->N;
+    int st = dev_alloc(&g->d_alpha, ne);
+    if (st == LDPC_OK && alpha_ucn) st = dev_alloc(&g->d_alpha_ucn, ne);
+    if (st == LDPC_OK) st = dev_alloc(&g->d_beta, nn);
+    if (st != LDPC_OK) return st;
+    bool ok = hipMemcpy(g->d_alpha, alpha, ne * sizeof(float), hipMemcpyHostToDevice) == hipSuccess;
+    if (alpha_ucn)
+        ok = ok && hipMemcpy(g->d_alpha_ucn, alpha_ucn, ne * sizeof(float),
+                             hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMemcpy(g->d_beta, beta, nn * sizeof(float), hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) return LDPC_ERR_HIP;
+    g->T_w = T;
+    return LDPC_OK;
+}
+
+int ldpc_ctx_create(ldpc_graph* g, int64_t B_max, int32_t T_max, ldpc_ctx** out) {
+    if (!out) return LDPC_ERR_ARG;
+    *out = nullptr;
+    if (!g || B_max <= 0 || T_max <= 0) return LDPC_ERR_ARG;
+    ldpc_ctx* c = new (std::nothrow) ldpc_ctx();
+    if (!c) return LDPC_ERR_OOM;
+    c->g = g;
+    c->B_max = B_max;
+    c->T_max = T_max;
+    c->ntiles_max = (int)((B_max + TILE - 1) / TILE);
+    DeviceGuard dg(g->device);
+    const int st = ensure_counters(c);
+    if (st != LDPC_OK) { ldpc_ctx_destroy(c); return st; }
+    *out = c;
+    return LDPC_OK;
+}
+
+int ldpc_ctx_destroy(ldpc_ctx* c) {
+    if (!c) return LDPC_ERR_ARG;
+    DeviceGuard dg(c->g->device);
+    dev_free(c->ch); dev_free(c->Tv); dev_free(c->c2v); dev_free(c->hd);
+    dev_free(c->wrong); dev_free(c->anypos); dev_free(c->biterr);
+    fused_free(c->fused);
+    delete c;
+    return LDPC_OK;
+}
+
+int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* bytes_per_cw,
+                     char* name, int32_t name_len) {
+    if (!c || !p) return LDPC_ERR_ARG;
+    const ldpc_graph* g = c->g;
+    const int mode = mode_of(p->decoding_type, p->q_bit);
+    if (mode < 0) return LDPC_ERR_ARG;
+    const bool ucn = g->d_alpha_ucn != nullptr;
+    int kern = p->kernel;
+    if (kern == LDPC_KERNEL_AUTO)
+        kern = fused_supported(g->dev, mode, p->T) ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
+    if (kern == LDPC_KERNEL_FUSED && !fused_supported(g->dev, mode, p->T)) return LDPC_ERR_UNSUPPORTED;
+    if (kern != LDPC_KERNEL_FLOOD && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_ARG;
+    const int64_t nv = (int64_t)g->N * g->z, ne = (int64_t)g->E * g->z;
+    int64_t bytes = 0;
+    const char* nm = "";
+    if (kern == LDPC_KERNEL_FLOOD) {
+        // per iteration: CN reads Tv (once per variable) and C2V_t (not at t=0), writes
+        // C2V_{t+1}; VN reads C2V_{t+1} and ch, writes Tv (not at T-1) and hard bits;
+        // UCN adds the hard-bit read.  Plus the prologue transpose (llr in, ch + Tv out).
+        for (int t = 0; t < p->T; ++t) {
+            bytes += nv * 4 + (t > 0 ? ne * 4 : 0) + ne * 4;
+            bytes += ne * 4 + nv * 4 + (t < p->T - 1 ? nv * 4 : 0) + nv / 8 + (ucn ? nv / 8 : 0);
+        }
+        bytes += nv * 4 * 3;
+        nm = "flood";
+    } else {
+        bytes = fused_bytes_per_cw(g->dev, p->T);
+        nm = "fused";
+    }
+    if (bytes_per_cw) *bytes_per_cw = bytes;
+    if (name && name_len > 0) {
+        std::strncpy(name, nm, (size_t)name_len - 1);
+        name[name_len - 1] = 0;
+    }
+    return LDPC_OK;
+}
+
+int ldpc_decode(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
+                const ldpc_decode_outputs* o, void* stream) {
+    if (!c || !p || !llr_dev) return LDPC_ERR_ARG;
+    ldpc_graph* g = c->g;
+    if (B <= 0 || B > c->B_max || p->T <= 0 || p->T > c->T_max) return LDPC_ERR_STATE;
+    if (g->T_w < p->T || !g->d_alpha || !g->d_beta) return LDPC_ERR_STATE;
+    const int mode = mode_of(p->decoding_type, p->q_bit);
+    if (mode < 0) return LDPC_ERR_ARG;
+    if (p->target_bits <= 0 || p->target_bits > g->N * g->z) return LDPC_ERR_ARG;
+    if (!(p->clip_llr > 0.f)) return LDPC_ERR_ARG;
+    ldpc_decode_outputs none{};
+    const ldpc_decode_outputs& out = o ? *o : none;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    DeviceGuard dg(g->device);
+    const bool ucn = g->d_alpha_ucn != nullptr;
+
+    int kern = p->kernel;
+    if (kern == LDPC_KERNEL_AUTO)
+        kern = fused_supported(g->dev, mode, p->T) ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
+    if (kern != LDPC_KERNEL_FLOOD && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_ARG;
+    if (kern == LDPC_KERNEL_FUSED && !fused_supported(g->dev, mode, p->T))
+        return LDPC_ERR_UNSUPPORTED;
+
+    const int ntiles = (int)((B + TILE - 1) / TILE);
+    const bool count = out.counters || out.frame_flags;
+    Bufs b{};
+    b.B = B;
+    b.ntiles = ntiles;
+    b.T = p->T;
+    b.n_vars = g->N * g->z;
+    b.target_bits = p->target_bits;
+    b.clip = p->clip_llr;
+    b.alpha = g->d_alpha;
+    b.alpha_ucn = g->d_alpha_ucn;
+    b.beta = g->d_beta;
+    b.app_out = out.app_all;
+    b.count = count ? 1 : 0;
+    b.wrong = c->wrong;
+    b.anypos = c->anypos;
+    b.biterr = c->biterr;
+    const bool want_bits = out.hard_bits || out.synd_bits;
+
+    if (count) {
+        if (hipMemsetAsync(c->wrong, 0, (size_t)p->T * ntiles * 4 * sizeof(uint64_t), s) != hipSuccess ||
+            hipMemsetAsync(c->anypos, 0, (size_t)ntiles * 4 * sizeof(uint64_t), s) != hipSuccess ||
+            hipMemsetAsync(c->biterr, 0, (size_t)ntiles * sizeof(int32_t), s) != hipSuccess)
+            return LDPC_ERR_HIP;
+    }
+
+    int st;
+    if (kern == LDPC_KERNEL_FLOOD) {
+        st = ensure_flood(c);
+        if (st != LDPC_OK) return st;
+        b.ch = c->ch;
+        b.Tv = c->Tv;
+        b.c2v = c->c2v;
+        b.hd = c->hd;
+        b.hd_all = want_bits ? 1 : 0;
+        b.store_hd = (ucn || want_bits) ? 1 : 0;
+        st = flood_decode(g->dev, b, llr_dev, mode, ucn, s);
+    } else {
+        st = fused_decode(g->dev, b, c->fused, llr_dev, mode, ucn, want_bits, c->ntiles_max,
+                          c->T_max, s);
+    }
+    if (st != LDPC_OK) return st;
+
+    if (count) {
+        hipLaunchKernelGGL(k_finalize, dim3(std::min(1024, (ntiles + 255) / 256)), dim3(256), 0, s, b,
+                           out.counters, out.frame_flags);
+    }
+    if (want_bits) {
+        Bufs be = b;
+        if (kern == LDPC_KERNEL_FUSED) fused_bits_view(c->fused, be);
+        else { be.hd = c->hd; be.hd_all = 1; }
+        if (out.hard_bits) {
+            const int nw = (g->N * g->z + 31) / 32;
+            const int64_t total = (int64_t)p->T * B * nw;
+            hipLaunchKernelGGL(k_export_hard, dim3((unsigned)std::min<int64_t>(4096, (total + 255) / 256)),
+                               dim3(256), 0, s, be, out.hard_bits, p->T, nw);
+        }
+        if (out.synd_bits) {
+            const int nw = (g->M * g->z + 31) / 32;
+            const int64_t total = (int64_t)p->T * B * nw;
+            hipLaunchKernelGGL(k_export_synd, dim3((unsigned)std::min<int64_t>(4096, (total + 255) / 256)),
+                               dim3(256), 0, s, g->dev, be, out.synd_bits, p->T, nw);
+        }
+    }
+    return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+}
+
+}  // extern "C"

@@ -1,0 +1,19 @@
+// ldpc_fused.h — fused (all iterations in one launch, LDS/register-resident) decoder.
+#pragma once
+#include "ldpc_internal.h"
+
+namespace ldpc {
+
+struct FusedWorkspace {
+    uint64_t* hd = nullptr;        // [T][tiles][n_vars][4] hard decisions (only for bit export)
+    int64_t hd_elems = 0;
+};
+
+bool fused_supported(const DevGraph& g, int mode, int T);
+int64_t fused_bytes_per_cw(const DevGraph& g, int T);
+int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
+                 bool ucn, bool want_bits, int ntiles_max, int T_max, hipStream_t s);
+void fused_bits_view(const FusedWorkspace& ws, Bufs& b);
+void fused_free(FusedWorkspace& ws);
+
+}  // namespace ldpc

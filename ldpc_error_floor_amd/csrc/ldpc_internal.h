@@ -1,0 +1,74 @@
+// ldpc_internal.h — shared device-side types of the MI355X NMS decoder (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "ldpc_nms.h"
+
+namespace ldpc {
+
+constexpr int TILE = 256;          // codewords per tile: 64 lanes x float4
+constexpr int VN_PER_WAVE = 8;     // variables handled by one wave in vn_update
+
+// decoding modes (decoding_type x q_bit)
+enum Mode : int { MODE_Q6 = 0, MODE_Q5, MODE_QM5, MODE_Q4, MODE_Q3, MODE_MS, MODE_MSNN };
+__host__ __device__ constexpr bool mode_is_qms(int m) { return m <= MODE_Q3; }
+
+inline int mode_of(int decoding_type, int q_bit) {
+    if (decoding_type == LDPC_DEC_MS) return MODE_MS;
+    if (decoding_type == LDPC_DEC_MS_NONUDGE) return MODE_MSNN;
+    if (decoding_type != LDPC_DEC_QMS) return -1;
+    switch (q_bit) {
+        case 6: return MODE_Q6;
+        case 5: return MODE_Q5;
+        case -5: return MODE_QM5;
+        case 4: return MODE_Q4;
+        case 3: return MODE_Q3;
+        default: return -1;
+    }
+}
+
+// Graph tables on the device (E(C) = row-major proto-edge order).
+struct DevGraph {
+    int M, N, z, E;
+    int n_checks, n_vars, n_edges, max_cdeg;
+    const int32_t* row_ptr;    // [M+1]
+    const int32_t* pe_row;     // [E]
+    const int32_t* pe_col;     // [E]
+    const int32_t* pe_shift;   // [E]  P[i,j] mod z
+    const int32_t* col_ptr;    // [N+1]
+    const int32_t* col_pe;     // [E]  proto edges of each column, ascending row
+};
+
+// Per-decode buffers and scalars.
+struct Bufs {
+    float* ch;                 // [tiles][n_vars][256]  channel LLR
+    float* Tv;                 // [tiles][n_vars][256]  lw + S (next iteration's VN total)
+    float* c2v;                // [tiles][n_edges][256] C->V messages (check-major rows)
+    uint64_t* hd;              // [slots][tiles][n_vars][4] hard decisions, ballot layout
+    uint64_t* wrong;           // [T][tiles][4] frame has a 1 among target bits at t
+    uint64_t* anypos;          // [tiles][4]    frame has APP > 0 among target bits at T-1
+    int32_t* biterr;           // [tiles]       target bits = 1 at T-1
+    float* app_out;            // [T][B][target_bits] or null
+    const float* alpha;        // [T][E]
+    const float* alpha_ucn;    // [T][E] or null
+    const float* beta;         // [T][N]
+    int64_t B;
+    int ntiles, T, n_vars, target_bits;
+    int hd_all;                // 1: hd kept for every iteration (slots T+1), 0: ring of 2
+    int store_hd, count;
+    float clip;
+};
+
+// hard decisions of iteration s (s = -1: prologue's lw_0) live in slot s+1 (or ring (s+1)&1)
+__host__ __device__ inline size_t hd_index(const Bufs& p, int s, int64_t tile, int v) {
+    const int slot = p.hd_all ? s + 1 : ((s + 1) & 1);
+    return (((size_t)slot * p.ntiles + tile) * p.n_vars + v) * 4;
+}
+
+inline int64_t round_up8(int64_t x) { return (x + 7) & ~int64_t(7); }
+
+int flood_decode(const DevGraph& g, const Bufs& b, const float* llr, int mode, bool ucn,
+                 hipStream_t s);
+
+}  // namespace ldpc

@@ -1,0 +1,181 @@
+"""``NMSDecoder``: the HIP decoder over torch device tensors.
+
+This is the build's replacement for the T-iteration graph that ``build_neural_network``
+unrolls (``Main_Functions.py:157-385``) and ``compute_results`` runs through ``sess.run``
+(``Print_Functions.py:147-151``).  Inputs are LLRs ``[B, N*z]`` (or ``[B, N, z]``, the
+``xa`` placeholder shape) in the reference's log(p1/p0) convention; outputs are
+``ya_output_all`` (``[T*B, Nt*z]`` float32), per-iteration hard bits / syndromes, and
+on-device FER/BER counters.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _native
+from .code import TannerGraph
+from .config import DECODING_MS, DECODING_MS_NONUDGE, DECODING_QMS, VALID_Q_BITS
+from .weights import DecoderWeights
+
+__all__ = ["NMSDecoder", "DecodeResult", "KERNELS"]
+
+KERNELS = {"auto": 0, "flood": 1, "fused": 2}
+
+
+@dataclass
+class DecodeResult:
+    app: Optional["object"] = None          # torch f32 [T, B, Nt*z]
+    hard: Optional["object"] = None         # torch int32 [T, B, ceil(N*z/32)] (bit words)
+    synd: Optional["object"] = None         # torch int32 [T, B, ceil(M*z/32)]
+    counters: Optional["object"] = None     # torch int64 [4]
+    flags: Optional["object"] = None        # torch uint8 [B]
+
+    def ya_output_all(self):
+        """``ya_output_all`` layout: iterations stacked on axis 0 -> [T*B, Nt*z]."""
+        T, B, n = self.app.shape
+        return self.app.reshape(T * B, n)
+
+
+def unpack_bits(words, n_bits: int) -> np.ndarray:
+    """[..., W] uint32 words (bit k of word w = bit 32w+k) -> [..., n_bits] uint8."""
+    w = np.ascontiguousarray(np.asarray(words).astype(np.uint32))
+    b = np.unpackbits(w.view(np.uint8).reshape(w.shape + (4,)), axis=-1, bitorder="little")
+    return b.reshape(w.shape[:-1] + (w.shape[-1] * 32,))[..., :n_bits]
+
+
+class NMSDecoder:
+    def __init__(self, proto, z: int, weights: DecoderWeights, decoding_type: int = DECODING_QMS,
+                 q_bit: int = 5, target_node: int = 0, clip_LLR: float = 20.0, device=None,
+                 kernel: str = "auto", B_max: int = 0):
+        import torch
+        self._torch = torch
+        if decoding_type not in (DECODING_MS, DECODING_QMS, DECODING_MS_NONUDGE):
+            raise ValueError(f"decoding_type {decoding_type} not supported")
+        if decoding_type == DECODING_QMS and q_bit not in VALID_Q_BITS:
+            raise ValueError(f"q_bit {q_bit} not in {VALID_Q_BITS}")
+        if kernel not in KERNELS:
+            raise ValueError(f"kernel must be one of {list(KERNELS)}")
+        self.graph = TannerGraph(np.asarray(proto), int(z))
+        self.z = int(z)
+        self.N, self.M = self.graph.N, self.graph.M
+        self.n_vars = self.N * self.z
+        self.n_checks = self.M * self.z
+        self.target_node = int(target_node) if target_node and target_node > 0 else self.N
+        self.target_bits = self.target_node * self.z
+        self.decoding_type = int(decoding_type)
+        self.q_bit = int(q_bit)
+        self.clip = float(clip_LLR)
+        self.kernel = kernel
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("NMSDecoder runs on a ROCm GPU device only (no CPU fallback)")
+        self._ext = _native.load()
+        self._g = self._ext.Graph(self.graph.proto.astype(np.int32), self.z,
+                                  self.device.index or 0)
+        self.set_weights(weights)
+        self._ctx = None
+        self._ctx_B = 0
+        self._ctx_T = 0
+        if B_max:
+            self._ensure_ctx(B_max, self.T)
+
+    # ------------------------------------------------------------------------------
+    def set_weights(self, weights: DecoderWeights):
+        W = weights
+        if W.alpha.shape[1] != self.graph.E or W.beta.shape[1] != self.N:
+            raise ValueError("weight tables do not match the graph")
+        self.weights = W
+        self.T = W.T
+        self._g.set_weights(np.ascontiguousarray(W.alpha, np.float32),
+                            None if W.alpha_ucn is None else np.ascontiguousarray(W.alpha_ucn, np.float32),
+                            np.ascontiguousarray(W.beta, np.float32))
+
+    def _ensure_ctx(self, B: int, T: int):
+        if self._ctx is None or B > self._ctx_B or T > self._ctx_T:
+            Bm = max(B, self._ctx_B)
+            Tm = max(T, self._ctx_T, self.T)
+            self._ctx = None
+            self._ctx = self._ext.Ctx(self._g, int(Bm), int(Tm))
+            self._ctx_B, self._ctx_T = Bm, Tm
+        return self._ctx
+
+    def kernel_info(self, T=None, kernel=None):
+        T = self.T if T is None else T
+        ctx = self._ensure_ctx(1, T)
+        return self._ext.kernel_info(ctx, T, self.decoding_type, self.q_bit, self.target_bits,
+                                     KERNELS[kernel or self.kernel])
+
+    def supports(self, kernel: str, T=None) -> bool:
+        try:
+            self.kernel_info(T, kernel)
+            return True
+        except RuntimeError:
+            return False
+
+    def _as_llr(self, llr):
+        torch = self._torch
+        if not isinstance(llr, torch.Tensor):
+            llr = torch.from_numpy(np.ascontiguousarray(np.asarray(llr, np.float32)))
+        llr = llr.to(device=self.device, dtype=torch.float32)
+        B = llr.shape[0]
+        llr = llr.reshape(B, -1).contiguous()
+        if llr.shape[1] != self.n_vars:
+            raise ValueError(f"llr has {llr.shape[1]} bits per codeword, graph has {self.n_vars}")
+        return llr
+
+    def decode(self, llr, T: Optional[int] = None, app: bool = True, hard: bool = False,
+               synd: bool = False, counters=None, flags: bool = False, kernel: Optional[str] = None,
+               stream=None, target_bits: Optional[int] = None) -> DecodeResult:
+        """Decode a batch.  ``counters`` may be a caller-owned int64[4] device tensor that is
+        accumulated into (``+=``); pass ``True`` to get a fresh one.  ``target_bits``
+        overrides the output / FER bit range (default Nt*z)."""
+        torch = self._torch
+        T = self.T if T is None else int(T)
+        nt = self.target_bits if target_bits is None else int(target_bits)
+        if T > self.T:
+            raise ValueError(f"T={T} exceeds the {self.T} iterations the weights cover")
+        llr = self._as_llr(llr)
+        B = int(llr.shape[0])
+        ctx = self._ensure_ctx(B, T)
+        res = DecodeResult()
+        dev = self.device
+        if app:
+            res.app = torch.empty((T, B, nt), dtype=torch.float32, device=dev)
+        if hard:
+            res.hard = torch.empty((T, B, (self.n_vars + 31) // 32), dtype=torch.int32, device=dev)
+        if synd:
+            res.synd = torch.empty((T, B, (self.n_checks + 31) // 32), dtype=torch.int32, device=dev)
+        if counters is True:
+            counters = torch.zeros(4, dtype=torch.int64, device=dev)
+        if counters is not None:
+            if counters.dtype != torch.int64 or counters.numel() < 4 or counters.device != dev:
+                raise ValueError("counters must be an int64[4] tensor on the decoder's device")
+            res.counters = counters
+        if flags:
+            res.flags = torch.empty(B, dtype=torch.uint8, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        ptr = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
+        self._ext.decode(ctx, llr.data_ptr(), B, T, self.decoding_type, self.q_bit,
+                         nt, self.clip, KERNELS[kernel or self.kernel],
+                         ptr(res.app), ptr(res.hard), ptr(res.synd), ptr(res.counters),
+                         ptr(res.flags), stream.cuda_stream)
+        return res
+
+    def awgn(self, B: int, sigma: float, seed: int, offset: int = 0, punct=(0, 0), short=(0, 0),
+             out=None, stream=None):
+        """On-GPU AWGN LLRs [B, N*z] for the all-zero word (Philox, see ldpc_channel.hip)."""
+        torch = self._torch
+        if out is None:
+            out = torch.empty((B, self.n_vars), dtype=torch.float32, device=self.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        self._ext.channel_awgn(out.data_ptr(), int(B), self.n_vars, float(sigma), int(seed),
+                               int(offset), self.decoding_type, self.q_bit, int(punct[0]),
+                               int(punct[1]), int(short[0]), int(short[1]), self.clip,
+                               stream.cuda_stream)
+        return out

@@ -1,0 +1,104 @@
+"""TF1-``Session``-compatible facade so the reference's FER loops run unchanged.
+
+The reference evaluates its decoder with
+``sess.run(fetches=net_dict["ya_output_all"] [, net_dict["lossa"]], feed_dict={net_dict['xa']:
+X, net_dict['ya']: Y, net_dict['etha']: e, net_dict['learn_rate']: 0})``
+(``Print_Functions.py:147-151``).  ``build_session`` returns ``(sess, net_dict)`` where
+``net_dict`` maps the same keys to string handles and ``sess.run`` accepts those handles
+(a single one or a list) plus ``ya_output{t}`` / ``ya_output_target{t}``.  The batch size is
+fixed like the reference's placeholders (``main_Base.py:124-125``): a different B raises.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .code import TannerGraph, load_base_graph
+from .config import NMSConfig
+from .decoder import NMSDecoder
+from .metrics import loss_forward
+from .weights import DecoderWeights, expand_weights, read_weight_file
+
+__all__ = ["Session", "build_session", "make_net_dict"]
+
+FEED_KEYS = ("xa", "ya", "etha", "learn_rate")
+
+
+def make_net_dict(T: int):
+    d = {k: k for k in FEED_KEYS + ("ya_output_all", "lossa")}
+    for t in range(T):
+        d[f"ya_output{t}"] = f"ya_output{t}"
+        d[f"ya_output_target{t}"] = f"ya_output_target{t}"
+    return d
+
+
+class Session:
+    def __init__(self, decoder: NMSDecoder, batch_size: int, T=None, loss_type: int = 2,
+                 loss_t_first=None):
+        self.decoder = decoder
+        self.batch_size = int(batch_size)
+        self.T = decoder.T if T is None else int(T)
+        self.loss_type = loss_type
+        self.loss_t_first = loss_t_first
+        self.calls = 0
+
+    def run(self, fetches, feed_dict):
+        single = not isinstance(fetches, (list, tuple))
+        keys = [fetches] if single else list(fetches)
+        feed = {(k if isinstance(k, str) else str(k)): v for k, v in feed_dict.items()}
+        if "xa" not in feed:
+            raise KeyError("feed_dict must provide 'xa'")
+        X = np.asarray(feed["xa"], dtype=np.float32)
+        B = X.shape[0]
+        if B != self.batch_size:
+            raise ValueError(f"xa batch {B} != placeholder batch {self.batch_size} "
+                             "(the reference's placeholders have a fixed batch size)")
+        res = self.decoder.decode(X.reshape(B, -1), T=self.T, app=True)
+        app = res.app.cpu().numpy()                           # [T, B, Nt*z]
+        self.calls += 1
+        out = []
+        T = self.T
+        full = None
+        for k in keys:
+            if k == "ya_output_all":
+                out.append(app.reshape(T * B, -1))
+            elif k == "lossa":
+                out.append(np.float32(loss_forward(app.reshape(T * B, -1), T, B, self.loss_type,
+                                                   float(feed.get("etha", 0.0)), feed.get("ya"),
+                                                   self.loss_t_first)))
+            elif k.startswith("ya_output_target"):
+                out.append(app[int(k[len("ya_output_target"):])])
+            elif k.startswith("ya_output"):
+                t = int(k[len("ya_output"):])
+                if self.decoder.target_bits == self.decoder.n_vars:
+                    out.append(app[t])
+                else:
+                    if full is None:
+                        full = self.decoder.decode(X.reshape(B, -1), T=T, app=True,
+                                                   target_bits=self.decoder.n_vars).app.cpu().numpy()
+                    out.append(full[t])
+            else:
+                raise KeyError(f"unsupported fetch {k!r}")
+        return out[0] if single else out
+
+
+def build_session(cfg: NMSConfig, proto=None, weights: DecoderWeights = None, device=None,
+                  kernel: str = "auto", graph_dir=None):
+    """Decoder + Session + net_dict for a reference-style config."""
+    import os
+    from .code import default_graph_dir
+    cfg.validate()
+    if proto is None:
+        gd = graph_dir or os.path.join(default_graph_dir(), "BaseGraph")
+        proto = load_base_graph(os.path.join(gd, cfg.filename + ".txt"))
+    g = TannerGraph(proto, cfg.z_value)
+    T = cfg.iters_max
+    if weights is None:
+        if cfg.weights_file is None:
+            raise ValueError("weights or cfg.weights_file required")
+        wf = read_weight_file(cfg.weights_file)
+        weights = expand_weights(cfg.sharing, wf.blocks, T, g, cfg.fixed_iter)
+    dec = NMSDecoder(proto, cfg.z_value, weights, cfg.decoding_type, cfg.q_bit,
+                     cfg.target_node(g.N, g.M), cfg.clip_LLR, device=device, kernel=kernel)
+    t_first = max(cfg.iters_max - cfg.iter_step - cfg.fixed_init, cfg.fixed_iter)
+    sess = Session(dec, cfg.batch_size, T, cfg.loss_type, t_first)
+    return sess, make_net_dict(T)

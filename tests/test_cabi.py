@@ -1,0 +1,63 @@
+"""C-ABI library: loads, exports every symbol include/ldpc_nms.h declares, and validates
+arguments before touching the GPU (CPU only — no compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "ldpc_nms.h")
+LIB = os.path.join(ROOT, "ldpc_error_floor_amd", "libldpc_nms.so")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(ldpc_\w+)\s*\(", src, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        pytest.fail(f"{LIB} not built: run python -m ldpc_error_floor_amd.build")
+    return ctypes.CDLL(LIB)
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for f in ("ldpc_graph_create", "ldpc_graph_destroy", "ldpc_weights_set", "ldpc_ctx_create",
+              "ldpc_ctx_destroy", "ldpc_decode", "ldpc_channel_awgn", "ldpc_kernel_info"):
+        assert f in fns
+
+
+def test_every_declared_symbol_is_exported(lib):
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_version_and_status_strings(lib):
+    assert lib.ldpc_abi_version() == 1
+    lib.ldpc_status_string.restype = ctypes.c_char_p
+    assert lib.ldpc_status_string(0) == b"ok"
+    assert b"argument" in lib.ldpc_status_string(-1)
+    assert lib.ldpc_status_string(-99) == b"unknown status"
+
+
+def test_argument_validation_without_gpu(lib):
+    out = ctypes.c_void_p()
+    proto = (ctypes.c_int32 * 4)(0, -1, 1, 0)
+    assert lib.ldpc_graph_create(None, 2, 2, 4, 0, ctypes.byref(out)) == -1
+    assert lib.ldpc_graph_create(proto, 0, 2, 4, 0, ctypes.byref(out)) == -1
+    assert lib.ldpc_graph_create(proto, 2, 2, 4, 0, None) == -1
+    bad = (ctypes.c_int32 * 4)(-3, -1, 1, 0)
+    assert lib.ldpc_graph_create(bad, 2, 2, 4, 0, ctypes.byref(out)) == -1
+    assert lib.ldpc_graph_destroy(None) == -1
+    assert lib.ldpc_ctx_destroy(None) == -1
+    assert lib.ldpc_decode(None, None, 1, None, None, None) == -1
+    assert lib.ldpc_ctx_create(None, 10, 10, ctypes.byref(out)) == -1
+    lib.ldpc_channel_awgn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                      ctypes.c_double, ctypes.c_uint64, ctypes.c_int64] + \
+        [ctypes.c_int32] * 6 + [ctypes.c_float, ctypes.c_void_p]
+    assert lib.ldpc_channel_awgn(None, 4, 10, 0.5, 1, 0, 2, 5, 0, 0, 0, 0, 20.0, None) == -1

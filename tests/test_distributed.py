@@ -1,0 +1,74 @@
+"""Multi-process FER sweep on CPU (gloo, world_size 2): every rank decodes a disjoint
+contiguous range of the global codeword stream and ONE all_reduce(SUM) of the counter block
+gives the same totals as a single process."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN, ROOT
+from ldpc_error_floor_amd.fer import fer_sweep, shard_range
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _make_decoder():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _helpers import OracleDecoder
+    from ldpc_error_floor_amd.code import TannerGraph, load_base_graph
+    from ldpc_error_floor_amd.weights import expand_weights
+    d = np.load(os.path.join(GOLDEN, "results_wman_303.npz"))
+    proto = load_base_graph(os.path.join(ROOT, "ldpc_error_floor_amd", "data", "BaseGraph",
+                                         "wman_N0576_R34_z24.txt"))
+    W = expand_weights((3, 0, 3), {0: d["w0"], 2: d["w2"]}, 20, TannerGraph(proto, 24))
+    return OracleDecoder(proto, 24, W)
+
+
+SIGMAS = [0.7943282, 0.65]
+N_CW, BATCH = 45, 8
+
+
+def _worker(rank, world, port, q):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        res = fer_sweep(_make_decoder(), SIGMAS, N_CW, BATCH, seed=1076)
+        q.put((rank, [(c.bit_err_last, c.frame_err_last, c.frame_err_all, c.loss2) for c in res]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_range_partitions():
+    for total in (0, 1, 7, 45, 1 << 20):
+        for world in (1, 2, 3, 8):
+            parts = [shard_range(total, r, world) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == total
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+
+
+def test_gloo_world2_equals_single_process():
+    single = [(c.bit_err_last, c.frame_err_last, c.frame_err_all, c.loss2)
+              for c in fer_sweep(_make_decoder(), SIGMAS, N_CW, BATCH, seed=1076)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0] == got[1] == single
+    assert single[0][1] > 0           # the low-SNR point has frame errors

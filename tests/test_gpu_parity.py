@@ -1,0 +1,79 @@
+"""HIP decoder vs the reference fixtures and the oracle, through the C ABI (GPU only)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import DECODER_CASES, GOLDEN, ROOT, load_case
+from _helpers import counters_from_app, flags_from_app
+
+pytestmark = pytest.mark.gpu
+KERNEL_NAMES = ["flood", "fused"]
+MS_ATOL = 1e-3
+
+
+def _decoder(c, kernel, device):
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    Nt = c["Nt"] if c["Nt"] < c["g"].N else 0
+    dec = NMSDecoder(c["g"].proto, c["z"], c["W"], c["dt"], c["q"], target_node=Nt,
+                     device=device, kernel=kernel)
+    if not dec.supports(kernel):
+        pytest.skip(f"{kernel} kernel does not support this configuration")
+    return dec
+
+
+def test_extension_is_native(cuda_device):
+    from ldpc_error_floor_amd import _native
+    mod = _native.load()
+    assert mod.__file__.startswith(os.path.join(ROOT, "ldpc_error_floor_amd"))
+    assert mod.abi_version() == 1
+
+
+@pytest.mark.parametrize("kernel", KERNEL_NAMES)
+@pytest.mark.parametrize("name", DECODER_CASES)
+def test_decoder_matches_reference(name, kernel, cuda_device):
+    from ldpc_error_floor_amd.decoder import unpack_bits
+    c = load_case(name)
+    dec = _decoder(c, kernel, cuda_device)
+    res = dec.decode(c["llr"], app=True, hard=True, synd=True, counters=True, flags=True)
+    app = res.app.cpu().numpy()
+    ref = c["app"]
+    if c["exact"]:
+        assert np.array_equal(app, ref), f"max |diff| {np.abs(app - ref).max()}"
+        hard_ok = np.ones(c["hard"].shape, bool)
+    else:
+        np.testing.assert_allclose(app, ref, rtol=0, atol=MS_ATOL)
+        hard_ok = np.ones(c["hard"].shape, bool)
+        hard_ok[:, :, :c["Nt"] * c["z"]] = np.abs(ref) >= MS_ATOL
+    hard = unpack_bits(res.hard.cpu().numpy(), dec.n_vars)
+    assert np.array_equal(hard[hard_ok], c["hard"][hard_ok])
+    synd = unpack_bits(res.synd.cpu().numpy(), dec.n_checks)
+    if hard_ok.all():
+        assert np.array_equal(synd, c["synd"])
+    assert np.array_equal(res.counters.cpu().numpy(), counters_from_app(app))
+    assert np.array_equal(res.flags.cpu().numpy(), flags_from_app(app))
+    if hard_ok.all():
+        assert np.array_equal(res.counters.cpu().numpy(), counters_from_app(ref))
+
+
+def test_session_fer_loop_reproduces_reference_results(cuda_device):
+    from ldpc_error_floor_amd import fer
+    from ldpc_error_floor_amd.code import TannerGraph, load_base_graph
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    from ldpc_error_floor_amd.session import Session, make_net_dict
+    from ldpc_error_floor_amd.weights import expand_weights
+    d = np.load(os.path.join(GOLDEN, "results_wman_303.npz"))
+    proto = load_base_graph(os.path.join(ROOT, "ldpc_error_floor_amd", "data", "BaseGraph",
+                                         "wman_N0576_R34_z24.txt"))
+    g = TannerGraph(proto, 24)
+    W = expand_weights((3, 0, 3), {0: d["w0"], 2: d["w2"]}, 20, g)
+    for kernel in KERNEL_NAMES:
+        dec = NMSDecoder(proto, 24, W, 2, 5, device=cuda_device, kernel=kernel)
+        if not dec.supports(kernel):
+            continue
+        sess = Session(dec, batch_size=int(d["B"]))
+        wr, nr = np.random.RandomState(2044), np.random.RandomState(1076)
+        Results, _ = fer.compute_results(int(d["sample_num"]), [], [], d["sigma"], wr, nr,
+                                         int(d["B"]), 0, g.N, g.M, 24, True, 20, sess,
+                                         make_net_dict(20), 0, 2, 0, 0, 0, 0, 5, 20.0)
+        np.testing.assert_array_equal(Results, d["Results"])

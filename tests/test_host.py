@@ -1,0 +1,188 @@
+"""Host-side logic: graph construction, code parameters, weight files, config, channel,
+metrics.  CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+from ldpc_error_floor_amd import code, config, metrics, weights, channel
+from ldpc_error_floor_amd.code import TannerGraph, CodeParams, load_base_graph
+
+DATA = os.path.join(ROOT, "ldpc_error_floor_amd", "data")
+GRAPHS = sorted(f[:-4] for f in os.listdir(os.path.join(DATA, "BaseGraph")) if f.endswith(".txt"))
+Z_OF = {"wman_N0576_R34_z24": 24, "802_11n_N648_R56_z27": 27, "MACKAY_N96_K48": 1,
+        "BCH_63_51": 1, "Polar_64_48": 1}
+
+
+def _z(name):
+    if name in Z_OF:
+        return Z_OF[name]
+    return int(name.split("_z")[1].split("_")[0])
+
+
+@pytest.mark.parametrize("name", GRAPHS)
+def test_tanner_graph_structure(name):
+    proto = load_base_graph(os.path.join(DATA, "BaseGraph", name + ".txt"))
+    z = _z(name)
+    g = TannerGraph(proto, z)
+    assert g.E == int((proto != -1).sum())
+    assert g.n_edges == g.E * z
+    # every check has deg(row) edges, every variable deg(col) edges
+    assert np.array_equal(np.diff(g.check_ptr), np.repeat(g.cn_deg, z))
+    assert np.array_equal(np.diff(g.var_ptr), np.repeat(g.vn_deg, z))
+    # lifting convention (Main_Functions.py:64-66): check i*z+h -> var j*z+(h+s)%z
+    e = np.arange(g.n_edges)
+    i = g.pe_row[g.edge_pe]
+    j = g.pe_col[g.edge_pe]
+    h = g.edge_check - i * z
+    assert np.array_equal(g.edge_check // z, i)
+    assert np.array_equal(g.edge_var, j * z + (h + proto[i, j] % z) % z)
+    # edges are check-major and inside a check ordered by column (E(C) order)
+    assert np.all(np.diff(g.edge_check) >= 0)
+    assert e.size == g.n_edges
+    if z <= 27:
+        H = g.parity_check_matrix()
+        assert H.sum() == g.n_edges   # no parallel edges
+
+
+def test_code_params_rate_quirk():
+    proto = load_base_graph(os.path.join(DATA, "BaseGraph", "wman_N0576_R34_z24.txt"))
+    cp = CodeParams(proto, 24)
+    assert cp.M == 6 and cp.N == 24 and cp.E == 88
+    assert cp.rate == pytest.approx(431 / 574, abs=0)           # punct/short num = 1 each
+    assert float(cp.sigma(3.5)) == pytest.approx(0.5453839, abs=1e-7)
+    p2 = load_base_graph(os.path.join(DATA, "BaseGraph", "802_11n_N648_R56_z27.txt"))
+    assert code.code_rate(p2, 27) == pytest.approx(539 / 646, abs=0)
+    p5 = load_base_graph(os.path.join(DATA, "BaseGraph",
+                                      "5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640.txt"))
+    assert code.code_rate(p5, 64, 1, 128, 513, 640) == pytest.approx(0.5, abs=0)
+    assert float(code.snr_to_sigma(2.0, 0.5)) == pytest.approx(0.7943282, abs=1e-7)
+
+
+def test_results_fixture_sigma_matches():
+    d = np.load(os.path.join(GOLDEN, "results_wman_303.npz"))
+    proto = load_base_graph(os.path.join(DATA, "BaseGraph", "wman_N0576_R34_z24.txt"))
+    np.testing.assert_array_equal(CodeParams(proto, 24).sigma(d["snr"]), d["sigma"])
+
+
+def test_weight_file_parse_and_reference_order():
+    wf = weights.read_weight_file(os.path.join(DATA, "Weights",
+                                               "C0_wman_N0576_R34_z24_Opt_Weight_End20.txt"))
+    assert wf.sharing == (3, 3, 3)
+    assert all(wf.blocks[k].shape == (20, 1) for k in range(3))
+    assert np.array_equal(wf.blocks[0], wf.blocks[1])           # UCN rows == CN rows
+    ref = dict(np.load(os.path.join(GOLDEN, "weights_reference_order.npz")))
+    tags = sorted({k.split("/")[0] for k in ref})
+    srcs = {"post_wman": "Weights/C0_wman_N0576_R34_z24_Opt_Weight_End20.txt",
+            "base303_wman": "Weights/C0_wman_N0576_R34_z24_Opt_Weight_End20.txt",
+            "wifi50": "Results/WIFI/Weights_Iter50.txt",
+            "g5_1024": "Results/5G/5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640_Weight_End50.txt"}
+    for tag in tags:
+        start, end, fixed, M, N, E, s0, s1, s2 = ref[f"{tag}/meta"].tolist()
+        got = weights.load_weights_reference_order(os.path.join(DATA, srcs[tag]), (s0, s1, s2),
+                                                   start, end, fixed, M, N, E)
+        for kind, rows in got.items():
+            for t in range(rows.shape[0]):
+                want = ref[f"{tag}/var_{kind}_{t}"]
+                assert np.array_equal(rows[t], np.broadcast_to(want, rows[t].shape)), (tag, kind, t)
+
+
+def test_expand_weights_semantics():
+    proto = load_base_graph(os.path.join(DATA, "BaseGraph",
+                                         "5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640.txt"))
+    g = TannerGraph(proto, 64)
+    wf = weights.read_weight_file(os.path.join(
+        DATA, "Results/5G/5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640_Weight_End50.txt"))
+    W = weights.expand_weights(wf.sharing, wf.blocks, 20, g)
+    assert W.alpha.shape == (20, g.E) and W.beta.shape == (20, g.N) and W.ucn
+    # type 2 CN: weight of edge e is the row weight of its check row
+    np.testing.assert_array_equal(W.alpha[3], wf.blocks[0][3][g.pe_row].astype(np.float32))
+    # type 4 reuses row fixed_iter from then on
+    rows = {0: np.arange(5 * g.E, dtype=np.float64).reshape(5, g.E) / 1000}
+    W4 = weights.expand_weights((4, 0, 0), rows, 9, g, fixed_iter=4)
+    assert np.array_equal(W4.alpha[8], W4.alpha[4]) and W4.alpha_ucn is None
+    assert np.all(W4.beta == 1)
+    with pytest.raises(ValueError):
+        weights.expand_weights((5, 0, 3), {0: np.ones((3, g.M)), 2: np.ones((3, 1))}, 3, g)
+    # UCN weights only for the matched pairs
+    assert weights.expand_weights((4, 4, 3), {0: np.ones((3, g.E)), 1: np.ones((3, g.E)),
+                                              2: np.ones((3, 1))}, 3, g, 2).alpha_ucn is None
+
+
+def test_check_params():
+    ok = config.check_params(0, [2, 3], (3, 0, 3), 20, 0, 20)
+    assert ok.tolist() == [2, 3]
+    assert config.check_params(1, [2, 3], (3, 3, 3), 30, 20, 10).tolist() == [0.0]
+    for args in [(2, [1, 2], (3, 0, 3), 20, 0, 20), (0, [2], (0, 0, 0), 20, 0, 20),
+                 (0, [2], (4, 0, 3), 30, 0, 7), (0, [2], (3, 0, 1), 20, 0, 20),
+                 (0, [2], (3, 2, 3), 20, 0, 20)]:
+        with pytest.raises(config.ConfigError):
+            config.check_params(*args)
+    cfg = config.NMSConfig()
+    assert cfg.word_seed == 2044 and cfg.noise_seed == 1076
+    with pytest.raises(config.ConfigError):
+        config.NMSConfig(decoding_type=0).validate()
+
+
+def test_channel_matches_reference():
+    ref = dict(np.load(os.path.join(GOLDEN, "channel_reference.npz")))
+    for tag in ("wman_q5", "wman_ms", "g5_q5", "g5_sp"):
+        z, N, M, dt, q, ps, pe, ss, se, B = ref[f"{tag}/spec"].tolist()
+        sig = ref[f"{tag}/sigma"]
+        wr = np.random.RandomState(2044)
+        nr = np.random.RandomState(1076)
+        X, Y = channel.create_mix_epoch(sig[:1], wr, nr, B, N, N - M, z, [], True, dt, ps, pe,
+                                        ss, se, q, 20.0)
+        X2, _ = channel.create_mix_epoch(sig, wr, nr, 7, N, N - M, z, [], True, dt, ps, pe, ss,
+                                         se, q, 20.0)
+        assert X.dtype == np.float64 and X.shape == (B, N, z)
+        assert np.array_equal(X, ref[f"{tag}/X"]), tag
+        assert np.array_equal(X2, ref[f"{tag}/X2"]), tag
+        assert np.array_equal(Y, ref[f"{tag}/Y"])
+        # RNG states advanced identically
+        assert np.array_equal(nr.normal(0, 1, 3), ref[f"{tag}/next_noise"])
+        assert np.array_equal(wr.randint(0, 2, 3), ref[f"{tag}/next_word"])
+
+
+def test_uncor_roundtrip(tmp_path):
+    X = np.round(np.random.RandomState(0).normal(0, 3, (5, 4, 3)) * 2) / 2
+    flag = np.array([1, 0, 1, 1, 0], float)
+    p = tmp_path / "Uncor.txt"
+    channel.write_uncor_file(flag, X, 12, str(p))
+    arr = np.loadtxt(p, dtype=np.float32, delimiter="\t")
+    assert arr.shape == (3, 15) and np.all(arr[:, :3] == 0)
+    inp = np.delete(arr, [0, 1, 2], 1)
+    Xb, Yb = channel.read_uncor_llr(inp, np.zeros(inp.shape, np.int64), 0, 3, 4, 3)
+    np.testing.assert_array_equal(Xb, X[flag == 1].astype(np.float32))
+
+
+def _calc_ber_fer_loop(y_pred_all, iters_max, Y_test, batch_size):
+    # straightforward per-iteration loop with the reference's contract
+    length = y_pred_all.shape[1]
+    flags = []
+    for i in range(iters_max):
+        blk = y_pred_all[i * batch_size:(i + 1) * batch_size]
+        flags.append(np.abs((blk >= 0) - Y_test[:, :length]).sum(axis=1) > 0)
+    uncor = np.min(np.array(flags, float), axis=0)
+    last = y_pred_all[(iters_max - 1) * batch_size:iters_max * batch_size]
+    err = ((last >= 0) - Y_test[:, :length]).sum(axis=1)
+    return (np.abs(err.sum()) / (Y_test.shape[0] * Y_test.shape[1]), flags[-1].sum() / Y_test.shape[0],
+            uncor.sum() / batch_size, uncor, err)
+
+
+def test_calc_ber_fer_contract():
+    rng = np.random.RandomState(3)
+    T, B, n = 6, 9, 40
+    y = np.round(rng.normal(-1, 2, (T * B, n)) * 2) / 2
+    y[:B * 2] = -3
+    Y = np.zeros((B, n + 8), np.int64)
+    a = metrics.calc_ber_fer(y, T, Y, B)
+    b = _calc_ber_fer_loop(y, T, Y, B)
+    for u, v in zip(a, b):
+        np.testing.assert_array_equal(u, v)
+
+
+def test_loss_forward_type2():
+    y = np.array([[-1.0, -2.0], [0.0, -1.0], [0.5, -3.0], [-1, -1]], np.float32)   # T=1, B=4
+    assert metrics.loss_forward(y, 1, 4, 2) == pytest.approx((0 + 0.5 + 1 + 0) / 4)
