@@ -18,6 +18,7 @@ struct ldpc_graph {
     int32_t* d_tables = nullptr;
     DevGraph dev{};
     int T_w = 0;
+    int per_edge_w = 0;        // CN weights differ inside a proto row (sharing 1/4)
     float* d_alpha = nullptr;
     float* d_alpha_ucn = nullptr;
     float* d_beta = nullptr;
@@ -314,6 +315,16 @@ int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* 
     ok = ok && hipMemcpy(g->d_beta, beta, nn * sizeof(float), hipMemcpyHostToDevice) == hipSuccess;
     if (!ok) return LDPC_ERR_HIP;
     g->T_w = T;
+    g->per_edge_w = 0;
+    for (int t = 0; t < T && !g->per_edge_w; ++t)
+        for (int i = 0; i < g->M && !g->per_edge_w; ++i)
+            for (int e = g->row_ptr[i] + 1; e < g->row_ptr[i + 1]; ++e) {
+                const size_t a0 = (size_t)t * g->E + g->row_ptr[i], a1 = (size_t)t * g->E + e;
+                if (alpha[a1] != alpha[a0] || (alpha_ucn && alpha_ucn[a1] != alpha_ucn[a0])) {
+                    g->per_edge_w = 1;
+                    break;
+                }
+            }
     return LDPC_OK;
 }
 
@@ -423,7 +434,7 @@ int ldpc_decode(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_
     b.biterr = c->biterr;
     const bool want_bits = out.hard_bits || out.synd_bits;
 
-    if (count) {
+    if (count && kern == LDPC_KERNEL_FLOOD) {
         if (hipMemsetAsync(c->wrong, 0, (size_t)p->T * ntiles * 4 * sizeof(uint64_t), s) != hipSuccess ||
             hipMemsetAsync(c->anypos, 0, (size_t)ntiles * 4 * sizeof(uint64_t), s) != hipSuccess ||
             hipMemsetAsync(c->biterr, 0, (size_t)ntiles * sizeof(int32_t), s) != hipSuccess)
@@ -443,11 +454,11 @@ int ldpc_decode(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_
         st = flood_decode(g->dev, b, llr_dev, mode, ucn, s);
     } else {
         st = fused_decode(g->dev, b, c->fused, llr_dev, mode, ucn, want_bits, c->ntiles_max,
-                          c->T_max, s);
+                          c->T_max, g->per_edge_w, out.counters, out.frame_flags, s);
     }
     if (st != LDPC_OK) return st;
 
-    if (count) {
+    if (count && kern == LDPC_KERNEL_FLOOD) {
         hipLaunchKernelGGL(k_finalize, dim3(std::min(1024, (ntiles + 255) / 256)), dim3(256), 0, s, b,
                            out.counters, out.frame_flags);
     }

@@ -12,7 +12,8 @@ struct FusedWorkspace {
 bool fused_supported(const DevGraph& g, int mode, int T);
 int64_t fused_bytes_per_cw(const DevGraph& g, int T);
 int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
-                 bool ucn, bool want_bits, int ntiles_max, int T_max, hipStream_t s);
+                 bool ucn, bool want_bits, int ntiles_max, int T_max, int per_edge_w,
+                 int64_t* counters, uint8_t* flags, hipStream_t s);
 void fused_bits_view(const FusedWorkspace& ws, Bufs& b);
 void fused_free(FusedWorkspace& ws);
 
