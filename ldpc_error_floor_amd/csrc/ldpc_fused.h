@@ -15,6 +15,14 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
                  bool ucn, bool want_bits, int ntiles_max, int T_max, int per_edge_w,
                  int64_t* counters, uint8_t* flags, hipStream_t s);
 void fused_bits_view(const FusedWorkspace& ws, Bufs& b);
+const char* fused_kernel_name(const DevGraph& g, int mode, int T);
+
+// v3 (ldpc_fused3.hip): shape-specialised variant, preferred when a shape fits
+bool fused3_supported(const DevGraph& g, int T);
+const char* fused3_shape_name(const DevGraph& g, int T);
+int fused3_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, float step,
+                  int clip_u, bool per_edge_w, uint64_t* hd_out, int64_t* counters,
+                  uint8_t* flags, hipStream_t s);
 void fused_free(FusedWorkspace& ws);
 
 }  // namespace ldpc

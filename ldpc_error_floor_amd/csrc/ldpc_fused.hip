@@ -21,6 +21,8 @@
 // Lanes: lane = slot * CW + cw.  The SLOTS = 64/CW slots of a wave work on SLOTS checks of
 // the same proto row (h = hg + slot*hstep), so the row's degree, columns, shifts and weights
 // stay wave-uniform (scalar registers) while each slot gathers its own variables.
+#include <cstdlib>
+
 #include "ldpc_fused.h"
 
 namespace ldpc {
@@ -389,8 +391,27 @@ float mode_step(int mode) {
 
 }  // namespace
 
+static int fused_version() {
+    const char* e = getenv("LDPC_FUSED_VERSION");
+    return e ? atoi(e) : 3;
+}
+
+static bool fused2_supported(const DevGraph& g, int T);
+
 bool fused_supported(const DevGraph& g, int mode, int T) {
     if (mode != MODE_Q5 && mode != MODE_QM5 && mode != MODE_Q4 && mode != MODE_Q3) return false;
+    if (g.n_vars >= 32768) return false;
+    if (fused_version() >= 3 && fused3_supported(g, T)) return true;
+    return fused2_supported(g, T);
+}
+
+const char* fused_kernel_name(const DevGraph& g, int mode, int T) {
+    if (!fused_supported(g, mode, T)) return "";
+    if (fused_version() >= 3 && fused3_supported(g, T)) return fused3_shape_name(g, T);
+    return "fused2";
+}
+
+static bool fused2_supported(const DevGraph& g, int T) {
     if (g.max_cdeg > FUSED_MAXDEG) return false;
     if (g.n_vars >= 65536 || g.z >= 65536) return false;      // 16-bit packed graph info
     const int cw = fused_cw(g, T);
@@ -414,6 +435,28 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
     const float step = mode_step(mode);
     const float cu = b.clip / step;
     if (cu != rintf(cu) || cu > 32000.f) return LDPC_ERR_UNSUPPORTED;
+    uint64_t* hd_out = nullptr;
+    if (want_bits) {
+        const size_t elems = (size_t)(T_max + 1) * ntiles_max * g.n_vars * 4;
+        if ((int64_t)elems > ws.hd_elems) {
+            if (ws.hd) (void)hipFree(ws.hd);
+            ws.hd = nullptr;
+            ws.hd_elems = 0;
+            if (hipMalloc(reinterpret_cast<void**>(&ws.hd), elems * sizeof(uint64_t)) != hipSuccess) {
+                (void)hipGetLastError();
+                return LDPC_ERR_OOM;
+            }
+            ws.hd_elems = (int64_t)elems;
+        }
+        if (hipMemsetAsync(ws.hd, 0, (size_t)(b.T + 1) * b.ntiles * g.n_vars * 4 * sizeof(uint64_t), s) != hipSuccess)
+            return LDPC_ERR_HIP;
+        hd_out = ws.hd;
+    }
+    if (fused_version() >= 3 && fused3_supported(g, b.T)) {
+        const int qmax = (mode == MODE_Q4) ? 7 : (mode == MODE_Q3) ? 3 : 15;
+        return fused3_decode(g, b, llr, qmax, step, (int)cu, per_edge_w != 0, hd_out, counters,
+                             flags, s);
+    }
     const int cw = fused_cw(g, b.T);
     FusedArgs a{};
     a.g = g;
@@ -435,22 +478,7 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
     a.ngroups = g.M * a.hstep;
     a.nent = (g.n_vars * cw + FUSED_THREADS - 1) / FUSED_THREADS;
     a.zmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.z - 1) / (uint64_t)g.z);
-    if (want_bits) {
-        const size_t elems = (size_t)(T_max + 1) * ntiles_max * g.n_vars * 4;
-        if ((int64_t)elems > ws.hd_elems) {
-            if (ws.hd) (void)hipFree(ws.hd);
-            ws.hd = nullptr;
-            ws.hd_elems = 0;
-            if (hipMalloc(reinterpret_cast<void**>(&ws.hd), elems * sizeof(uint64_t)) != hipSuccess) {
-                (void)hipGetLastError();
-                return LDPC_ERR_OOM;
-            }
-            ws.hd_elems = (int64_t)elems;
-        }
-        if (hipMemsetAsync(ws.hd, 0, (size_t)(b.T + 1) * b.ntiles * g.n_vars * 4 * sizeof(uint64_t), s) != hipSuccess)
-            return LDPC_ERR_HIP;
-        a.hd_out = ws.hd;
-    }
+    a.hd_out = hd_out;
     a.counters = counters;
     a.flags = flags;
     const int nblocks = (int)((b.B + cw - 1) / cw);

@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Run a few decodes of one kernel for rocprofv3 (kernel trace / PMC counters).
+usage: python3 tools/prof_decode.py --kernel fused --batch 262144 --reps 3"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="fused")
+    ap.add_argument("--batch", type=int, default=1 << 18)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--snr", type=float, default=3.5)
+    a = ap.parse_args()
+    import torch
+    import bench
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    proto, g, W, cp = bench.load_problem(20)
+    dec = NMSDecoder(proto, 24, W, 2, 5, kernel=a.kernel, B_max=a.batch)
+    llr = dec.awgn(a.batch, float(cp.sigma(a.snr)), seed=1076)
+    cnt = torch.zeros(4, dtype=torch.int64, device=llr.device)
+    for _ in range(a.reps):
+        dec.decode(llr, app=False, counters=cnt)
+    torch.cuda.synchronize()
+    print("counters", cnt.tolist(), "kernel", dec.kernel_info()[1])
+
+
+if __name__ == "__main__":
+    main()
