@@ -382,7 +382,7 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
         nm = "flood";
     } else {
         bytes = fused_bytes_per_cw(g->dev, p->T);
-        nm = fused_kernel_name(g->dev, mode, p->T);
+        nm = fused_kernel_name(g->dev, mode, p->T, g->per_edge_w != 0);
     }
     if (bytes_per_cw) *bytes_per_cw = bytes;
     if (name && name_len > 0) {

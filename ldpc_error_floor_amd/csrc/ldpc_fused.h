@@ -15,7 +15,13 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
                  bool ucn, bool want_bits, int ntiles_max, int T_max, int per_edge_w,
                  int64_t* counters, uint8_t* flags, hipStream_t s);
 void fused_bits_view(const FusedWorkspace& ws, Bufs& b);
-const char* fused_kernel_name(const DevGraph& g, int mode, int T);
+const char* fused_kernel_name(const DevGraph& g, int mode, int T, bool per_edge_w);
+
+// v4 (ldpc_fused4.hip): two codewords per lane (packed 16-bit), preferred when it fits
+bool fused4_supported(const DevGraph& g, int T, int qmax, bool per_edge_w);
+const char* fused4_shape_name(const DevGraph& g, int T);
+int fused4_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, float step,
+                  int clip_u, uint64_t* hd_out, int64_t* counters, uint8_t* flags, hipStream_t s);
 
 // v3 (ldpc_fused3.hip): shape-specialised variant, preferred when a shape fits
 bool fused3_supported(const DevGraph& g, int T);

@@ -393,10 +393,12 @@ float mode_step(int mode) {
 
 static int fused_version() {
     const char* e = getenv("LDPC_FUSED_VERSION");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : 4;
 }
 
 static bool fused2_supported(const DevGraph& g, int T);
+
+static int mode_qmax(int mode) { return (mode == MODE_Q4) ? 7 : (mode == MODE_Q3) ? 3 : 15; }
 
 bool fused_supported(const DevGraph& g, int mode, int T) {
     if (mode != MODE_Q5 && mode != MODE_QM5 && mode != MODE_Q4 && mode != MODE_Q3) return false;
@@ -405,8 +407,10 @@ bool fused_supported(const DevGraph& g, int mode, int T) {
     return fused2_supported(g, T);
 }
 
-const char* fused_kernel_name(const DevGraph& g, int mode, int T) {
+const char* fused_kernel_name(const DevGraph& g, int mode, int T, bool per_edge_w) {
     if (!fused_supported(g, mode, T)) return "";
+    if (fused_version() >= 4 && fused4_supported(g, T, mode_qmax(mode), per_edge_w))
+        return fused4_shape_name(g, T);
     if (fused_version() >= 3 && fused3_supported(g, T)) return fused3_shape_name(g, T);
     return "fused2";
 }
@@ -452,8 +456,10 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
             return LDPC_ERR_HIP;
         hd_out = ws.hd;
     }
+    if (fused_version() >= 4 && fused4_supported(g, b.T, mode_qmax(mode), per_edge_w != 0))
+        return fused4_decode(g, b, llr, mode_qmax(mode), step, (int)cu, hd_out, counters, flags, s);
     if (fused_version() >= 3 && fused3_supported(g, b.T)) {
-        const int qmax = (mode == MODE_Q4) ? 7 : (mode == MODE_Q3) ? 3 : 15;
+        const int qmax = mode_qmax(mode);
         return fused3_decode(g, b, llr, qmax, step, (int)cu, per_edge_w != 0, hd_out, counters,
                              flags, s);
     }

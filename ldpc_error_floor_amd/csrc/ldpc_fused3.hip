@@ -56,20 +56,33 @@ __device__ __forceinline__ int q_mag(int m, float w, float step, float inv, int 
 }
 
 struct St3 {
-    int mA, mB, idx, ucn;
-    uint32_t osg;
+    int mA, mB;        // quantized magnitudes (raw minima with per-edge weights)
+    uint32_t oh;       // one-hot argmin edge
+    uint32_t ns;       // bit k: message of edge k is negative (even count of other positives)
+    int ucn;           // syndrome of the previous hard decision (per-edge weights only)
 };
+
+// -1 if bit k of x is set, else 0 (v_bfe_i32)
+__device__ __forceinline__ int bitmask(uint32_t x, int k) { return ((int)(x << (31 - k))) >> 31; }
 
 template <bool PEW>
 __device__ __forceinline__ int msg3(const St3& s, int k, float w, float wu, float step, float inv,
                                     int qmax) {
-    int m = (k == s.idx) ? s.mB : s.mA;
+    const int eq = bitmask(s.oh, k);
+    int m = (eq & s.mB) | (~eq & s.mA);                     // v_bfi
     if constexpr (PEW) m = q_mag(m, s.ucn ? wu : w, step, inv, qmax);
-    return ((s.osg >> k) & 1u) ? m : -m;
+    const int sg = bitmask(s.ns, k);
+    return (m ^ sg) - sg;                                   // sg ? -m : m
+}
+
+__device__ __forceinline__ int med3i(int x, int lo, int hi) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "s"(hi));
+    return r;
 }
 
 template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW>
-__global__ void __launch_bounds__(1024, 1)
+__global__ void __launch_bounds__(1024)
 k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ alpha_ucn) {
     constexpr int SLOTS = 64 / CW;
     constexpr int LOGCW = (CW == 64) ? 6 : (CW == 32) ? 5 : (CW == 16) ? 4 : 3;
@@ -134,9 +147,11 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
             const int hg = grp - i * a.hstep;
             const int r0 = a.row_ptr[i];
             const int deg = a.row_ptr[i + 1] - r0;
-            const int h = hg + slot * a.hstep;
+            // consecutive checks on consecutive slots: their variable rows are adjacent, so
+            // the two slots sharing a ds_read lane group hit disjoint bank halves
+            const int h = hg * SLOTS + slot;
             gval[gi] = h < z;
-            const int hl = (h < z) ? h : hg;
+            const int hl = (h < z) ? h : hg * SLOTS;
             grow[gi] = (uint32_t)r0 | ((uint32_t)deg << 16);
 #pragma unroll
             for (int k = 0; k < MAXDEG; ++k) {
@@ -152,7 +167,7 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
 
     St3 st[MAXG];
 #pragma unroll
-    for (int gi = 0; gi < MAXG; ++gi) { st[gi].mA = 0; st[gi].mB = 0; st[gi].idx = 0; st[gi].ucn = 0; st[gi].osg = 0; }
+    for (int gi = 0; gi < MAXG; ++gi) { st[gi].mA = 0; st[gi].mB = 0; st[gi].oh = 0; st[gi].ns = 0; st[gi].ucn = 0; }
 
     for (int t = 0; t < a.T; ++t) {
         if (tid == 0 && t > 0) {        // fold iteration t-1's frame flags (its VN phase is done)
@@ -164,6 +179,70 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
         const float* atp = alpha + (size_t)(t > 0 ? t - 1 : 0) * a.E;
         const float* aup = UCN ? alpha_ucn + (size_t)(t > 0 ? t - 1 : 0) * a.E : nullptr;
         // ======== check nodes ================================================================
+        // pass 1 for every group first (reads only), then pass 2 (S scatter): the groups'
+        // dependency chains are independent, so the compiler can interleave them.
+        uint32_t K1[MAXG], K2[MAXG], NEG[MAXG], SYN[MAXG];
+#pragma unroll
+        for (int gi = 0; gi < MAXG; ++gi) {
+            K1[gi] = ((uint32_t)F3_BIG_U << 6) | 63u;
+            K2[gi] = K1[gi];
+            NEG[gi] = 0;
+            SYN[gi] = 0;
+            const int grp = wave + gi * NWV;
+            if (grp >= a.ngroups) break;
+            const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
+            const int r0 = (int)(ri & 0xFFFFu);
+            const int deg = (int)(ri >> 16);
+            const St3& s = st[gi];
+            uint32_t c1 = ((uint32_t)F3_BIG_U << 6) | 63u, c2 = c1;
+#pragma unroll
+            for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
+                if (c8 < deg) {
+                    uint32_t wv[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int k = c8 + j;
+                        const uint32_t pk = gad[gi][k >> 1];
+                        const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
+                        wv[j] = *reinterpret_cast<const uint32_t*>(smem + addr);
+                    }
+                    uint32_t kk[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int k = c8 + j;
+                        kk[j] = ((uint32_t)F3_BIG_U << 6) | 63u;
+                        if (k < deg) {
+                            const int tv = ((int)(wv[j] << 17)) >> 17;            // bits 14..0
+                            const float w = PEW ? atp[r0 + k] : 0.f;
+                            const float wu = (PEW && UCN) ? aup[r0 + k] : 0.f;
+                            const int cold = msg3<PEW>(s, k, w, wu, step, inv, qmax);
+                            const int x = med3i(tv - cold, -qmax, qmax);          // Q(v2c)
+                            const uint32_t mag = (uint32_t)max(x, -x);            // 0 == +1e-4
+                            kk[j] = (mag << 6) | (uint32_t)k;
+                            NEG[gi] |= ((uint32_t)x >> 31) << k;
+                            if (UCN) SYN[gi] ^= (wv[j] >> 15) & 1u;
+                        }
+                    }
+                    uint32_t lo[4], hi[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) { lo[j] = min(kk[2 * j], kk[2 * j + 1]); hi[j] = max(kk[2 * j], kk[2 * j + 1]); }
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const uint32_t a1 = lo[2 * j], a2 = hi[2 * j], b1 = lo[2 * j + 1], b2 = hi[2 * j + 1];
+                        lo[j] = min(a1, b1);
+                        hi[j] = min(max(a1, b1), min(a2, b2));
+                    }
+                    const uint32_t d1 = min(lo[0], lo[1]);
+                    const uint32_t d2 = min(max(lo[0], lo[1]), min(hi[0], hi[1]));
+                    const uint32_t o1 = c1, o2 = c2;
+                    c1 = min(o1, d1);
+                    c2 = min(max(o1, d1), min(o2, d2));
+                }
+            }
+            uint32_t lo[1] = {c1}, hi[1] = {c2};
+            K1[gi] = lo[0];
+            K2[gi] = hi[0];
+        }
 #pragma unroll
         for (int gi = 0; gi < MAXG; ++gi) {
             const int grp = wave + gi * NWV;
@@ -172,48 +251,14 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
             const int r0 = (int)(ri & 0xFFFFu);
             const int deg = (int)(ri >> 16);
             St3& s = st[gi];
-            uint32_t k1 = ((uint32_t)F3_BIG_U << 6) | 63u, k2 = k1;
-            uint32_t neg = 0, syn = 0;
-#pragma unroll
-            for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
-                if (c8 < deg) {
-                    uint32_t wv[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int k = c8 + j;
-                        if (k < MAXDEG) {
-                            const uint32_t pk = gad[gi][k >> 1];
-                            const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
-                            wv[j] = *reinterpret_cast<const uint32_t*>(smem + addr);
-                        }
-                    }
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int k = c8 + j;
-                        if (k < MAXDEG && k < deg) {
-                            const int tv = ((int)(wv[j] << 17)) >> 17;          // bits 14..0
-                            const float w = PEW ? atp[r0 + k] : 0.f;
-                            const float wu = (PEW && UCN) ? aup[r0 + k] : 0.f;
-                            const int cold = msg3<PEW>(s, k, w, wu, step, inv, qmax);
-                            int x = tv - cold;
-                            x = min(max(x, -qmax), qmax);                      // Q(v2c)
-                            const uint32_t mag = (uint32_t)(x < 0 ? -x : x);   // 0 == +1e-4
-                            const uint32_t key = (mag << 6) | (uint32_t)k;
-                            k2 = max(k1, min(k2, key));
-                            k1 = min(k1, key);
-                            neg |= ((uint32_t)x >> 31) << k;
-                            if (UCN) syn ^= (wv[j] >> 15) & 1u;
-                        }
-                    }
-                }
-            }
             const uint32_t dmask = (deg >= 32) ? 0xFFFFFFFFu : ((1u << deg) - 1u);
-            const uint32_t pos = ~neg & dmask;
+            const uint32_t pos = ~NEG[gi] & dmask;
             const uint32_t par = __popc(pos) & 1u;
-            s.osg = pos ^ (par ? 0xFFFFFFFFu : 0u);
-            s.idx = (int)(k1 & 63u);
+            const uint32_t syn = SYN[gi];
+            s.ns = ~(pos ^ (par ? 0xFFFFFFFFu : 0u));      // negative: even count of other positives
+            s.oh = 1u << (K1[gi] & 63u);
             s.ucn = (int)syn;
-            const int m1 = (int)(k1 >> 6), m2 = (int)(k2 >> 6);
+            const int m1 = (int)(K1[gi] >> 6), m2 = (int)(K2[gi] >> 6);
             if (PEW) {
                 s.mA = m1;
                 s.mB = m2;
@@ -229,7 +274,7 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         const int k = c8 + j;
-                        if (k < MAXDEG && k < deg) {
+                        if (k < deg) {
                             const uint32_t pk = gad[gi][k >> 1];
                             const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
                             const float w = PEW ? at[r0 + k] : 0.f;
