@@ -393,7 +393,7 @@ float mode_step(int mode) {
 
 static int fused_version() {
     const char* e = getenv("LDPC_FUSED_VERSION");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 3;   // v4 (packed) is opt-in until it beats v3
 }
 
 static bool fused2_supported(const DevGraph& g, int T);

@@ -15,6 +15,7 @@
 //   LDS W[v][cw]  u32 = S_{t+1} (bits 31..16, ds_add) | hd_t (bit 15) | Tv (bits 14..0, signed)
 //       CH[v][cw] f32 channel LLR;  BETA[T][N];  RED[8] frame-flag masks / counters
 #include <cstdio>
+#include <cstdlib>
 
 #include "ldpc_fused.h"
 
@@ -41,11 +42,16 @@ struct F3Args {
     int n_vars, N, E, z;
     int hstep, ngroups, nent;
     uint32_t zmagic;
+    int ablate;        // diagnostic only (LDPC_DIAG_ABLATE): 1 skip CN pass 1, 2 skip pass 2, 4 skip VN
 };
 
 __device__ __forceinline__ int q_units(float x, float inv, int qmax) {
-    const float r = fminf(fmaxf(rintf(x * inv), -(float)qmax), (float)qmax);
+    const float r = __builtin_amdgcn_fmed3f(rintf(x * inv), -(float)qmax, (float)qmax);
     return (int)r;
+}
+// Q(x) in grid units when x is already scaled by the (power-of-two) inverse step
+__device__ __forceinline__ int q_scaled(float xs, float qm) {
+    return (int)__builtin_amdgcn_fmed3f(rintf(xs), -qm, qm);
 }
 
 __device__ __forceinline__ int q_mag(int m, float w, float step, float inv, int qmax) {
@@ -115,18 +121,25 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
     {
         float* scr = reinterpret_cast<float*>(W);            // [CW][nv+1]
         const int rl = nv + 1;
-        for (int f = tid; f < CW * nv; f += NT) {
-            const int r = f / nv, v = f - r * nv;
-            scr[r * rl + v] = (r < nvalid) ? a.llr[(b0 + r) * nv + v] : 0.f;
+        for (int v0 = 0; v0 < nv; v0 += NT) {
+            const int v = v0 + tid;
+            float x[CW];
+#pragma unroll
+            for (int r = 0; r < CW; ++r)
+                x[r] = (v < nv && r < nvalid) ? a.llr[(b0 + r) * nv + v] : 0.f;
+#pragma unroll
+            for (int r = 0; r < CW; ++r)
+                if (v < nv) scr[r * rl + v] = x[r];
         }
-        for (int f = tid; f < a.T * a.N; f += NT) BETA[f] = a.beta[f];
+        // beta pre-multiplied by 1/step (a power of two): fl32(ch*beta)/step == fl32(ch*(beta/step))
+        for (int f = tid; f < a.T * a.N; f += NT) BETA[f] = a.beta[f] * inv;
         if (tid < 8) RED[tid] = (tid == 1) ? ~0ull : 0ull;
         __syncthreads();
         for (int e = tid; e < total; e += NT) CH[e] = scr[(e & (CW - 1)) * rl + (e >> LOGCW)];
         __syncthreads();
         for (int e = tid; e < total; e += NT) {
             const uint32_t v = (uint32_t)e >> LOGCW;
-            const int t0 = q_units(CH[e] * BETA[__umulhi(v, a.zmagic)], inv, qmax);   // lw_0
+            const int t0 = q_scaled(CH[e] * BETA[__umulhi(v, a.zmagic)], (float)qmax);   // lw_0
             W[e] = ((uint32_t)t0 & 0x7FFFu) | ((uint32_t)(t0 >= 0) << 15);           // hd_{-1}
         }
     }
@@ -190,6 +203,7 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
             SYN[gi] = 0;
             const int grp = wave + gi * NWV;
             if (grp >= a.ngroups) break;
+            if (a.ablate & 1) continue;
             const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
             const int r0 = (int)(ri & 0xFFFFu);
             const int deg = (int)(ri >> 16);
@@ -268,6 +282,7 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 s.mB = q_mag(m2, w, step, inv, qmax);
             }
             if (!gval[gi]) { s.mA = 0; s.mB = 0; }    // duplicate stand-in check: no messages
+            if (a.ablate & 2) continue;
 #pragma unroll
             for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
                 if (c8 < deg) {
@@ -291,7 +306,45 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
         const bool last = (t == a.T - 1);
         const float* bnext = BETA + (size_t)(last ? t : t + 1) * a.N;
         uint32_t any_hd = 0, any_pos = 0, nbits = 0;
-        for (int r = 0; r < a.nent; ++r) {
+        const float qmf = (float)qmax;
+        const bool full_target = a.target_bits >= nv;
+        if (a.app_out == nullptr && a.hd_out == nullptr) {
+            // fast path: 4 entries' LDS reads in flight before any is consumed
+            for (int r0 = 0; r0 < ((a.ablate & 4) ? 0 : a.nent); r0 += 4) {
+                uint32_t wv[4], vv[4];
+                float chv[4], bv[4];
+                bool in[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int e = tid + (r0 + j) * NT;
+                    in[j] = e < total;
+                    const int ee = in[j] ? e : tid;
+                    vv[j] = (uint32_t)ee >> LOGCW;
+                    wv[j] = W[ee];
+                    chv[j] = CH[ee];
+                    bv[j] = bnext[__umulhi(vv[j], a.zmagic)];
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int e = tid + (r0 + j) * NT;
+                    const int S = (int)wv[j] >> 16;
+                    int app = q_scaled(chv[j] * inv, qmf) + S;                // Q(xa) + sum C2V
+                    app = med3i(app, -a.clip_u, a.clip_u);                   // clip +-clip_LLR
+                    if (in[j]) {
+                        if (!last) {
+                            const int tn = q_scaled(chv[j] * bv[j], qmf) + S;
+                            W[e] = UCN ? (((uint32_t)tn & 0x7FFFu) | (((uint32_t)~app >> 16) & 0x8000u))
+                                       : ((uint32_t)tn & 0xFFFFu);
+                        }
+                        const bool tgt = full_target || (int)vv[j] < a.target_bits;
+                        const uint32_t hdb = (uint32_t)(app >= 0) & (uint32_t)tgt;
+                        any_hd |= hdb;
+                        if (last) { any_pos |= (uint32_t)(app > 0) & (uint32_t)tgt; nbits += hdb; }
+                    }
+                }
+            }
+        } else {
+        for (int r = 0; r < ((a.ablate & 4) ? 0 : a.nent); ++r) {
             const int e = tid + r * NT;
             if (e < total) {
                 const uint32_t v = (uint32_t)e >> LOGCW;
@@ -301,7 +354,7 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 int app = q_units(ch, inv, qmax) + S;                    // Q(xa) + sum C2V
                 app = min(max(app, -a.clip_u), a.clip_u);                // clip +-clip_LLR
                 if (!last) {
-                    const int tn = q_units(ch * bnext[__umulhi(v, a.zmagic)], inv, qmax) + S;
+                    const int tn = q_scaled(ch * bnext[__umulhi(v, a.zmagic)], (float)qmax) + S;
                     W[e] = ((uint32_t)tn & 0x7FFFu) | ((uint32_t)(app >= 0) << 15);
                 }
                 if ((int)v < a.target_bits) {
@@ -318,6 +371,7 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     atomicOr(reinterpret_cast<unsigned long long*>(a.hd_out + idx), 1ull << (bl >> 2));
                 }
             }
+        }
         }
         unsigned long long bw = __ballot(any_hd);
         unsigned long long m = 0;
@@ -484,6 +538,7 @@ int fused3_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, 
     a.ngroups = p.ngroups;
     a.nent = (g.n_vars * sh.cw + 64 * p.nw - 1) / (64 * p.nw);
     a.zmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.z - 1) / (uint64_t)g.z);
+    if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // timing only
     const int nblocks = (int)((b.B + sh.cw - 1) / sh.cw);
     const float* au = b.alpha_ucn;
     switch (p.shape) {
