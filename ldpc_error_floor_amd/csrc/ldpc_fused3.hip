@@ -69,15 +69,24 @@ struct St3 {
 };
 
 // -1 if bit k of x is set, else 0 (v_bfe_i32)
-__device__ __forceinline__ int bitmask(uint32_t x, int k) { return ((int)(x << (31 - k))) >> 31; }
+
+__device__ __forceinline__ int bfe1(uint32_t x, int k) {           // -1 if bit k set, else 0
+    int r;
+    asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "v"(x), "s"(k));
+    return r;
+}
+__device__ __forceinline__ int bfi(int mask, int a, int b) {         // mask ? a : b (bitwise)
+    int r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
+    return r;
+}
 
 template <bool PEW>
 __device__ __forceinline__ int msg3(const St3& s, int k, float w, float wu, float step, float inv,
                                     int qmax) {
-    const int eq = bitmask(s.oh, k);
-    int m = (eq & s.mB) | (~eq & s.mA);                     // v_bfi
+    int m = bfi(bfe1(s.oh, k), s.mB, s.mA);                 // argmin edge ? mB : mA
     if constexpr (PEW) m = q_mag(m, s.ucn ? wu : w, step, inv, qmax);
-    const int sg = bitmask(s.ns, k);
+    const int sg = bfe1(s.ns, k);
     return (m ^ sg) - sg;                                   // sg ? -m : m
 }
 
@@ -209,49 +218,54 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
             const int deg = (int)(ri >> 16);
             const St3& s = st[gi];
             uint32_t c1 = ((uint32_t)F3_BIG_U << 6) | 63u, c2 = c1;
+            // one chunk of 8 edges; `full` is a literal at each call site, so full chunks carry
+            // no masks, and in the last (partial) chunk slots k >= deg read a duplicate address
+            // and are neutralised with wave-uniform masks — no per-edge branches either way.
+            auto chunk = [&](const int c8, const bool full) __attribute__((always_inline)) {
+                uint32_t wv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int k = c8 + j;
+                    const uint32_t pk = gad[gi][k >> 1];
+                    const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
+                    wv[j] = *reinterpret_cast<const uint32_t*>(smem + addr);
+                }
+                uint32_t kk[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int k = c8 + j;
+                    const bool in = full || k < deg;
+                    const int tv = ((int)(wv[j] << 17)) >> 17;                 // bits 14..0
+                    const int kw = in ? k : 0;
+                    const float w = PEW ? atp[r0 + kw] : 0.f;
+                    const float wu = (PEW && UCN) ? aup[r0 + kw] : 0.f;
+                    const int cold = msg3<PEW>(s, k, w, wu, step, inv, qmax);
+                    const int d = tv - cold;                                   // V->C before Q
+                    const uint32_t mag = (uint32_t)min(max(d, -d), qmax);      // |Q(v2c)|, 0 == +1e-4
+                    kk[j] = (mag << 6) | (uint32_t)k;
+                    if (!full) kk[j] |= in ? 0u : 0xFFFFFFFFu;
+                    NEG[gi] |= ((uint32_t)d >> 31) << k;                      // Q keeps the sign
+                    if (UCN) SYN[gi] ^= (wv[j] >> 15) & (in ? 1u : 0u);
+                }
+                uint32_t lo[4], hi[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { lo[j] = min(kk[2 * j], kk[2 * j + 1]); hi[j] = max(kk[2 * j], kk[2 * j + 1]); }
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const uint32_t a1 = lo[2 * j], a2 = hi[2 * j], b1 = lo[2 * j + 1], b2 = hi[2 * j + 1];
+                    lo[j] = min(a1, b1);
+                    hi[j] = min(max(a1, b1), min(a2, b2));
+                }
+                const uint32_t d1 = min(lo[0], lo[1]);
+                const uint32_t d2 = min(max(lo[0], lo[1]), min(hi[0], hi[1]));
+                const uint32_t o1 = c1, o2 = c2;
+                c1 = min(o1, d1);
+                c2 = min(max(o1, d1), min(o2, d2));
+            };
 #pragma unroll
             for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
-                if (c8 < deg) {
-                    uint32_t wv[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int k = c8 + j;
-                        const uint32_t pk = gad[gi][k >> 1];
-                        const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
-                        wv[j] = *reinterpret_cast<const uint32_t*>(smem + addr);
-                    }
-                    uint32_t kk[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int k = c8 + j;
-                        kk[j] = ((uint32_t)F3_BIG_U << 6) | 63u;
-                        if (k < deg) {
-                            const int tv = ((int)(wv[j] << 17)) >> 17;            // bits 14..0
-                            const float w = PEW ? atp[r0 + k] : 0.f;
-                            const float wu = (PEW && UCN) ? aup[r0 + k] : 0.f;
-                            const int cold = msg3<PEW>(s, k, w, wu, step, inv, qmax);
-                            const int x = med3i(tv - cold, -qmax, qmax);          // Q(v2c)
-                            const uint32_t mag = (uint32_t)max(x, -x);            // 0 == +1e-4
-                            kk[j] = (mag << 6) | (uint32_t)k;
-                            NEG[gi] |= ((uint32_t)x >> 31) << k;
-                            if (UCN) SYN[gi] ^= (wv[j] >> 15) & 1u;
-                        }
-                    }
-                    uint32_t lo[4], hi[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) { lo[j] = min(kk[2 * j], kk[2 * j + 1]); hi[j] = max(kk[2 * j], kk[2 * j + 1]); }
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const uint32_t a1 = lo[2 * j], a2 = hi[2 * j], b1 = lo[2 * j + 1], b2 = hi[2 * j + 1];
-                        lo[j] = min(a1, b1);
-                        hi[j] = min(max(a1, b1), min(a2, b2));
-                    }
-                    const uint32_t d1 = min(lo[0], lo[1]);
-                    const uint32_t d2 = min(max(lo[0], lo[1]), min(hi[0], hi[1]));
-                    const uint32_t o1 = c1, o2 = c2;
-                    c1 = min(o1, d1);
-                    c2 = min(max(o1, d1), min(o2, d2));
-                }
+                if (c8 + 8 <= deg) chunk(c8, true);
+                else if (c8 < deg) chunk(c8, false);
             }
             uint32_t lo[1] = {c1}, hi[1] = {c2};
             K1[gi] = lo[0];
@@ -283,22 +297,26 @@ k_fused3(F3Args a, const float* __restrict__ alpha, const float* __restrict__ al
             }
             if (!gval[gi]) { s.mA = 0; s.mB = 0; }    // duplicate stand-in check: no messages
             if (a.ablate & 2) continue;
+            auto scatter = [&](const int c8, const bool full) __attribute__((always_inline)) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int k = c8 + j;
+                    const bool in = full || k < deg;
+                    const uint32_t pk = gad[gi][k >> 1];
+                    const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
+                    const int kw = in ? k : 0;
+                    const float w = PEW ? at[r0 + kw] : 0.f;
+                    const float wu = (PEW && UCN) ? au[r0 + kw] : 0.f;
+                    const int c = msg3<PEW>(s, k, w, wu, step, inv, qmax);
+                    uint32_t v = (uint32_t)c << 16;
+                    if (!full) v &= in ? 0xFFFFFFFFu : 0u;                    // padding slot adds 0
+                    atomicAdd(reinterpret_cast<uint32_t*>(smem + addr), v);
+                }
+            };
 #pragma unroll
             for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
-                if (c8 < deg) {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int k = c8 + j;
-                        if (k < deg) {
-                            const uint32_t pk = gad[gi][k >> 1];
-                            const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
-                            const float w = PEW ? at[r0 + k] : 0.f;
-                            const float wu = (PEW && UCN) ? au[r0 + k] : 0.f;
-                            const int c = msg3<PEW>(s, k, w, wu, step, inv, qmax);
-                            atomicAdd(reinterpret_cast<uint32_t*>(smem + addr), (uint32_t)c << 16);
-                        }
-                    }
-                }
+                if (c8 + 8 <= deg) scatter(c8, true);
+                else if (c8 < deg) scatter(c8, false);
             }
         }
         __syncthreads();
