@@ -29,6 +29,12 @@ const char* fused3_shape_name(const DevGraph& g, int T);
 int fused3_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, float step,
                   int clip_u, bool per_edge_w, uint64_t* hd_out, int64_t* counters,
                   uint8_t* flags, hipStream_t s);
+// v5 (ldpc_fused5.hip): byte-packed check state, default when a shape fits
+bool fused5_supported(const DevGraph& g, int T);
+const char* fused5_shape_name(const DevGraph& g, int T);
+int fused5_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, float step,
+                  int clip_u, bool per_edge_w, uint64_t* hd_out, int64_t* counters,
+                  uint8_t* flags, hipStream_t s);
 void fused_free(FusedWorkspace& ws);
 
 }  // namespace ldpc

@@ -393,7 +393,7 @@ float mode_step(int mode) {
 
 static int fused_version() {
     const char* e = getenv("LDPC_FUSED_VERSION");
-    return e ? atoi(e) : 3;   // v4 (packed) is opt-in until it beats v3
+    return e ? atoi(e) : 5;   // 5: v5 (fallback v3), 4: v4 packed experiment, 3: v3, 2: v2
 }
 
 static bool fused2_supported(const DevGraph& g, int T);
@@ -403,13 +403,15 @@ static int mode_qmax(int mode) { return (mode == MODE_Q4) ? 7 : (mode == MODE_Q3
 bool fused_supported(const DevGraph& g, int mode, int T) {
     if (mode != MODE_Q5 && mode != MODE_QM5 && mode != MODE_Q4 && mode != MODE_Q3) return false;
     if (g.n_vars >= 32768) return false;
+    if (fused_version() >= 5 && fused5_supported(g, T)) return true;
     if (fused_version() >= 3 && fused3_supported(g, T)) return true;
     return fused2_supported(g, T);
 }
 
 const char* fused_kernel_name(const DevGraph& g, int mode, int T, bool per_edge_w) {
     if (!fused_supported(g, mode, T)) return "";
-    if (fused_version() >= 4 && fused4_supported(g, T, mode_qmax(mode), per_edge_w))
+    if (fused_version() >= 5 && fused5_supported(g, T)) return fused5_shape_name(g, T);
+    if (fused_version() == 4 && fused4_supported(g, T, mode_qmax(mode), per_edge_w))
         return fused4_shape_name(g, T);
     if (fused_version() >= 3 && fused3_supported(g, T)) return fused3_shape_name(g, T);
     return "fused2";
@@ -456,7 +458,10 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
             return LDPC_ERR_HIP;
         hd_out = ws.hd;
     }
-    if (fused_version() >= 4 && fused4_supported(g, b.T, mode_qmax(mode), per_edge_w != 0))
+    if (fused_version() >= 5 && fused5_supported(g, b.T))
+        return fused5_decode(g, b, llr, mode_qmax(mode), step, (int)cu, per_edge_w != 0, hd_out,
+                             counters, flags, s);
+    if (fused_version() == 4 && fused4_supported(g, b.T, mode_qmax(mode), per_edge_w != 0))
         return fused4_decode(g, b, llr, mode_qmax(mode), step, (int)cu, hd_out, counters, flags, s);
     if (fused_version() >= 3 && fused3_supported(g, b.T)) {
         const int qmax = mode_qmax(mode);

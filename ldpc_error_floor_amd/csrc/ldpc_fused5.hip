@@ -1,0 +1,590 @@
+// ldpc_fused5.hip — fused QMS decoder, v5: byte-packed check state, 2-op message decode.
+//
+// Same semantics and work mapping as v3 (ldpc_fused3.hip: one workgroup owns CW codewords for
+// all T iterations, lane = slot*CW + cw, a wave's slots take consecutive checks of one proto
+// row, per-edge LDS addresses precomputed and packed 2x16 bit).  What changes is how a check's
+// compressed min-sum state is held and decoded, which sets the VALU count per edge:
+//
+//  * P   — one VGPR holding the check's four possible output messages as signed bytes
+//          [+mA, -mA, +mB, -mB] (mA: min over all edges, mB: second minimum, both already
+//          weighted and quantized, in grid units);
+//  * SEL — 5-bit fields, six edges per VGPR: field = 8*negative + 16*is_argmin, i.e. the bit
+//          offset of the edge's message inside P.  Decoding a message is
+//          v_bfe_i32(P, SEL >> 5*pos, 8): 2 ops (v3: 5).
+//  * pass 1 folds V->C magnitudes with one v_min + one v_med3 per edge (running first/second
+//    minimum of key = |v2c| << 8 | edge code), and the V->C signs with one v_alignbit per
+//    edge, which appends the top 5 bits of v2c (= 5 copies of its sign) to a SEL-shaped word;
+//    the quantizer clamp moves after the minimum (clamp is monotonic);
+//  * W[v][cw] = Tv (bits 31..16, signed) | hd (bit 15) | S + 2^14 (bits 14..0): pass 1 reads Tv
+//    with an SDWA sign-extended word select, pass 2 adds the message without a shift;
+//  * an edge slot past a check's degree points at a per-codeword dummy word whose Tv is
+//    +16383: its |v2c| never wins a minimum, its sign is positive, its hd bit is 0, and pass 2
+//    adds into it harmlessly (the VN phase resets it), so partial chunks need no masks.
+//
+// Per-edge weights (sharing types with one weight per edge) keep raw minima in P (16 bit
+// each) and quantize per edge at decode; this path is correct but not tuned.
+#include <cstdio>
+#include <cstdlib>
+
+#include "ldpc_fused.h"
+
+namespace ldpc {
+
+namespace {
+
+constexpr int F5_BIG_U = 1023;               // "no other edge": value 10000 (Main_Functions.py:248)
+constexpr size_t F5_LDS_MAX = 160 * 1024;
+constexpr uint32_t F5_SBIAS = 16384;         // S field bias (bits 14..0)
+constexpr uint32_t F5_DUMMY_W = (16383u << 16) | F5_SBIAS;
+
+struct F5Args {
+    const float* llr;
+    const float* beta;
+    float* app_out;
+    uint64_t* hd_out;
+    int64_t* counters;
+    uint8_t* flags;
+    const int32_t* row_ptr;
+    const int32_t* pe_col;
+    const int32_t* pe_shift;
+    int64_t B;
+    int ntiles, T, target_bits, clip_u, qmax;
+    float inv, step;
+    int n_vars, N, E, z;
+    int hstep, ngroups, nent;
+    uint32_t zmagic;
+    int ablate;        // diagnostic only (LDPC_DIAG_ABLATE): 1 skip CN pass 1, 2 skip pass 2, 4 skip VN
+};
+
+__device__ __forceinline__ int q_units5(float x, float inv, int qmax) {
+    return (int)__builtin_amdgcn_fmed3f(rintf(x * inv), -(float)qmax, (float)qmax);
+}
+// Q(x) in grid units when x is already scaled by the (power-of-two) inverse step
+__device__ __forceinline__ int q_scaled5(float xs, float qm) {
+    return (int)__builtin_amdgcn_fmed3f(rintf(xs), -qm, qm);
+}
+// quantized C->V magnitude: Q(relu(|o| * w)), |o| in grid units (>= F5_BIG_U: the 10000 rule)
+__device__ __forceinline__ int q_mag5(int m, float w, float step, float inv, int qmax) {
+    const float mv = (m >= F5_BIG_U) ? 10000.0f : (float)m * step;
+    float x = mv * w;                          // fl32(|o| * w)
+    x = (x > 0.f) ? x : 0.f;                   // x * [x > 0]
+    return q_units5(x, inv, qmax);
+}
+
+__device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ int clampi(int x, int lo, int hi) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "s"(hi));
+    return r;
+}
+
+// ---- SEL layout: edge k -> word k/6, field position counted from the last inserted edge -----
+template <int MAXDEG>
+struct Sel {
+    static constexpr int NSEL = (MAXDEG + 5) / 6;
+    static constexpr int nins(int w) { return (MAXDEG - 6 * w) < 6 ? (MAXDEG - 6 * w) : 6; }
+    static constexpr int pos(int k) { return nins(k / 6) - 1 - (k % 6); }
+    static constexpr int shift(int k) { return 5 * pos(k); }
+    static constexpr uint32_t code(int k) { return ((uint32_t)(k / 6) << 5) | (uint32_t)(5 * pos(k) + 4); }
+    static constexpr uint32_t f3mask(int w) {
+        uint32_t m = 0;
+        for (int i = 0; i < nins(w); ++i) m |= 8u << (5 * i);
+        return m;
+    }
+    // number of edges of word w inside chunk [c8, c8+8)
+    static constexpr int in_chunk(int w, int c8) {
+        int n = 0;
+        for (int k = c8; k < c8 + 8 && k < MAXDEG; ++k) n += (k / 6 == w);
+        return n;
+    }
+};
+
+template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW>
+__global__ void __launch_bounds__(1024)
+k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ alpha_ucn) {
+    using SL = Sel<MAXDEG>;
+    constexpr int NSEL = SL::NSEL;
+    constexpr int SLOTS = 64 / CW;
+    constexpr int LOGCW = (CW == 64) ? 6 : (CW == 32) ? 5 : (CW == 16) ? 4 : 3;
+    constexpr int NPK = (MAXDEG + 1) / 2;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int nv = a.n_vars;
+    const int total = nv * CW;
+    uint32_t* W = reinterpret_cast<uint32_t*>(smem);                              // [nv*CW + CW]
+    float* CH = reinterpret_cast<float*>(smem + ((size_t)total + CW) * 4);        // [nv*CW]
+    float* BETA = CH + total;                                                     // [T*N]
+    unsigned long long* RED = reinterpret_cast<unsigned long long*>(
+        smem + ((((size_t)total + CW) * 4 + (size_t)total * 4 + (size_t)a.T * a.N * 4 + 15) & ~(size_t)15));
+
+    const int tid = threadIdx.x;
+    const int NT = blockDim.x;
+    const int NWV = NT >> 6;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int slot = lane >> LOGCW;
+    const int cw = lane & (CW - 1);
+    const int64_t b0 = (int64_t)blockIdx.x * CW;
+    const int64_t nvalid = (b0 + CW <= a.B) ? CW : (a.B - b0);
+    const unsigned long long cwmask = (CW == 64) ? ~0ull : ((1ull << CW) - 1);
+    const unsigned long long valid_cw = (nvalid >= 64) ? ~0ull : ((1ull << nvalid) - 1);
+    const int qmax = a.qmax;
+    const float inv = a.inv, step = a.step;
+    const int z = a.z;
+
+    // ---- prologue: coalesced LLR block -> padded scratch -> CH[v][cw]; beta; W = Tv_0 | hd ----
+    {
+        float* scr = reinterpret_cast<float*>(W);            // [CW][nv+1]
+        const int rl = nv + 1;
+        for (int v0 = 0; v0 < nv; v0 += NT) {
+            const int v = v0 + tid;
+            float x[CW];
+#pragma unroll
+            for (int r = 0; r < CW; ++r)
+                x[r] = (v < nv && r < nvalid) ? a.llr[(b0 + r) * nv + v] : 0.f;
+#pragma unroll
+            for (int r = 0; r < CW; ++r)
+                if (v < nv) scr[r * rl + v] = x[r];
+        }
+        // beta pre-multiplied by 1/step (a power of two): fl32(ch*beta)/step == fl32(ch*(beta/step))
+        for (int f = tid; f < a.T * a.N; f += NT) BETA[f] = a.beta[f] * inv;
+        if (tid < 8) RED[tid] = (tid == 1) ? ~0ull : 0ull;
+        __syncthreads();
+        for (int e = tid; e < total; e += NT) CH[e] = scr[(e & (CW - 1)) * rl + (e >> LOGCW)];
+        __syncthreads();
+        for (int e = tid; e < total; e += NT) {
+            const uint32_t v = (uint32_t)e >> LOGCW;
+            const int t0 = q_scaled5(CH[e] * BETA[__umulhi(v, a.zmagic)], (float)qmax);  // lw_0
+            W[e] = ((uint32_t)t0 << 16) | ((uint32_t)(t0 >= 0) << 15) | F5_SBIAS;     // hd_{-1}
+        }
+        if (tid < CW) W[total + tid] = F5_DUMMY_W;
+    }
+
+    // ---- per-group edge addresses (bytes, 16-bit packed), row info, lane validity ----------
+    uint32_t gad[MAXG][NPK];
+    uint32_t grow[MAXG];
+    bool gval[MAXG];
+    const uint32_t dummy_byte = (uint32_t)(total + cw) * 4u;
+#pragma unroll
+    for (int gi = 0; gi < MAXG; ++gi) {
+        grow[gi] = 0;
+        gval[gi] = false;
+#pragma unroll
+        for (int p = 0; p < NPK; ++p) gad[gi][p] = 0;
+        const int grp = wave + gi * NWV;
+        if (grp < a.ngroups) {
+            const int i = grp / a.hstep;
+            const int hg = grp - i * a.hstep;
+            const int r0 = a.row_ptr[i];
+            const int deg = a.row_ptr[i + 1] - r0;
+            const int h = hg * SLOTS + slot;
+            gval[gi] = h < z;
+            const int hl = (h < z) ? h : hg * SLOTS;
+            grow[gi] = (uint32_t)r0 | ((uint32_t)deg << 16);
+#pragma unroll
+            for (int k = 0; k < MAXDEG; ++k) {
+                uint32_t byte = dummy_byte;
+                if (k < deg) {
+                    int hs = hl + a.pe_shift[r0 + k];
+                    hs = (hs >= z) ? hs - z : hs;
+                    byte = (uint32_t)(((a.pe_col[r0 + k] * z + hs) << LOGCW) + cw) * 4u;
+                }
+                gad[gi][k >> 1] |= (k & 1) ? (byte << 16) : byte;
+            }
+        }
+    }
+    __syncthreads();
+
+    // check state: P (messages / raw minima), SEL (per-edge fields), ucn (syndrome, PEW only)
+    uint32_t P[MAXG], SEL[MAXG][NSEL];
+    int UC[MAXG];
+#pragma unroll
+    for (int gi = 0; gi < MAXG; ++gi) {
+        P[gi] = 0;
+        UC[gi] = 0;
+#pragma unroll
+        for (int w = 0; w < NSEL; ++w) SEL[gi][w] = 0;
+    }
+
+    // C->V message of edge k from a check's state
+    auto msg = [&](const int gi, const int k, const float* wt, const float* wtu, const int r0)
+        __attribute__((always_inline)) -> int {
+        const uint32_t f = SEL[gi][k / 6] >> SL::shift(k);
+        if constexpr (!PEW) {
+            return __builtin_amdgcn_sbfe((int)P[gi], f, 8);
+        } else {
+            const int m = (int)((f & 16u) ? (P[gi] >> 16) : (P[gi] & 0xFFFFu));
+            const float w = (UCN && UC[gi]) ? wtu[r0 + k] : wt[r0 + k];
+            const int mq = q_mag5(m, w, step, inv, qmax);
+            return (f & 8u) ? -mq : mq;
+        }
+    };
+
+    for (int t = 0; t < a.T; ++t) {
+        if (tid == 0 && t > 0) {        // fold iteration t-1's frame flags (its VN phase is done)
+            RED[1] &= RED[0];
+            RED[0] = 0;
+        }
+        const float* at = alpha + (size_t)t * a.E;
+        const float* au = UCN ? alpha_ucn + (size_t)t * a.E : nullptr;
+        const float* atp = alpha + (size_t)(t > 0 ? t - 1 : 0) * a.E;
+        const float* aup = UCN ? alpha_ucn + (size_t)(t > 0 ? t - 1 : 0) * a.E : nullptr;
+        // ======== check nodes: pass 1 (read Tv, fold minima and signs) + new state ==========
+#pragma unroll
+        for (int gi = 0; gi < MAXG; ++gi) {
+            const int grp = wave + gi * NWV;
+            if (grp >= a.ngroups) break;
+            if (a.ablate & 1) continue;
+            const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
+            const int r0 = (int)(ri & 0xFFFFu);
+            const int deg = (int)(ri >> 16);
+            uint32_t c1 = 0xFFFFFFFFu, c2 = 0xFFFFFFFFu;
+            uint32_t NG[NSEL];
+#pragma unroll
+            for (int w = 0; w < NSEL; ++w) NG[w] = 0;
+            uint32_t syn = 0;
+#pragma unroll
+            for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
+                if (c8 < deg) {
+                    uint32_t wv[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int k = c8 + j;
+                        if (k < MAXDEG) {
+                            const uint32_t pk = gad[gi][k >> 1];
+                            const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
+                            wv[j] = *reinterpret_cast<const uint32_t*>(smem + addr);
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int k = c8 + j;
+                        if (k < MAXDEG) {
+                            const int cold = msg(gi, k, atp, aup, r0);
+                            const int d = (int)(short)(wv[j] >> 16) - cold;      // V->C before Q
+                            const uint32_t key = ((uint32_t)max(d, -d) << 8) | SL::code(k);
+                            NG[k / 6] = __builtin_amdgcn_alignbit(NG[k / 6], (uint32_t)d, 27);
+                            const uint32_t o1 = c1;
+                            c1 = min(o1, key);
+                            c2 = med3u(o1, c2, key);
+                            if (UCN) syn ^= (wv[j] >> 15) & 1u;
+                        }
+                    }
+                } else {
+                    // chunk skipped (deg <= c8): its edges enter as positive (zero) sign fields
+#pragma unroll
+                    for (int w = 0; w < NSEL; ++w) {
+                        const int n = SL::in_chunk(w, c8);
+                        if (n > 0) NG[w] <<= 5 * n;
+                    }
+                }
+            }
+            // ---- new state: quantized minima, sign fields, argmin field ----
+            int m1 = min((int)(c1 >> 8), qmax);
+            int m2 = (deg < 2) ? F5_BIG_U : min((int)(c2 >> 8), qmax);
+            uint32_t nneg = 0;
+#pragma unroll
+            for (int w = 0; w < NSEL; ++w) {
+                NG[w] &= SL::f3mask(w);
+                nneg += __popc(NG[w]);
+            }
+            // message sign: negative iff the V->C sign is negative XOR (count of positives odd)
+            const uint32_t pm = ((uint32_t)(deg - (int)nneg) & 1u) ? 0xFFFFFFFFu : 0u;
+            const uint32_t code = c1 & 255u;
+            const uint32_t onebit = 1u << (code & 31u);
+            const uint32_t wsel = code >> 5;
+#pragma unroll
+            for (int w = 0; w < NSEL; ++w)
+                SEL[gi][w] = (NG[w] ^ (pm & SL::f3mask(w))) | ((wsel == (uint32_t)w) ? onebit : 0u);
+            if constexpr (PEW) {
+                UC[gi] = (int)syn;
+                P[gi] = gval[gi] ? ((uint32_t)m1 | ((uint32_t)m2 << 16)) : 0u;
+            } else {
+                const float w = (UCN && syn) ? au[r0] : at[r0];
+                const int mA = q_mag5(m1, w, step, inv, qmax);
+                const int mB = q_mag5(m2, w, step, inv, qmax);
+                const uint32_t pa = ((uint32_t)mA & 0xFFu) | (((uint32_t)(-mA) & 0xFFu) << 8);
+                const uint32_t pb = ((uint32_t)mB & 0xFFu) | (((uint32_t)(-mB) & 0xFFu) << 8);
+                P[gi] = gval[gi] ? (pa | (pb << 16)) : 0u;    // duplicate stand-in check: no messages
+            }
+        }
+        // ======== check nodes: pass 2 (scatter C->V into S) =================================
+#pragma unroll
+        for (int gi = 0; gi < MAXG; ++gi) {
+            const int grp = wave + gi * NWV;
+            if (grp >= a.ngroups) break;
+            if (a.ablate & 2) continue;
+            const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
+            const int r0 = (int)(ri & 0xFFFFu);
+            const int deg = (int)(ri >> 16);
+#pragma unroll
+            for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
+                if (c8 < deg) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int k = c8 + j;
+                        if (k < MAXDEG) {
+                            const uint32_t pk = gad[gi][k >> 1];
+                            const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
+                            const int c = msg(gi, k, at, au, r0);
+                            atomicAdd(reinterpret_cast<uint32_t*>(smem + addr), (uint32_t)c);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // ======== variable nodes ===========================================================
+        const bool last = (t == a.T - 1);
+        const float* bnext = BETA + (size_t)(last ? t : t + 1) * a.N;
+        uint32_t any_hd = 0, any_pos = 0, nbits = 0;
+        const float qmf = (float)qmax;
+        const bool full_target = a.target_bits >= nv;
+        const int sb = -(int)F5_SBIAS;
+        if (tid < CW) W[total + tid] = F5_DUMMY_W;    // pass-2 adds of padding edges
+        if (a.app_out == nullptr && a.hd_out == nullptr) {
+            // fast path: 4 entries' LDS reads in flight before any is consumed
+            for (int r0 = 0; r0 < ((a.ablate & 4) ? 0 : a.nent); r0 += 4) {
+                uint32_t wv[4], vv[4];
+                float chv[4], bv[4];
+                bool in[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int e = tid + (r0 + j) * NT;
+                    in[j] = e < total;
+                    const int ee = in[j] ? e : tid;
+                    vv[j] = (uint32_t)ee >> LOGCW;
+                    wv[j] = W[ee];
+                    chv[j] = CH[ee];
+                    bv[j] = bnext[__umulhi(vv[j], a.zmagic)];
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int e = tid + (r0 + j) * NT;
+                    const int S = (int)(wv[j] & 0x7FFFu) + sb;
+                    int app = q_scaled5(chv[j] * inv, qmf) + S;               // Q(xa) + sum C2V
+                    app = clampi(app, -a.clip_u, a.clip_u);                   // clip +-clip_LLR
+                    if (in[j]) {
+                        if (!last) {
+                            const int tn = q_scaled5(chv[j] * bv[j], qmf) + S;
+                            W[e] = UCN ? (((uint32_t)tn << 16) | (((uint32_t)~app >> 16) & 0x8000u) | F5_SBIAS)
+                                       : (((uint32_t)tn << 16) | F5_SBIAS);
+                        }
+                        const bool tgt = full_target || (int)vv[j] < a.target_bits;
+                        const uint32_t hdb = (uint32_t)(app >= 0) & (uint32_t)tgt;
+                        any_hd |= hdb;
+                        if (last) { any_pos |= (uint32_t)(app > 0) & (uint32_t)tgt; nbits += hdb; }
+                    }
+                }
+            }
+        } else {
+        for (int r = 0; r < ((a.ablate & 4) ? 0 : a.nent); ++r) {
+            const int e = tid + r * NT;
+            if (e < total) {
+                const uint32_t v = (uint32_t)e >> LOGCW;
+                const uint32_t wv = W[e];
+                const int S = (int)(wv & 0x7FFFu) + sb;
+                const float ch = CH[e];
+                int app = q_units5(ch, inv, qmax) + S;                   // Q(xa) + sum C2V
+                app = min(max(app, -a.clip_u), a.clip_u);                // clip +-clip_LLR
+                if (!last) {
+                    const int tn = q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], (float)qmax) + S;
+                    W[e] = ((uint32_t)tn << 16) | ((uint32_t)(app >= 0) << 15) | F5_SBIAS;
+                }
+                if ((int)v < a.target_bits) {
+                    any_hd |= (uint32_t)(app >= 0);
+                    if (last) { any_pos |= (uint32_t)(app > 0); nbits += (uint32_t)(app >= 0); }
+                    if (a.app_out && cw < nvalid)
+                        a.app_out[((size_t)t * a.B + b0 + cw) * a.target_bits + v] = (float)app * step;
+                }
+                if (a.hd_out && app >= 0 && cw < nvalid) {
+                    const int64_t b = b0 + cw;
+                    const int64_t tile = b / TILE;
+                    const int bl = (int)(b - tile * TILE);
+                    const size_t idx = ((((size_t)(t + 1) * a.ntiles + tile) * nv + v) * 4) + (bl & 3);
+                    atomicOr(reinterpret_cast<unsigned long long*>(a.hd_out + idx), 1ull << (bl >> 2));
+                }
+            }
+        }
+        }
+        unsigned long long bw = __ballot(any_hd);
+        unsigned long long m = 0;
+#pragma unroll
+        for (int s2 = 0; s2 < SLOTS; ++s2) m |= (bw >> (s2 * CW)) & cwmask;
+        if (lane == 0 && m) atomicOr(&RED[0], m);
+        if (last) {
+            bw = __ballot(any_pos);
+            m = 0;
+#pragma unroll
+            for (int s2 = 0; s2 < SLOTS; ++s2) m |= (bw >> (s2 * CW)) & cwmask;
+            if (lane == 0 && m) atomicOr(&RED[2], m);
+            uint32_t nb = (cw < nvalid) ? nbits : 0u;
+            for (int off = 32; off > 0; off >>= 1) nb += __shfl_xor(nb, off);
+            if (lane == 0 && nb) atomicAdd(&RED[3], (unsigned long long)nb);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const unsigned long long wl = RED[0] & valid_cw;
+        const unsigned long long all = RED[1] & RED[0] & valid_cw;
+        const unsigned long long ap = RED[2] & valid_cw;
+        if (a.counters) {
+            const unsigned long long c0 = RED[3];
+            const unsigned long long c1 = __popcll(wl);
+            const unsigned long long c2 = __popcll(all);
+            const unsigned long long c3 = 2ull * __popcll(ap) + __popcll(wl & ~ap);
+            unsigned long long* cc = reinterpret_cast<unsigned long long*>(a.counters);
+            if (c0) atomicAdd(cc + 0, c0);
+            if (c1) atomicAdd(cc + 1, c1);
+            if (c2) atomicAdd(cc + 2, c2);
+            if (c3) atomicAdd(cc + 3, c3);
+        }
+        RED[5] = all;
+        RED[6] = wl;
+    }
+    if (a.flags) {
+        __syncthreads();
+        if (tid < nvalid)
+            a.flags[b0 + tid] = (uint8_t)(((RED[5] >> tid) & 1) | (((RED[6] >> tid) & 1) << 1));
+    }
+}
+
+// ---- shapes ------------------------------------------------------------------------------
+struct Shape5 {
+    int cw, maxg, maxdeg;
+};
+constexpr Shape5 kShapes5[] = {
+    {16, 3, 16},   // wman-like (z=24, deg 14-15)
+    {16, 3, 24},   // 802.11n-like (deg 22)
+    {8, 5, 16},    // 5G BG2-like (z=64, deg <= 10)
+    {64, 3, 8},    // z=1 sparse (MacKay)
+    {64, 2, 32},   // z=1 dense rows (BCH)
+};
+
+size_t f5_lds(int nv, int cw, int T, int N) {
+    return ((((size_t)nv * cw + cw) * 4 + (size_t)nv * cw * 4 + (size_t)T * N * 4 + 15) & ~(size_t)15) + 8 * 8;
+}
+
+struct Plan5 {
+    int shape = -1, nw = 0, hstep = 0, ngroups = 0;
+    size_t lds = 0;
+};
+
+Plan5 plan5(const DevGraph& g, int T) {
+    Plan5 best;
+    double best_score = 0;
+    for (int si = 0; si < (int)(sizeof(kShapes5) / sizeof(kShapes5[0])); ++si) {
+        const Shape5& sh = kShapes5[si];
+        if ((g.z == 1) != (sh.cw == 64)) continue;
+        if (g.max_cdeg > sh.maxdeg) continue;
+        const int slots = 64 / sh.cw;
+        const int hstep = (g.z + slots - 1) / slots;
+        const int ngroups = g.M * hstep;
+        const int nw = (ngroups + sh.maxg - 1) / sh.maxg;
+        if (nw > 16 || nw < 1) continue;
+        const size_t lds = f5_lds(g.n_vars, sh.cw, T, g.N);
+        if (lds > F5_LDS_MAX) continue;
+        if ((size_t)g.n_vars * sh.cw * 4 + sh.cw * 4 >= 65536) continue;    // 16-bit addresses
+        const int wg_lds = (int)(F5_LDS_MAX / lds);
+        const int wg_waves = 32 / nw;
+        const int wgs = std::max(1, std::min(wg_lds, wg_waves));
+        const double eff = (double)g.max_cdeg / (double)(((g.max_cdeg + 7) / 8) * 8);
+        const double score = (double)(wgs * nw) * eff + 1e-3 * sh.cw;
+        if (score > best_score) {
+            best_score = score;
+            best.shape = si;
+            best.nw = nw;
+            best.hstep = hstep;
+            best.ngroups = ngroups;
+            best.lds = lds;
+        }
+    }
+    return best;
+}
+
+template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW>
+int launch5k(const F5Args& a, int nblocks, int nw, size_t lds, const float* alpha,
+             const float* alpha_ucn, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused5<CW, MAXG, MAXDEG, UCN, PEW>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)F5_LDS_MAX);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_fused5<CW, MAXG, MAXDEG, UCN, PEW>), dim3(nblocks), dim3(64 * nw), lds, s,
+                       a, alpha, alpha_ucn);
+    return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+}
+
+template <int CW, int MAXG, int MAXDEG>
+int launch5s(const F5Args& a, int nblocks, int nw, size_t lds, const float* alpha,
+             const float* alpha_ucn, bool pew, hipStream_t s) {
+    if (alpha_ucn)
+        return pew ? launch5k<CW, MAXG, MAXDEG, true, true>(a, nblocks, nw, lds, alpha, alpha_ucn, s)
+                   : launch5k<CW, MAXG, MAXDEG, true, false>(a, nblocks, nw, lds, alpha, alpha_ucn, s);
+    return pew ? launch5k<CW, MAXG, MAXDEG, false, true>(a, nblocks, nw, lds, alpha, nullptr, s)
+               : launch5k<CW, MAXG, MAXDEG, false, false>(a, nblocks, nw, lds, alpha, nullptr, s);
+}
+
+}  // namespace
+
+bool fused5_supported(const DevGraph& g, int T) { return plan5(g, T).shape >= 0; }
+
+const char* fused5_shape_name(const DevGraph& g, int T) {
+    static thread_local char buf[64];
+    const Plan5 p = plan5(g, T);
+    if (p.shape < 0) return "";
+    const Shape5& sh = kShapes5[p.shape];
+    snprintf(buf, sizeof(buf), "fused5[cw%d,g%d,d%d,w%d]", sh.cw, sh.maxg, sh.maxdeg, p.nw);
+    return buf;
+}
+
+int fused5_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, float step,
+                  int clip_u, bool per_edge_w, uint64_t* hd_out, int64_t* counters,
+                  uint8_t* flags, hipStream_t s) {
+    const Plan5 p = plan5(g, b.T);
+    if (p.shape < 0) return LDPC_ERR_UNSUPPORTED;
+    const Shape5& sh = kShapes5[p.shape];
+    F5Args a{};
+    a.llr = llr;
+    a.beta = b.beta;
+    a.app_out = b.app_out;
+    a.hd_out = hd_out;
+    a.counters = counters;
+    a.flags = flags;
+    a.row_ptr = g.row_ptr;
+    a.pe_col = g.pe_col;
+    a.pe_shift = g.pe_shift;
+    a.B = b.B;
+    a.ntiles = b.ntiles;
+    a.T = b.T;
+    a.target_bits = b.target_bits;
+    a.clip_u = clip_u;
+    a.qmax = qmax;
+    a.step = step;
+    a.inv = 1.0f / step;
+    a.n_vars = g.n_vars;
+    a.N = g.N;
+    a.E = g.E;
+    a.z = g.z;
+    a.hstep = p.hstep;
+    a.ngroups = p.ngroups;
+    a.nent = (g.n_vars * sh.cw + 64 * p.nw - 1) / (64 * p.nw);
+    a.zmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.z - 1) / (uint64_t)g.z);
+    if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // timing only
+    const int nblocks = (int)((b.B + sh.cw - 1) / sh.cw);
+    const float* au = b.alpha_ucn;
+    switch (p.shape) {
+        case 0: return launch5s<16, 3, 16>(a, nblocks, p.nw, p.lds, b.alpha, au, per_edge_w, s);
+        case 1: return launch5s<16, 3, 24>(a, nblocks, p.nw, p.lds, b.alpha, au, per_edge_w, s);
+        case 2: return launch5s<8, 5, 16>(a, nblocks, p.nw, p.lds, b.alpha, au, per_edge_w, s);
+        case 3: return launch5s<64, 3, 8>(a, nblocks, p.nw, p.lds, b.alpha, au, per_edge_w, s);
+        case 4: return launch5s<64, 2, 32>(a, nblocks, p.nw, p.lds, b.alpha, au, per_edge_w, s);
+        default: return LDPC_ERR_UNSUPPORTED;
+    }
+}
+
+}  // namespace ldpc
