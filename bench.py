@@ -163,7 +163,8 @@ def main():
     bytes_cw = survey_bytes_per_cw(g.E, g.N, 24, T)
     achieved = bytes_cw * B / (primary["kernel_ms"] / 1e3) / 1e9
     traffic = None
-    tf = os.path.join(ROOT, "profiles", f"traffic_{primary['name']}.json")
+    safe = "".join(ch if (ch.isalnum() or ch in "_.-") else "_" for ch in primary["name"])
+    tf = os.path.join(ROOT, "profiles", f"traffic_{safe}.json")
     if os.path.exists(tf):
         try:
             with open(tf) as f:

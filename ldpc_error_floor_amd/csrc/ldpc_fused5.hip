@@ -23,6 +23,8 @@
 //
 // Per-edge weights (sharing types with one weight per edge) keep raw minima in P (16 bit
 // each) and quantize per edge at decode; this path is correct but not tuned.
+#include <climits>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 
@@ -52,6 +54,8 @@ struct F5Args {
     float inv, step;
     int n_vars, N, E, z;
     int hstep, ngroups, nent;
+    int nfull, cpw;    // VN: full 64-entry chunks, chunks per wave
+    int Mp;            // proto rows
     uint32_t zmagic;
     int ablate;        // diagnostic only (LDPC_DIAG_ABLATE): 1 skip CN pass 1, 2 skip pass 2, 4 skip VN
 };
@@ -103,7 +107,7 @@ struct Sel {
     }
 };
 
-template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW>
+template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW, bool OUT, bool LUT>
 __global__ void __launch_bounds__(1024)
 k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ alpha_ucn) {
     using SL = Sel<MAXDEG>;
@@ -119,6 +123,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     float* BETA = CH + total;                                                     // [T*N]
     unsigned long long* RED = reinterpret_cast<unsigned long long*>(
         smem + ((((size_t)total + CW) * 4 + (size_t)total * 4 + (size_t)a.T * a.N * 4 + 15) & ~(size_t)15));
+    uint16_t* QT = reinterpret_cast<uint16_t*>(RED + 8);                          // [T][Mp][qmax+2]
 
     const int tid = threadIdx.x;
     const int NT = blockDim.x;
@@ -152,6 +157,19 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         // beta pre-multiplied by 1/step (a power of two): fl32(ch*beta)/step == fl32(ch*(beta/step))
         for (int f = tid; f < a.T * a.N; f += NT) BETA[f] = a.beta[f] * inv;
         if (tid < 8) RED[tid] = (tid == 1) ? ~0ull : 0ull;
+        if constexpr (LUT) {
+            // QT[t][row][m] = [+q, -q] bytes, q = Q(relu(|o| * alpha_t,row)), |o| = m grid units
+            // (m = qmax+1 stands for "no other edge", the 10000 value)
+            const int nq = qmax + 2;
+            for (int f = tid; f < a.T * a.Mp * nq; f += NT) {
+                const int m = f % nq;
+                const int tr = f / nq;
+                const int tt = tr / a.Mp, row = tr - tt * a.Mp;
+                const float w = alpha[(size_t)tt * a.E + a.row_ptr[row]];
+                const int q = q_mag5(m > qmax ? F5_BIG_U : m, w, step, inv, qmax);
+                QT[f] = (uint16_t)(((uint32_t)q & 0xFFu) | (((uint32_t)(-q) & 0xFFu) << 8));
+            }
+        }
         __syncthreads();
         for (int e = tid; e < total; e += NT) CH[e] = scr[(e & (CW - 1)) * rl + (e >> LOGCW)];
         __syncthreads();
@@ -183,7 +201,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             const int h = hg * SLOTS + slot;
             gval[gi] = h < z;
             const int hl = (h < z) ? h : hg * SLOTS;
-            grow[gi] = (uint32_t)r0 | ((uint32_t)deg << 16);
+            grow[gi] = (uint32_t)r0 | ((uint32_t)deg << 16) | ((uint32_t)i << 24);
 #pragma unroll
             for (int k = 0; k < MAXDEG; ++k) {
                 uint32_t byte = dummy_byte;
@@ -240,7 +258,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             if (a.ablate & 1) continue;
             const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
             const int r0 = (int)(ri & 0xFFFFu);
-            const int deg = (int)(ri >> 16);
+            const int deg = (int)((ri >> 16) & 0xFFu);
             uint32_t c1 = 0xFFFFFFFFu, c2 = 0xFFFFFFFFu;
             uint32_t NG[NSEL];
 #pragma unroll
@@ -283,32 +301,44 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 }
             }
             // ---- new state: quantized minima, sign fields, argmin field ----
-            int m1 = min((int)(c1 >> 8), qmax);
-            int m2 = (deg < 2) ? F5_BIG_U : min((int)(c2 >> 8), qmax);
-            uint32_t nneg = 0;
+            // parity of the negative V->C signs: every sign field holds 5 copies of its sign
+            uint32_t nbit = 0;
 #pragma unroll
-            for (int w = 0; w < NSEL; ++w) {
-                NG[w] &= SL::f3mask(w);
-                nneg += __popc(NG[w]);
-            }
-            // message sign: negative iff the V->C sign is negative XOR (count of positives odd)
-            const uint32_t pm = ((uint32_t)(deg - (int)nneg) & 1u) ? 0xFFFFFFFFu : 0u;
+            for (int w = 0; w < NSEL; ++w) nbit += __popc(NG[w]);
+            // message sign = V->C sign XOR (count of positives odd); the XOR is applied to P
+            // (byte swap inside each half) for byte-packed P, to the fields for PEW
+            const bool podd = ((uint32_t)deg + nbit) & 1u;
             const uint32_t code = c1 & 255u;
             const uint32_t onebit = 1u << (code & 31u);
             const uint32_t wsel = code >> 5;
+            const uint32_t pm = (PEW && podd) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
             for (int w = 0; w < NSEL; ++w)
-                SEL[gi][w] = (NG[w] ^ (pm & SL::f3mask(w))) | ((wsel == (uint32_t)w) ? onebit : 0u);
+                SEL[gi][w] = ((NG[w] ^ pm) & SL::f3mask(w)) | ((wsel == (uint32_t)w) ? onebit : 0u);
+            const int m1 = min((int)(c1 >> 8), qmax);
             if constexpr (PEW) {
+                const int m2 = (deg < 2) ? F5_BIG_U : min((int)(c2 >> 8), qmax);
                 UC[gi] = (int)syn;
                 P[gi] = gval[gi] ? ((uint32_t)m1 | ((uint32_t)m2 << 16)) : 0u;
             } else {
-                const float w = (UCN && syn) ? au[r0] : at[r0];
-                const int mA = q_mag5(m1, w, step, inv, qmax);
-                const int mB = q_mag5(m2, w, step, inv, qmax);
-                const uint32_t pa = ((uint32_t)mA & 0xFFu) | (((uint32_t)(-mA) & 0xFFu) << 8);
-                const uint32_t pb = ((uint32_t)mB & 0xFFu) | (((uint32_t)(-mB) & 0xFFu) << 8);
-                P[gi] = gval[gi] ? (pa | (pb << 16)) : 0u;    // duplicate stand-in check: no messages
+                uint32_t p;
+                if constexpr (LUT) {
+                    // [+m, -m] byte pairs of Q(relu(m*w)) for this iteration and proto row
+                    const int ib = (deg < 2) ? qmax + 1 : min((int)(c2 >> 8), qmax);
+                    const int row = (int)((ri >> 24) & 0xFFu);
+                    const uint16_t* qt = QT + (t * a.Mp + row) * (qmax + 2);
+                    p = (uint32_t)qt[m1] | ((uint32_t)qt[ib] << 16);
+                } else {
+                    const int m2 = (deg < 2) ? F5_BIG_U : min((int)(c2 >> 8), qmax);
+                    const float w = (UCN && syn) ? au[r0] : at[r0];
+                    const int mA = q_mag5(m1, w, step, inv, qmax);
+                    const int mB = q_mag5(m2, w, step, inv, qmax);
+                    const uint32_t pa = ((uint32_t)mA & 0xFFu) | (((uint32_t)(-mA) & 0xFFu) << 8);
+                    const uint32_t pb = ((uint32_t)mB & 0xFFu) | (((uint32_t)(-mB) & 0xFFu) << 8);
+                    p = pa | (pb << 16);
+                }
+                p = __builtin_amdgcn_perm(p, p, podd ? 0x02030001u : 0x03020100u);
+                P[gi] = gval[gi] ? p : 0u;    // duplicate stand-in check: no messages
             }
         }
         // ======== check nodes: pass 2 (scatter C->V into S) =================================
@@ -319,7 +349,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             if (a.ablate & 2) continue;
             const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
             const int r0 = (int)(ri & 0xFFFFu);
-            const int deg = (int)(ri >> 16);
+            const int deg = (int)((ri >> 16) & 0xFFu);
 #pragma unroll
             for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
                 if (c8 < deg) {
@@ -342,44 +372,98 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         const float* bnext = BETA + (size_t)(last ? t : t + 1) * a.N;
         uint32_t any_hd = 0, any_pos = 0, nbits = 0;
         const float qmf = (float)qmax;
-        const bool full_target = a.target_bits >= nv;
         const int sb = -(int)F5_SBIAS;
         if (tid < CW) W[total + tid] = F5_DUMMY_W;    // pass-2 adds of padding edges
-        if (a.app_out == nullptr && a.hd_out == nullptr) {
-            // fast path: 4 entries' LDS reads in flight before any is consumed
-            for (int r0 = 0; r0 < ((a.ablate & 4) ? 0 : a.nent); r0 += 4) {
-                uint32_t wv[4], vv[4];
-                float chv[4], bv[4];
-                bool in[4];
+        if constexpr (!OUT) {
+            // counters only.  A wave owns the contiguous 64-entry chunks [c_beg, c_end); with
+            // SLOTS | z a chunk lies in one proto column, so beta is wave-uniform.  Only the
+            // hard-decision sign matters here, and clipping never changes a sign.
+            int amax = INT_MIN;                       // max APP over the target entries
+            const int c_beg = wave * a.cpw;
+            const int c_end = min(c_beg + a.cpw, a.nfull);
+            const bool zuni = (z % SLOTS) == 0;
+            const uint32_t cvalid = (cw < nvalid) ? 1u : 0u;
+            const int tb = a.target_bits;
+            // one loop body per (last iteration, whole word is target) pair; 4 chunks per trip
+            // with the reads issued first.  Reads past c_end stay inside LDS and are unused.
+            auto vn_loop = [&](auto lastc, auto fullc, auto zunic) __attribute__((always_inline)) {
+                constexpr bool LAST = decltype(lastc)::value;
+                constexpr bool FULLT = decltype(fullc)::value;
+                constexpr bool ZUNI = decltype(zunic)::value;
+                const uint32_t* Wr = W + c_beg * 64 + lane;
+                const float* Cr = CH + c_beg * 64 + lane;
+                for (int c = c_beg; c < c_end; c += 4, Wr += 256, Cr += 256) {
+                    uint32_t wv[4];
+                    float chv[4], bv[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int e = tid + (r0 + j) * NT;
-                    in[j] = e < total;
-                    const int ee = in[j] ? e : tid;
-                    vv[j] = (uint32_t)ee >> LOGCW;
-                    wv[j] = W[ee];
-                    chv[j] = CH[ee];
-                    bv[j] = bnext[__umulhi(vv[j], a.zmagic)];
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int e = tid + (r0 + j) * NT;
-                    const int S = (int)(wv[j] & 0x7FFFu) + sb;
-                    int app = q_scaled5(chv[j] * inv, qmf) + S;               // Q(xa) + sum C2V
-                    app = clampi(app, -a.clip_u, a.clip_u);                   // clip +-clip_LLR
-                    if (in[j]) {
-                        if (!last) {
-                            const int tn = q_scaled5(chv[j] * bv[j], qmf) + S;
-                            W[e] = UCN ? (((uint32_t)tn << 16) | (((uint32_t)~app >> 16) & 0x8000u) | F5_SBIAS)
-                                       : (((uint32_t)tn << 16) | F5_SBIAS);
+                    for (int j = 0; j < 4; ++j) {
+                        wv[j] = Wr[j * 64];
+                        chv[j] = Cr[j * 64];
+                        if (!LAST) {
+                            if (ZUNI) {
+                                const uint32_t col = __umulhi((uint32_t)((c + j) * SLOTS), a.zmagic);
+                                bv[j] = bnext[__builtin_amdgcn_readfirstlane(col)];
+                            } else {
+                                const uint32_t v = (uint32_t)((c + j) * 64 + lane) >> LOGCW;
+                                bv[j] = bnext[__umulhi(v, a.zmagic)];
+                            }
                         }
-                        const bool tgt = full_target || (int)vv[j] < a.target_bits;
-                        const uint32_t hdb = (uint32_t)(app >= 0) & (uint32_t)tgt;
-                        any_hd |= hdb;
-                        if (last) { any_pos |= (uint32_t)(app > 0) & (uint32_t)tgt; nbits += hdb; }
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (j == 0 || c + j < c_end) {
+                            const int s = (int)(wv[j] & 0x7FFFu);                     // S + bias
+                            const int app = q_scaled5(chv[j] * inv, qmf) + s + sb;    // Q(xa) + sum C2V
+                            int appt = app;
+                            if (!FULLT) {
+                                const int v = ((c + j) * 64 + lane) >> LOGCW;
+                                appt = (v < tb) ? app : INT_MIN;
+                            }
+                            amax = max(amax, appt);
+                            if (!LAST) {
+                                const int tn = q_scaled5(chv[j] * bv[j], qmf) + s + sb;
+                                const_cast<uint32_t*>(Wr)[j * 64] =
+                                    UCN ? (((uint32_t)tn << 16) | (((uint32_t)~app >> 16) & 0x8000u) | F5_SBIAS)
+                                        : (((uint32_t)tn << 16) | F5_SBIAS);
+                            } else {
+                                nbits += (uint32_t)(appt >= 0) & cvalid;
+                            }
+                        }
+                    }
+                }
+            };
+            using T_ = std::true_type;
+            using F_ = std::false_type;
+            if (!(a.ablate & 4)) {
+                const bool fullt = tb >= nv;
+                if (last) {                       // no W update: beta unused
+                    if (fullt) vn_loop(T_{}, T_{}, T_{}); else vn_loop(T_{}, F_{}, T_{});
+                } else if (zuni) {
+                    if (fullt) vn_loop(F_{}, T_{}, T_{}); else vn_loop(F_{}, F_{}, T_{});
+                } else {
+                    if (fullt) vn_loop(F_{}, T_{}, F_{}); else vn_loop(F_{}, F_{}, F_{});
+                }
+            }
+            // the partial last chunk (n_vars*CW not a multiple of 64), per-lane checks
+            if (a.nfull * 64 < total && wave == (a.nfull / max(a.cpw, 1)) % NWV && !(a.ablate & 4)) {
+                const int e = a.nfull * 64 + lane;
+                if (e < total) {
+                    const uint32_t v = (uint32_t)e >> LOGCW;
+                    const int s = (int)(W[e] & 0x7FFFu);
+                    const float ch = CH[e];
+                    const int app = q_scaled5(ch * inv, qmf) + s + sb;
+                    const int appt = ((int)v < a.target_bits) ? app : INT_MIN;
+                    amax = max(amax, appt);
+                    if (!last) {
+                        const int tn = q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], qmf) + s + sb;
+                        W[e] = ((uint32_t)tn << 16) | (((uint32_t)~app >> 16) & 0x8000u) | F5_SBIAS;
+                    } else {
+                        nbits += (uint32_t)(appt >= 0) & (uint32_t)cvalid;
                     }
                 }
             }
+            any_hd = amax >= 0;
+            any_pos = amax > 0;
         } else {
         for (int r = 0; r < ((a.ablate & 4) ? 0 : a.nent); ++r) {
             const int e = tid + r * NT;
@@ -409,6 +493,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 }
             }
         }
+        if (last) nbits = (cw < nvalid) ? nbits : 0u;
         }
         unsigned long long bw = __ballot(any_hd);
         unsigned long long m = 0;
@@ -421,7 +506,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
 #pragma unroll
             for (int s2 = 0; s2 < SLOTS; ++s2) m |= (bw >> (s2 * CW)) & cwmask;
             if (lane == 0 && m) atomicOr(&RED[2], m);
-            uint32_t nb = (cw < nvalid) ? nbits : 0u;
+            uint32_t nb = nbits;
             for (int off = 32; off > 0; off >>= 1) nb += __shfl_xor(nb, off);
             if (lane == 0 && nb) atomicAdd(&RED[3], (unsigned long long)nb);
         }
@@ -505,28 +590,41 @@ Plan5 plan5(const DevGraph& g, int T) {
     return best;
 }
 
-template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW>
-int launch5k(const F5Args& a, int nblocks, int nw, size_t lds, const float* alpha,
+template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW, bool OUT, bool LUT>
+int launch5o(const F5Args& a, int nblocks, int nw, size_t lds, const float* alpha,
              const float* alpha_ucn, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused5<CW, MAXG, MAXDEG, UCN, PEW>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused5<CW, MAXG, MAXDEG, UCN, PEW, OUT, LUT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)F5_LDS_MAX);
         attr = true;
     }
-    hipLaunchKernelGGL((k_fused5<CW, MAXG, MAXDEG, UCN, PEW>), dim3(nblocks), dim3(64 * nw), lds, s,
+    hipLaunchKernelGGL((k_fused5<CW, MAXG, MAXDEG, UCN, PEW, OUT, LUT>), dim3(nblocks), dim3(64 * nw), lds, s,
                        a, alpha, alpha_ucn);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 
+// the weight table is used when every row shares one weight and there is no UCN weight set
+template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW>
+int launch5k(const F5Args& a, int nblocks, int nw, size_t lds, bool lut, const float* alpha,
+             const float* alpha_ucn, hipStream_t s) {
+    constexpr bool CANLUT = !UCN && !PEW;
+    const bool out = a.app_out || a.hd_out;
+    if (CANLUT && lut)
+        return out ? launch5o<CW, MAXG, MAXDEG, UCN, PEW, true, CANLUT>(a, nblocks, nw, lds, alpha, alpha_ucn, s)
+                   : launch5o<CW, MAXG, MAXDEG, UCN, PEW, false, CANLUT>(a, nblocks, nw, lds, alpha, alpha_ucn, s);
+    return out ? launch5o<CW, MAXG, MAXDEG, UCN, PEW, true, false>(a, nblocks, nw, lds, alpha, alpha_ucn, s)
+               : launch5o<CW, MAXG, MAXDEG, UCN, PEW, false, false>(a, nblocks, nw, lds, alpha, alpha_ucn, s);
+}
+
 template <int CW, int MAXG, int MAXDEG>
-int launch5s(const F5Args& a, int nblocks, int nw, size_t lds, const float* alpha,
+int launch5s(const F5Args& a, int nblocks, int nw, size_t lds, bool lut, const float* alpha,
              const float* alpha_ucn, bool pew, hipStream_t s) {
     if (alpha_ucn)
-        return pew ? launch5k<CW, MAXG, MAXDEG, true, true>(a, nblocks, nw, lds, alpha, alpha_ucn, s)
-                   : launch5k<CW, MAXG, MAXDEG, true, false>(a, nblocks, nw, lds, alpha, alpha_ucn, s);
-    return pew ? launch5k<CW, MAXG, MAXDEG, false, true>(a, nblocks, nw, lds, alpha, nullptr, s)
-               : launch5k<CW, MAXG, MAXDEG, false, false>(a, nblocks, nw, lds, alpha, nullptr, s);
+        return pew ? launch5k<CW, MAXG, MAXDEG, true, true>(a, nblocks, nw, lds, lut, alpha, alpha_ucn, s)
+                   : launch5k<CW, MAXG, MAXDEG, true, false>(a, nblocks, nw, lds, lut, alpha, alpha_ucn, s);
+    return pew ? launch5k<CW, MAXG, MAXDEG, false, true>(a, nblocks, nw, lds, lut, alpha, nullptr, s)
+               : launch5k<CW, MAXG, MAXDEG, false, false>(a, nblocks, nw, lds, lut, alpha, nullptr, s);
 }
 
 }  // namespace
@@ -545,9 +643,17 @@ const char* fused5_shape_name(const DevGraph& g, int T) {
 int fused5_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, float step,
                   int clip_u, bool per_edge_w, uint64_t* hd_out, int64_t* counters,
                   uint8_t* flags, hipStream_t s) {
-    const Plan5 p = plan5(g, b.T);
+    Plan5 p = plan5(g, b.T);
     if (p.shape < 0) return LDPC_ERR_UNSUPPORTED;
     const Shape5& sh = kShapes5[p.shape];
+    // weight table (uniform row weights, no UCN set): only if it costs no workgroup slot per CU
+    bool lut = !per_edge_w && b.alpha_ucn == nullptr && g.M < 256 &&
+               getenv("LDPC_F5_NOLUT") == nullptr;
+    if (lut) {
+        const size_t lds_lut = p.lds + (((size_t)b.T * g.M * (qmax + 2) * 2 + 15) & ~(size_t)15);
+        if (lds_lut > F5_LDS_MAX || F5_LDS_MAX / lds_lut < F5_LDS_MAX / p.lds) lut = false;
+        else p.lds = lds_lut;
+    }
     F5Args a{};
     a.llr = llr;
     a.beta = b.beta;
@@ -573,16 +679,19 @@ int fused5_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, 
     a.hstep = p.hstep;
     a.ngroups = p.ngroups;
     a.nent = (g.n_vars * sh.cw + 64 * p.nw - 1) / (64 * p.nw);
+    a.nfull = g.n_vars * sh.cw / 64;
+    a.cpw = (a.nfull + p.nw - 1) / p.nw;
+    a.Mp = g.M;
     a.zmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.z - 1) / (uint64_t)g.z);
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // timing only
     const int nblocks = (int)((b.B + sh.cw - 1) / sh.cw);
     const float* au = b.alpha_ucn;
     switch (p.shape) {
-        case 0: return launch5s<16, 3, 16>(a, nblocks, p.nw, p.lds, b.alpha, au, per_edge_w, s);
-        case 1: return launch5s<16, 3, 24>(a, nblocks, p.nw, p.lds, b.alpha, au, per_edge_w, s);
-        case 2: return launch5s<8, 5, 16>(a, nblocks, p.nw, p.lds, b.alpha, au, per_edge_w, s);
-        case 3: return launch5s<64, 3, 8>(a, nblocks, p.nw, p.lds, b.alpha, au, per_edge_w, s);
-        case 4: return launch5s<64, 2, 32>(a, nblocks, p.nw, p.lds, b.alpha, au, per_edge_w, s);
+        case 0: return launch5s<16, 3, 16>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s);
+        case 1: return launch5s<16, 3, 24>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s);
+        case 2: return launch5s<8, 5, 16>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s);
+        case 3: return launch5s<64, 3, 8>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s);
+        case 4: return launch5s<64, 2, 32>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s);
         default: return LDPC_ERR_UNSUPPORTED;
     }
 }

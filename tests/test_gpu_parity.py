@@ -77,3 +77,19 @@ def test_session_fer_loop_reproduces_reference_results(cuda_device):
                                          int(d["B"]), 0, g.N, g.M, 24, True, 20, sess,
                                          make_net_dict(20), 0, 2, 0, 0, 0, 0, 5, 20.0)
         np.testing.assert_array_equal(Results, d["Results"])
+
+
+@pytest.mark.parametrize("kernel", KERNEL_NAMES)
+@pytest.mark.parametrize("name", DECODER_CASES)
+def test_counters_only_decode_matches_reference(name, kernel, cuda_device):
+    """The counters/flags-only launch (what fer_sweep and bench.py run) is a separate kernel
+    build from the APP-exporting one; it must give the same counters and frame flags."""
+    c = load_case(name)
+    dec = _decoder(c, kernel, cuda_device)
+    res = dec.decode(c["llr"], app=False, counters=True, flags=True)
+    full = dec.decode(c["llr"], app=True, counters=True, flags=True)
+    assert np.array_equal(res.counters.cpu().numpy(), full.counters.cpu().numpy())
+    assert np.array_equal(res.flags.cpu().numpy(), full.flags.cpu().numpy())
+    if c["exact"]:
+        assert np.array_equal(res.counters.cpu().numpy(), counters_from_app(c["app"]))
+        assert np.array_equal(res.flags.cpu().numpy(), flags_from_app(c["app"]))

@@ -47,6 +47,11 @@ def test_kernels_agree_ragged_large(cuda_device, ucn):
     ref = nms_oracle.decode(x, dec.graph.proto, 24, W.alpha, W.alpha_ucn, W.beta, 20, 2, 5)["app"]
     assert np.array_equal(app[:, :96], ref)
     assert 0 < outs["fused"]["counters"][1] < B     # 2.0 dB: some frames fail
+    # counters/flags-only launches (a separate kernel build) on the same ragged batch
+    for k in ("flood", "fused"):
+        r = dec.decode(llr, app=False, counters=True, flags=True, kernel=k)
+        assert np.array_equal(r.counters.cpu().numpy(), counters_from_app(app)), k
+        assert np.array_equal(r.flags.cpu().numpy(), flags_from_app(app)), k
 
 
 @pytest.mark.parametrize("B", [1, 31, 33, 255, 257])
