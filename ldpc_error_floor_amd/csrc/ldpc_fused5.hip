@@ -8,12 +8,13 @@
 //  * P   — one VGPR holding the check's four possible output messages as signed bytes
 //          [+mA, -mA, +mB, -mB] (mA: min over all edges, mB: second minimum, both already
 //          weighted and quantized, in grid units);
-//  * SEL — 5-bit fields, six edges per VGPR: field = 8*negative + 16*is_argmin, i.e. the bit
-//          offset of the edge's message inside P.  Decoding a message is
-//          v_bfe_i32(P, SEL >> 5*pos, 8): 2 ops (v3: 5).
+//  * SEL — one selector byte per edge, four edges per VGPR: byte = 2*is_argmin + negative,
+//          the index of the edge's message inside P.  v_perm_b32(P, P, SEL[w]) yields four
+//          edges' messages, and pass 1 subtracts a message straight from its byte with an
+//          SDWA sign-extended source: a quarter op per edge to decode (v3: 5 ops).
 //  * pass 1 folds V->C magnitudes with one v_min + one v_med3 per edge (running first/second
 //    minimum of key = |v2c| << 8 | edge code), and the V->C signs with one v_alignbit per
-//    edge, which appends the top 5 bits of v2c (= 5 copies of its sign) to a SEL-shaped word;
+//    edge, which appends the top byte of v2c (8 copies of its sign) to a SEL-shaped word;
 //    the quantizer clamp moves after the minimum (clamp is monotonic);
 //  * W[v][cw] = Tv (bits 31..16, signed) | hd (bit 15) | S + 2^14 (bits 14..0): pass 1 reads Tv
 //    with an SDWA sign-extended word select, pass 2 adds the message without a shift;
@@ -86,29 +87,30 @@ __device__ __forceinline__ int clampi(int x, int lo, int hi) {
     return r;
 }
 
-// ---- SEL layout: edge k -> word k/6, field position counted from the last inserted edge -----
+// ---- SEL layout: edge k -> byte of word k/4, counted from the last inserted edge ------------
+// A selector byte is 2*is_argmin + negative: the index of the edge's message inside P, so
+// v_perm_b32(P, P, SEL[w]) yields the messages of four edges at once.
 template <int MAXDEG>
 struct Sel {
-    static constexpr int NSEL = (MAXDEG + 5) / 6;
-    static constexpr int nins(int w) { return (MAXDEG - 6 * w) < 6 ? (MAXDEG - 6 * w) : 6; }
-    static constexpr int pos(int k) { return nins(k / 6) - 1 - (k % 6); }
-    static constexpr int shift(int k) { return 5 * pos(k); }
-    static constexpr uint32_t code(int k) { return ((uint32_t)(k / 6) << 5) | (uint32_t)(5 * pos(k) + 4); }
-    static constexpr uint32_t f3mask(int w) {
+    static constexpr int NSEL = (MAXDEG + 3) / 4;
+    static constexpr int nins(int w) { return (MAXDEG - 4 * w) < 4 ? (MAXDEG - 4 * w) : 4; }
+    static constexpr int pos(int k) { return nins(k / 4) - 1 - (k % 4); }
+    static constexpr uint32_t code(int k) { return ((uint32_t)(k / 4) << 5) | (uint32_t)(8 * pos(k) + 1); }
+    static constexpr uint32_t bmask(int w) {
         uint32_t m = 0;
-        for (int i = 0; i < nins(w); ++i) m |= 8u << (5 * i);
+        for (int i = 0; i < nins(w); ++i) m |= 1u << (8 * i);
         return m;
     }
     // number of edges of word w inside chunk [c8, c8+8)
     static constexpr int in_chunk(int w, int c8) {
         int n = 0;
-        for (int k = c8; k < c8 + 8 && k < MAXDEG; ++k) n += (k / 6 == w);
+        for (int k = c8; k < c8 + 8 && k < MAXDEG; ++k) n += (k / 4 == w);
         return n;
     }
 };
 
 template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW, bool OUT, bool LUT>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(CW == 16 && MAXDEG == 16 ? 6 : 1)))
 k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ alpha_ucn) {
     using SL = Sel<MAXDEG>;
     constexpr int NSEL = SL::NSEL;
@@ -227,18 +229,20 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         for (int w = 0; w < NSEL; ++w) SEL[gi][w] = 0;
     }
 
-    // C->V message of edge k from a check's state
-    auto msg = [&](const int gi, const int k, const float* wt, const float* wtu, const int r0)
-        __attribute__((always_inline)) -> int {
-        const uint32_t f = SEL[gi][k / 6] >> SL::shift(k);
+    // C->V message of edge k, given R = v_perm(P, P, SEL[k/4]) (the word's four messages)
+    auto msg = [&](const int gi, const int k, const uint32_t R, const float* wt, const float* wtu,
+                   const int r0) __attribute__((always_inline)) -> int {
         if constexpr (!PEW) {
-            return __builtin_amdgcn_sbfe((int)P[gi], f, 8);
+            return (int)(signed char)(R >> (8 * SL::pos(k)));
         } else {
-            const int m = (int)((f & 16u) ? (P[gi] >> 16) : (P[gi] & 0xFFFFu));
+            const int m = (int)((R >> (8 * SL::pos(k))) & 0xFFu);        // 255: no other edge
             const float w = (UCN && UC[gi]) ? wtu[r0 + k] : wt[r0 + k];
-            const int mq = q_mag5(m, w, step, inv, qmax);
-            return (f & 8u) ? -mq : mq;
+            const int mq = q_mag5(m == 255 ? F5_BIG_U : m, w, step, inv, qmax);
+            return ((SEL[gi][k / 4] >> (8 * SL::pos(k))) & 1u) ? -mq : mq;
         }
+    };
+    auto perm_word = [&](const int gi, const int w) __attribute__((always_inline)) -> uint32_t {
+        return (w < NSEL) ? __builtin_amdgcn_perm(P[gi], P[gi], SEL[gi][w < NSEL ? w : 0]) : 0u;
     };
 
     for (int t = 0; t < a.T; ++t) {
@@ -277,14 +281,16 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                             wv[j] = *reinterpret_cast<const uint32_t*>(smem + addr);
                         }
                     }
+                    const uint32_t R0 = perm_word(gi, c8 / 4), R1 = perm_word(gi, c8 / 4 + 1);
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         const int k = c8 + j;
                         if (k < MAXDEG) {
-                            const int cold = msg(gi, k, atp, aup, r0);
+                            const int cold = msg(gi, k, j < 4 ? R0 : R1, atp, aup, r0);
                             const int d = (int)(short)(wv[j] >> 16) - cold;      // V->C before Q
                             const uint32_t key = ((uint32_t)max(d, -d) << 8) | SL::code(k);
-                            NG[k / 6] = __builtin_amdgcn_alignbit(NG[k / 6], (uint32_t)d, 27);
+                            // append the byte of sign copies of d to the edge's selector word
+                            NG[k / 4] = __builtin_amdgcn_alignbit(NG[k / 4], (uint32_t)d, 24);
                             const uint32_t o1 = c1;
                             c1 = min(o1, key);
                             c2 = med3u(o1, c2, key);
@@ -296,17 +302,19 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
 #pragma unroll
                     for (int w = 0; w < NSEL; ++w) {
                         const int n = SL::in_chunk(w, c8);
-                        if (n > 0) NG[w] <<= 5 * n;
+                        if (n > 0) NG[w] = (n >= 4) ? 0u : (NG[w] << (8 * n));
                     }
                 }
             }
-            // ---- new state: quantized minima, sign fields, argmin field ----
-            // parity of the negative V->C signs: every sign field holds 5 copies of its sign
+            // ---- new state: quantized minima, selector bytes, argmin bit ----
             uint32_t nbit = 0;
 #pragma unroll
-            for (int w = 0; w < NSEL; ++w) nbit += __popc(NG[w]);
-            // message sign = V->C sign XOR (count of positives odd); the XOR is applied to P
-            // (byte swap inside each half) for byte-packed P, to the fields for PEW
+            for (int w = 0; w < NSEL; ++w) {
+                NG[w] &= SL::bmask(w);                 // bit 0 of each byte: V->C sign negative
+                nbit += __popc(NG[w]);
+            }
+            // message sign = V->C sign XOR (count of positives odd): applied to P as a byte
+            // swap inside each half; for PEW (P holds magnitudes) to the selector bytes
             const bool podd = ((uint32_t)deg + nbit) & 1u;
             const uint32_t code = c1 & 255u;
             const uint32_t onebit = 1u << (code & 31u);
@@ -314,12 +322,12 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             const uint32_t pm = (PEW && podd) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
             for (int w = 0; w < NSEL; ++w)
-                SEL[gi][w] = ((NG[w] ^ pm) & SL::f3mask(w)) | ((wsel == (uint32_t)w) ? onebit : 0u);
+                SEL[gi][w] = (NG[w] ^ (pm & SL::bmask(w))) | ((wsel == (uint32_t)w) ? onebit : 0u);
             const int m1 = min((int)(c1 >> 8), qmax);
             if constexpr (PEW) {
-                const int m2 = (deg < 2) ? F5_BIG_U : min((int)(c2 >> 8), qmax);
+                const uint32_t m2 = (deg < 2) ? 255u : (uint32_t)min((int)(c2 >> 8), qmax);
                 UC[gi] = (int)syn;
-                P[gi] = gval[gi] ? ((uint32_t)m1 | ((uint32_t)m2 << 16)) : 0u;
+                P[gi] = gval[gi] ? ((uint32_t)m1 * 0x0101u | (m2 * 0x0101u) << 16) : 0u;
             } else {
                 uint32_t p;
                 if constexpr (LUT) {
@@ -353,13 +361,14 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
 #pragma unroll
             for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
                 if (c8 < deg) {
+                    const uint32_t R0 = perm_word(gi, c8 / 4), R1 = perm_word(gi, c8 / 4 + 1);
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         const int k = c8 + j;
                         if (k < MAXDEG) {
                             const uint32_t pk = gad[gi][k >> 1];
                             const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
-                            const int c = msg(gi, k, at, au, r0);
+                            const int c = msg(gi, k, j < 4 ? R0 : R1, at, au, r0);
                             atomicAdd(reinterpret_cast<uint32_t*>(smem + addr), (uint32_t)c);
                         }
                     }
