@@ -39,6 +39,11 @@ constexpr int F5_BIG_U = 1023;               // "no other edge": value 10000 (Ma
 constexpr size_t F5_LDS_MAX = 160 * 1024;
 constexpr uint32_t F5_SBIAS = 16384;         // S field bias (bits 14..0)
 constexpr uint32_t F5_DUMMY_W = (16383u << 16) | F5_SBIAS;
+constexpr float F5_MAGIC = 12582912.0f;                 // 1.5 * 2^23
+constexpr int F5_MAGIC_BITS = 0x4B400000;              // bit pattern of F5_MAGIC
+constexpr int F5_APP0 = F5_MAGIC_BITS + (int)F5_SBIAS;  // APP == 0 in the VN's biased domain
+// (Tv + F5_APP0) * 2^16 + F5_WBIAS == (Tv << 16) | F5_SBIAS  (mod 2^32)
+constexpr uint32_t F5_WBIAS = F5_SBIAS - (uint32_t)F5_APP0 * 65536u;
 
 struct F5Args {
     const float* llr;
@@ -268,24 +273,26 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
 #pragma unroll
             for (int w = 0; w < NSEL; ++w) NG[w] = 0;
             uint32_t syn = 0;
+            // one chunk of 8 edges, straight-line: padding slots (k >= deg) read the dummy word
+            // (|v2c| never minimal, positive sign).  Skipping them behind scalar branches was
+            // measured slower: the branches split the chunk's schedule.
+            auto chunk1 = [&](const int c8, const bool full) __attribute__((always_inline)) {
+                uint32_t wv[8];
 #pragma unroll
-            for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
-                if (c8 < deg) {
-                    uint32_t wv[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int k = c8 + j;
-                        if (k < MAXDEG) {
-                            const uint32_t pk = gad[gi][k >> 1];
-                            const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
-                            wv[j] = *reinterpret_cast<const uint32_t*>(smem + addr);
-                        }
+                for (int j = 0; j < 8; ++j) {
+                    const int k = c8 + j;
+                    if (k < MAXDEG && (full || k < deg)) {
+                        const uint32_t pk = gad[gi][k >> 1];
+                        const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
+                        wv[j] = *reinterpret_cast<const uint32_t*>(smem + addr);
                     }
-                    const uint32_t R0 = perm_word(gi, c8 / 4), R1 = perm_word(gi, c8 / 4 + 1);
+                }
+                const uint32_t R0 = perm_word(gi, c8 / 4), R1 = perm_word(gi, c8 / 4 + 1);
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int k = c8 + j;
-                        if (k < MAXDEG) {
+                for (int j = 0; j < 8; ++j) {
+                    const int k = c8 + j;
+                    if (k < MAXDEG) {
+                        if (full || k < deg) {
                             const int cold = msg(gi, k, j < 4 ? R0 : R1, atp, aup, r0);
                             const int d = (int)(short)(wv[j] >> 16) - cold;      // V->C before Q
                             const uint32_t key = ((uint32_t)max(d, -d) << 8) | SL::code(k);
@@ -295,8 +302,16 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                             c1 = min(o1, key);
                             c2 = med3u(o1, c2, key);
                             if (UCN) syn ^= (wv[j] >> 15) & 1u;
+                        } else {
+                            NG[k / 4] <<= 8;                                     // positive
                         }
                     }
+                }
+            };
+#pragma unroll
+            for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
+                if (c8 < deg) {
+                    chunk1(c8, true);
                 } else {
                     // chunk skipped (deg <= c8): its edges enter as positive (zero) sign fields
 #pragma unroll
@@ -358,21 +373,22 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
             const int r0 = (int)(ri & 0xFFFFu);
             const int deg = (int)((ri >> 16) & 0xFFu);
+            auto chunk2 = [&](const int c8, const bool full) __attribute__((always_inline)) {
+                const uint32_t R0 = perm_word(gi, c8 / 4), R1 = perm_word(gi, c8 / 4 + 1);
 #pragma unroll
-            for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
-                if (c8 < deg) {
-                    const uint32_t R0 = perm_word(gi, c8 / 4), R1 = perm_word(gi, c8 / 4 + 1);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int k = c8 + j;
-                        if (k < MAXDEG) {
-                            const uint32_t pk = gad[gi][k >> 1];
-                            const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
-                            const int c = msg(gi, k, j < 4 ? R0 : R1, at, au, r0);
-                            atomicAdd(reinterpret_cast<uint32_t*>(smem + addr), (uint32_t)c);
-                        }
+                for (int j = 0; j < 8; ++j) {
+                    const int k = c8 + j;
+                    if (k < MAXDEG && (full || k < deg)) {
+                        const uint32_t pk = gad[gi][k >> 1];
+                        const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
+                        const int c = msg(gi, k, j < 4 ? R0 : R1, at, au, r0);
+                        atomicAdd(reinterpret_cast<uint32_t*>(smem + addr), (uint32_t)c);
                     }
                 }
+            };
+#pragma unroll
+            for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
+                if (c8 < deg) chunk2(c8, true);
             }
         }
         __syncthreads();
@@ -421,21 +437,29 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         if (j == 0 || c + j < c_end) {
+                            // Q(y) for y already scaled to grid units: clamp to +-qmax, then
+                            // add 1.5*2^23 so the float add rounds half to even (as rintf) and
+                            // the integer sits in the low mantissa bits: bits - F5_MAGIC_BITS
                             const int s = (int)(wv[j] & 0x7FFFu);                     // S + bias
-                            const int app = q_scaled5(chv[j] * inv, qmf) + s + sb;    // Q(xa) + sum C2V
-                            int appt = app;
+                            const float yc = __builtin_amdgcn_fmed3f(chv[j] * inv, -qmf, qmf);
+                            const int qc = __float_as_int(yc + F5_MAGIC);
+                            // APP + F5_MAGIC_BITS + S bias: the sign test is against that offset
+                            const int appb = qc + s;
+                            int appt = appb;
                             if (!FULLT) {
                                 const int v = ((c + j) * 64 + lane) >> LOGCW;
-                                appt = (v < tb) ? app : INT_MIN;
+                                appt = (v < tb) ? appb : INT_MIN;
                             }
                             amax = max(amax, appt);
                             if (!LAST) {
-                                const int tn = q_scaled5(chv[j] * bv[j], qmf) + s + sb;
-                                const_cast<uint32_t*>(Wr)[j * 64] =
-                                    UCN ? (((uint32_t)tn << 16) | (((uint32_t)~app >> 16) & 0x8000u) | F5_SBIAS)
-                                        : (((uint32_t)tn << 16) | F5_SBIAS);
+                                const float yb = __builtin_amdgcn_fmed3f(chv[j] * bv[j], -qmf, qmf);
+                                const int tb2 = __float_as_int(yb + F5_MAGIC) + s;   // Tv + biases
+                                // W = (Tv << 16) | S bias, Tv = tb2 - F5_MAGIC_BITS - S bias
+                                uint32_t wn = (uint32_t)tb2 * 65536u + F5_WBIAS;
+                                if (UCN) wn |= (appb >= F5_APP0) ? 0x8000u : 0u;
+                                const_cast<uint32_t*>(Wr)[j * 64] = wn;
                             } else {
-                                nbits += (uint32_t)(appt >= 0) & cvalid;
+                                nbits += (uint32_t)(appt >= F5_APP0) & cvalid;
                             }
                         }
                     }
@@ -462,17 +486,17 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     const float ch = CH[e];
                     const int app = q_scaled5(ch * inv, qmf) + s + sb;
                     const int appt = ((int)v < a.target_bits) ? app : INT_MIN;
-                    amax = max(amax, appt);
+                    amax = max(amax, appt == INT_MIN ? INT_MIN : appt + F5_APP0);
                     if (!last) {
                         const int tn = q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], qmf) + s + sb;
                         W[e] = ((uint32_t)tn << 16) | (((uint32_t)~app >> 16) & 0x8000u) | F5_SBIAS;
                     } else {
-                        nbits += (uint32_t)(appt >= 0) & (uint32_t)cvalid;
+                        nbits += (uint32_t)(appt >= 0 && appt != INT_MIN) & (uint32_t)cvalid;
                     }
                 }
             }
-            any_hd = amax >= 0;
-            any_pos = amax > 0;
+            any_hd = amax >= F5_APP0;
+            any_pos = amax > F5_APP0;
         } else {
         for (int r = 0; r < ((a.ablate & 4) ? 0 : a.nent); ++r) {
             const int e = tid + r * NT;

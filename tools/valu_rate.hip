@@ -1,0 +1,101 @@
+// VALU issue-rate probe for the instruction mix of the fused decoder's check pass.
+// Each lane runs NITER rounds of 8 independent chains (no memory traffic in the loop); the
+// rate is wave-instructions per SIMD-cycle, computed from the measured time and the clock
+// reported by hipDeviceProp.  Build: hipcc --offload-arch=gfx950 -O3 tools/valu_rate.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+constexpr int NITER = 65536;
+
+template <int MIX>
+__global__ void __launch_bounds__(256) k_mix(uint32_t* out, uint32_t seed, unsigned long long* cyc) {
+    uint32_t a[8], b[8], c[8];
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        a[j] = seed * (threadIdx.x + 1) + j;
+        b[j] = a[j] ^ 0x5a5a5a5a;
+        c[j] = a[j] * 3u;
+    }
+    for (int it = 0; it < NITER; ++it) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (MIX == 0) {            // plain v_add_u32
+                asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 1) {     // v_med3_u32 (VOP3)
+                asm volatile("v_med3_u32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+            } else if (MIX == 2) {     // SDWA subtract, word/byte selects
+                asm volatile("v_sub_u32_sdwa %0, sext(%0), sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:BYTE_2"
+                             : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 3) {     // v_perm_b32
+                asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+            } else if (MIX == 4) {     // v_alignbit_b32
+                asm volatile("v_alignbit_b32 %0, %0, %1, 24" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 5) {     // the pass-1 edge sequence: sdwa sub, neg, max, lshl_or, alignbit, min, med3
+                uint32_t d, n, k;
+                asm volatile("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:BYTE_1"
+                             : "=v"(d) : "v"(a[j]), "v"(b[j]));
+                asm volatile("v_sub_u32 %0, 0, %1" : "=v"(n) : "v"(d));
+                asm volatile("v_max_i32 %0, %1, %2" : "=v"(n) : "v"(d), "v"(n));
+                asm volatile("v_lshl_or_b32 %0, %1, 8, 5" : "=v"(k) : "v"(n));
+                asm volatile("v_alignbit_b32 %0, %0, %1, 24" : "+v"(c[j]) : "v"(d));
+                asm volatile("v_min_u32 %0, %0, %1" : "+v"(b[j]) : "v"(k));
+                asm volatile("v_med3_u32 %0, %1, %0, %2" : "+v"(a[j]) : "v"(b[j]), "v"(k));
+            } else if (MIX == 6) {     // dependent chain of v_add (one chain per lane)
+                asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[0]) : "v"(b[j]));
+            }
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r ^= a[j] ^ b[j] ^ c[j];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+    if ((threadIdx.x & 63) == 0) atomicMax(cyc, t1 - t0);     // longest wave, shader clocks
+}
+
+template <int MIX>
+void run(const char* name, int ops_per_j, int waves_per_simd, int ncu, double clk_ghz, uint32_t* d) {
+    const int block = 256;                                  // 4 waves = 1 per SIMD
+    const int grid = ncu * waves_per_simd;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    unsigned long long* cyc = reinterpret_cast<unsigned long long*>(d + (size_t)ncu * 8 * 256 * 2);
+    hipLaunchKernelGGL(k_mix<MIX>, dim3(grid), dim3(block), 0, 0, d, 7u, cyc);
+    hipMemset(cyc, 0, 8);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL(k_mix<MIX>, dim3(grid), dim3(block), 0, 0, d, 9u, cyc);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    unsigned long long c = 0;
+    hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
+    // s_memtime counts shader-clock cycles: per SIMD, waves_per_simd waves shared the cycles
+    const double per_simd_instr = (double)waves_per_simd * NITER * 8.0 * ops_per_j;
+    printf("%-28s waves/SIMD %d  %8.3f ms  %6.2f shader cycles per wave-instr  (clock %.2f GHz)\n",
+           name, waves_per_simd, ms, (double)c / per_simd_instr, (double)c / (ms * 1e6));
+}
+
+int main() {
+    hipDeviceProp_t p;
+    hipGetDeviceProperties(&p, 0);
+    const int ncu = p.multiProcessorCount;
+    const double clk = p.clockRate / 1e6;                   // kHz -> GHz
+    printf("%s  CUs %d  clock %.3f GHz (device max; the measured rate uses it)\n", p.name, ncu, clk);
+    uint32_t* d;
+    hipMalloc(&d, (size_t)ncu * 8 * 256 * 4 * 4);
+    for (int w : {1, 2, 4, 6, 8}) {
+        run<0>("v_add_u32", 1, w, ncu, clk, d);
+        run<1>("v_med3_u32", 1, w, ncu, clk, d);
+        run<2>("v_sub_u32_sdwa", 1, w, ncu, clk, d);
+        run<3>("v_perm_b32", 1, w, ncu, clk, d);
+        run<4>("v_alignbit_b32", 1, w, ncu, clk, d);
+        run<5>("pass-1 edge (7 ops)", 7, w, ncu, clk, d);
+        run<6>("dependent v_add chain", 1, w, ncu, clk, d);
+    }
+    hipFree(d);
+    return 0;
+}
