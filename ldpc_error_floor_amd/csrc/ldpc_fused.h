@@ -7,6 +7,8 @@ namespace ldpc {
 struct FusedWorkspace {
     uint64_t* hd = nullptr;        // [T][tiles][n_vars][4] hard decisions (only for bit export)
     int64_t hd_elems = 0;
+    void* tables = nullptr;        // per-decode tables shared by all workgroups (v5)
+    size_t tables_bytes = 0;
 };
 
 bool fused_supported(const DevGraph& g, int mode, int T);
@@ -32,9 +34,9 @@ int fused3_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, 
 // v5 (ldpc_fused5.hip): byte-packed check state, default when a shape fits
 bool fused5_supported(const DevGraph& g, int T);
 const char* fused5_shape_name(const DevGraph& g, int T);
-int fused5_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, float step,
-                  int clip_u, bool per_edge_w, uint64_t* hd_out, int64_t* counters,
-                  uint8_t* flags, hipStream_t s);
+int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr,
+                  int qmax, float step, int clip_u, bool per_edge_w, uint64_t* hd_out,
+                  int64_t* counters, uint8_t* flags, hipStream_t s);
 void fused_free(FusedWorkspace& ws);
 
 }  // namespace ldpc

@@ -459,7 +459,7 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
         hd_out = ws.hd;
     }
     if (fused_version() >= 5 && fused5_supported(g, b.T))
-        return fused5_decode(g, b, llr, mode_qmax(mode), step, (int)cu, per_edge_w != 0, hd_out,
+        return fused5_decode(g, b, ws, llr, mode_qmax(mode), step, (int)cu, per_edge_w != 0, hd_out,
                              counters, flags, s);
     if (fused_version() == 4 && fused4_supported(g, b.T, mode_qmax(mode), per_edge_w != 0))
         return fused4_decode(g, b, llr, mode_qmax(mode), step, (int)cu, hd_out, counters, flags, s);
@@ -512,6 +512,9 @@ void fused_free(FusedWorkspace& ws) {
     if (ws.hd) (void)hipFree(ws.hd);
     ws.hd = nullptr;
     ws.hd_elems = 0;
+    if (ws.tables) (void)hipFree(ws.tables);
+    ws.tables = nullptr;
+    ws.tables_bytes = 0;
 }
 
 }  // namespace ldpc

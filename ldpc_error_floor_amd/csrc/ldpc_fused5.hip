@@ -62,6 +62,8 @@ struct F5Args {
     int hstep, ngroups, nent;
     int nfull, cpw;    // VN: full 64-entry chunks, chunks per wave
     int Mp;            // proto rows
+    const float* betas;        // [T][N] beta / step (setup kernel)
+    const uint16_t* qtab;      // [T][Mp][qmax+2] weight table (setup kernel), LUT builds only
     uint32_t zmagic;
     int ablate;        // diagnostic only (LDPC_DIAG_ABLATE): 1 skip CN pass 1, 2 skip pass 2, 4 skip VN
 };
@@ -161,21 +163,12 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             for (int r = 0; r < CW; ++r)
                 if (v < nv) scr[r * rl + v] = x[r];
         }
-        // beta pre-multiplied by 1/step (a power of two): fl32(ch*beta)/step == fl32(ch*(beta/step))
-        for (int f = tid; f < a.T * a.N; f += NT) BETA[f] = a.beta[f] * inv;
+        // beta / step and the weight table come precomputed (k_f5_tables): plain copies
+        for (int f = tid; f < a.T * a.N; f += NT) BETA[f] = a.betas[f];
         if (tid < 8) RED[tid] = (tid == 1) ? ~0ull : 0ull;
         if constexpr (LUT) {
-            // QT[t][row][m] = [+q, -q] bytes, q = Q(relu(|o| * alpha_t,row)), |o| = m grid units
-            // (m = qmax+1 stands for "no other edge", the 10000 value)
-            const int nq = qmax + 2;
-            for (int f = tid; f < a.T * a.Mp * nq; f += NT) {
-                const int m = f % nq;
-                const int tr = f / nq;
-                const int tt = tr / a.Mp, row = tr - tt * a.Mp;
-                const float w = alpha[(size_t)tt * a.E + a.row_ptr[row]];
-                const int q = q_mag5(m > qmax ? F5_BIG_U : m, w, step, inv, qmax);
-                QT[f] = (uint16_t)(((uint32_t)q & 0xFFu) | (((uint32_t)(-q) & 0xFFu) << 8));
-            }
+            const int nqt = a.T * a.Mp * (qmax + 2);
+            for (int f = tid; f < nqt; f += NT) QT[f] = a.qtab[f];
         }
         __syncthreads();
         for (int e = tid; e < total; e += NT) CH[e] = scr[(e & (CW - 1)) * rl + (e >> LOGCW)];
@@ -570,6 +563,26 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     }
 }
 
+// Per-decode tables shared by every workgroup:
+//   betas[t][n] = beta[t][n] / step  (a power of two: fl32(ch*beta)/step == fl32(ch*(beta/step)))
+//   qtab[t][row][m] = [+q, -q] bytes, q = Q(relu(|o| * alpha_t,row)), |o| = m grid units
+//                     (m = qmax+1 stands for "no other edge", the 10000 value)
+__global__ void k_f5_tables(const float* __restrict__ alpha, const float* __restrict__ beta,
+                            const int32_t* __restrict__ row_ptr, int T, int Mp, int E, int N,
+                            int qmax, float step, float inv, float* betas, uint16_t* qtab) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < T * N) betas[f] = beta[f] * inv;
+    const int nq = qmax + 2;
+    if (qtab && f < T * Mp * nq) {
+        const int m = f % nq;
+        const int tr = f / nq;
+        const int tt = tr / Mp, row = tr - tt * Mp;
+        const float w = alpha[(size_t)tt * E + row_ptr[row]];
+        const int q = q_mag5(m > qmax ? F5_BIG_U : m, w, step, inv, qmax);
+        qtab[f] = (uint16_t)(((uint32_t)q & 0xFFu) | (((uint32_t)(-q) & 0xFFu) << 8));
+    }
+}
+
 // ---- shapes ------------------------------------------------------------------------------
 struct Shape5 {
     int cw, maxg, maxdeg;
@@ -673,9 +686,9 @@ const char* fused5_shape_name(const DevGraph& g, int T) {
     return buf;
 }
 
-int fused5_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, float step,
-                  int clip_u, bool per_edge_w, uint64_t* hd_out, int64_t* counters,
-                  uint8_t* flags, hipStream_t s) {
+int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr,
+                  int qmax, float step, int clip_u, bool per_edge_w, uint64_t* hd_out,
+                  int64_t* counters, uint8_t* flags, hipStream_t s) {
     Plan5 p = plan5(g, b.T);
     if (p.shape < 0) return LDPC_ERR_UNSUPPORTED;
     const Shape5& sh = kShapes5[p.shape];
@@ -717,6 +730,31 @@ int fused5_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, 
     a.Mp = g.M;
     a.zmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.z - 1) / (uint64_t)g.z);
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // timing only
+    // shared tables: one small launch per decode instead of per-workgroup dependent loads
+    const size_t nbeta = (size_t)b.T * g.N, nqt = (size_t)b.T * g.M * (qmax + 2);
+    const size_t tbytes = ((nbeta * 4 + 255) & ~(size_t)255) + nqt * 2;
+    if (tbytes > ws.tables_bytes) {
+        if (ws.tables) (void)hipFree(ws.tables);
+        ws.tables = nullptr;
+        ws.tables_bytes = 0;
+        if (hipMalloc(&ws.tables, tbytes) != hipSuccess) {
+            (void)hipGetLastError();
+            return LDPC_ERR_OOM;
+        }
+        ws.tables_bytes = tbytes;
+    }
+    float* betas = reinterpret_cast<float*>(ws.tables);
+    uint16_t* qtab = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(ws.tables) +
+                                                 ((nbeta * 4 + 255) & ~(size_t)255));
+    {
+        const size_t nthr = std::max(nbeta, lut ? nqt : (size_t)0);
+        hipLaunchKernelGGL(k_f5_tables, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s,
+                           b.alpha, b.beta, g.row_ptr, b.T, g.M, g.E, g.N, qmax, step, 1.0f / step,
+                           betas, lut ? qtab : nullptr);
+        if (hipGetLastError() != hipSuccess) return LDPC_ERR_HIP;
+    }
+    a.betas = betas;
+    a.qtab = qtab;
     const int nblocks = (int)((b.B + sh.cw - 1) / sh.cw);
     const float* au = b.alpha_ucn;
     switch (p.shape) {
