@@ -16,14 +16,14 @@ __all__ = [
     "NMSConfig", "ConfigError", "check_params",
     "DecoderWeights", "read_weight_file", "load_weights_reference_order", "expand_weights",
     "flat_weights", "create_mix_epoch", "quantize_host", "read_uncor_llr", "write_uncor_file",
-    "calc_ber_fer", "Counters", "loss_forward", "NMSDecoder", "Session", "build_session",
+    "calc_ber_fer", "Counters", "loss_forward", "NMSDecoder", "Decoder", "Session", "build_session",
     "compute_results", "fer_sweep",
 ]
 
 
 def __getattr__(name):
     # GPU-facing pieces import torch + the HIP extension lazily.
-    if name in ("NMSDecoder", "DecodeResult"):
+    if name in ("NMSDecoder", "Decoder", "DecodeResult"):
         from . import decoder
         return getattr(decoder, name)
     if name in ("Session", "build_session", "make_net_dict"):

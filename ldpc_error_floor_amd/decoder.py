@@ -19,7 +19,7 @@ from .code import TannerGraph
 from .config import DECODING_MS, DECODING_MS_NONUDGE, DECODING_QMS, VALID_Q_BITS
 from .weights import DecoderWeights
 
-__all__ = ["NMSDecoder", "DecodeResult", "KERNELS"]
+__all__ = ["NMSDecoder", "Decoder", "DecodeResult", "KERNELS"]
 
 KERNELS = {"auto": 0, "flood": 1, "fused": 2}
 
@@ -166,10 +166,13 @@ class NMSDecoder:
                          ptr(res.flags), stream.cuda_stream)
         return res
 
-    def awgn(self, B: int, sigma: float, seed: int, offset: int = 0, punct=(0, 0), short=(0, 0),
+    def awgn(self, B: int, sigma: float, seed: int, offset: int = 0, punct=None, short=None,
              out=None, stream=None):
-        """On-GPU AWGN LLRs [B, N*z] for the all-zero word (Philox, see ldpc_channel.hip)."""
+        """On-GPU AWGN LLRs [B, N*z] for the all-zero word (Philox, see ldpc_channel.hip).
+        ``punct`` / ``short`` default to the ranges the decoder was built with (``Decoder``)."""
         torch = self._torch
+        punct = getattr(self, "punct", (0, 0)) if punct is None else punct
+        short = getattr(self, "short", (0, 0)) if short is None else short
         if out is None:
             out = torch.empty((B, self.n_vars), dtype=torch.float32, device=self.device)
         if stream is None:
@@ -179,3 +182,36 @@ class NMSDecoder:
                                int(punct[1]), int(short[0]), int(short[1]), self.clip,
                                stream.cuda_stream)
         return out
+
+
+def Decoder(graph_txt: str, z: int, punct=(0, 0), short=(0, 0), sharing=(3, 0, 3),
+            decoding_type: int = DECODING_QMS, q_bit: int = 5, weights_txt: Optional[str] = None,
+            T: Optional[int] = None, target_node: int = 0, fixed_iter: int = 0,
+            clip_LLR: float = 20.0, device=None, kernel: str = "auto", B_max: int = 0) -> NMSDecoder:
+    """File-level constructor (SURVEY §8 b): a base-graph text file (``BaseGraph/*.txt``, read
+    like ``init_parameter``, ``Main_Functions.py:8-38``) and a weights file
+    (``Weights/*.txt``, ``Main_Functions.py:387-439``) -> an ``NMSDecoder``.
+
+    ``punct`` / ``short`` are the 1-based inclusive ranges of ``create_mix_epoch``
+    (``Print_Functions.py:29-72``); they belong to the channel, so they only become the
+    defaults of ``awgn``.  ``T`` defaults to the number of iterations the weight file holds;
+    without a weight file the decoder uses flat weights (alpha 1, beta 1) for ``T`` iterations.
+    """
+    from .code import load_base_graph
+    from .weights import expand_weights, read_weight_file, flat_weights
+    proto = load_base_graph(graph_txt)
+    g = TannerGraph(proto, int(z))
+    if weights_txt is not None:
+        wf = read_weight_file(weights_txt)
+        if T is None:
+            T = max(int(b.shape[0]) for b in wf.blocks.values()) if wf.blocks else 1
+        W = expand_weights(tuple(sharing), wf.blocks, int(T), g, fixed_iter)
+    else:
+        if T is None:
+            raise ValueError("T is required without a weights file")
+        W = flat_weights(g, int(T))
+    dec = NMSDecoder(proto, z, W, decoding_type, q_bit, target_node, clip_LLR, device=device,
+                     kernel=kernel, B_max=B_max)
+    dec.punct = (int(punct[0]), int(punct[1]))
+    dec.short = (int(short[0]), int(short[1]))
+    return dec

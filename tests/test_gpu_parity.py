@@ -93,3 +93,17 @@ def test_counters_only_decode_matches_reference(name, kernel, cuda_device):
     if c["exact"]:
         assert np.array_equal(res.counters.cpu().numpy(), counters_from_app(c["app"]))
         assert np.array_equal(res.flags.cpu().numpy(), flags_from_app(c["app"]))
+
+
+def test_file_level_decoder_matches_reference(cuda_device):
+    """Decoder(graph_txt, z, ..., weights_txt) (SURVEY §8 b) on the wman fixture."""
+    from ldpc_error_floor_amd.decoder import Decoder
+    c = load_case("wman_303_q5_snr2.0")
+    data = os.path.join(ROOT, "ldpc_error_floor_amd", "data")
+    dec = Decoder(os.path.join(data, "BaseGraph", "wman_N0576_R34_z24.txt"), 24,
+                  sharing=(3, 0, 3), decoding_type=2, q_bit=5,
+                  weights_txt=os.path.join(data, "Weights", "C0_wman_N0576_R34_z24_Opt_Weight_End20.txt"),
+                  device=cuda_device)
+    assert dec.T == 20
+    res = dec.decode(c["llr"], app=True)
+    assert np.array_equal(res.app.cpu().numpy(), c["app"])

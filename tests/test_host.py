@@ -186,3 +186,14 @@ def test_calc_ber_fer_contract():
 def test_loss_forward_type2():
     y = np.array([[-1.0, -2.0], [0.0, -1.0], [0.5, -3.0], [-1, -1]], np.float32)   # T=1, B=4
     assert metrics.loss_forward(y, 1, 4, 2) == pytest.approx((0 + 0.5 + 1 + 0) / 4)
+
+
+def test_file_level_decoder_refuses_cpu_device():
+    """No CPU fallback: the file-level constructor reads the files, then refuses a CPU device."""
+    import pytest
+    from ldpc_error_floor_amd.decoder import Decoder
+    data = os.path.join(ROOT, "ldpc_error_floor_amd", "data")
+    with pytest.raises(RuntimeError):
+        Decoder(os.path.join(data, "BaseGraph", "wman_N0576_R34_z24.txt"), 24, sharing=(3, 0, 3),
+                weights_txt=os.path.join(data, "Weights", "C0_wman_N0576_R34_z24_Opt_Weight_End20.txt"),
+                device="cpu")
