@@ -113,6 +113,20 @@ int ldpc_channel_awgn(float* llr_dev, int64_t B, int32_t n_vars, double sigma, u
                       int32_t punct_end, int32_t short_start, int32_t short_end, float clip_llr,
                       void* stream);
 
+/* Uncorrected-frame collection for the on-device sweep (replaces the host selection in
+   compute_results -> write_uncor_file, Print_Functions.py:155-156 and :120-126).
+   Writes the indices b < B with (frame_flags[b] & mask) == want into idx_dev[0..cap) (order
+   within the batch is not preserved: sort the few indices on the host) and the number of
+   matches (which may exceed cap) into *count_dev (zeroed by the call).  With the decoder's
+   frame_flags, mask = want = 1 selects the frames wrong at every iteration (uncor_flag). */
+int ldpc_collect_frames(const uint8_t* flags_dev, int64_t B, uint32_t mask, uint32_t want,
+                        int64_t* idx_dev, int64_t cap, int64_t* count_dev, void* stream);
+
+/* dst[r][:] = src[idx[r]][:] for r < n (n <= 65535 per call): the LLR rows of the collected
+   frames, on the device, before the copy to the host. */
+int ldpc_gather_rows(const float* src_dev, int64_t n_cols, const int64_t* idx_dev, int64_t n,
+                     float* dst_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,7 +24,8 @@ BUILD = os.path.join(PKG, "_build")
 ARCH = os.environ.get("LDPC_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["ldpc_capi.hip", "ldpc_flood.hip", "ldpc_fused.hip", "ldpc_fused3.hip",
-               "ldpc_fused4.hip", "ldpc_fused5.hip", "ldpc_channel.hip"]
+               "ldpc_fused4.hip", "ldpc_fused5.hip", "ldpc_channel.hip",
+               "ldpc_collect.hip"]
 HEADERS = ["ldpc_internal.h", "ldpc_fused.h"]
 LIB = os.path.join(PKG, "libldpc_nms.so")
 EXT = os.path.join(PKG, "_ldpc_nms" + sysconfig.get_config_var("EXT_SUFFIX"))

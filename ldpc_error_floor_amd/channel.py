@@ -17,7 +17,7 @@ import os
 import numpy as np
 
 __all__ = ["quantize_host", "create_mix_epoch", "read_uncor_llr", "write_uncor_file",
-           "load_uncor_inputs"]
+           "append_uncor_rows", "load_uncor_inputs"]
 
 
 def quantize_host(x, q_bit: int):
@@ -78,9 +78,17 @@ def write_uncor_file(uncor_flag, training_received_data, code_length, path="Unco
     """Append frames with ``uncor_flag == 1`` as 3 zero columns + negated LLRs (``%.1f``)."""
     sel = np.asarray(uncor_flag) == 1
     num = int(np.sum(sel))
-    data = -np.reshape(np.asarray(training_received_data)[sel, :, :], [num, code_length])
+    append_uncor_rows(np.reshape(np.asarray(training_received_data)[sel, :, :], [num, code_length]),
+                      path)
+
+
+def append_uncor_rows(llr_rows, path="Uncor.txt"):
+    """The row format of ``write_uncor_file`` (``Print_Functions.py:120-126``) for LLR rows
+    [n, N*z] already selected (e.g. collected on the GPU by ``NMSDecoder.collect_uncorrected``)."""
+    rows = np.asarray(llr_rows, np.float64)
+    num = rows.shape[0]
     with open(path, "a") as f:
-        np.savetxt(f, np.concatenate((np.zeros((num, 3)), data), axis=1), fmt="%.1f",
+        np.savetxt(f, np.concatenate((np.zeros((num, 3)), -rows), axis=1), fmt="%.1f",
                    delimiter="\t")
 
 

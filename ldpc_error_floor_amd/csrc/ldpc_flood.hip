@@ -177,10 +177,7 @@ __global__ void __launch_bounds__(256) k_vn_update(DevGraph g, Bufs p, int t) {
     if (tile >= p.ntiles) return;
     const int grp = uniform((int)(item - tile * ngroups));
     const int lane = threadIdx.x & 63;
-    const size_t tbase = (size_t)tile * TILE + 4 * lane;
     const float* Ct = p.c2v + (size_t)tile * g.n_edges * TILE + 4 * lane;
-    const float beta_next_row = 0.f;
-    (void)beta_next_row;
     const bool count = p.count != 0;
     bool valid[4];
 #pragma unroll

@@ -88,11 +88,6 @@ __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
-__device__ __forceinline__ int clampi(int x, int lo, int hi) {
-    int r;
-    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "s"(hi));
-    return r;
-}
 
 // ---- SEL layout: edge k -> byte of word k/4, counted from the last inserted edge ------------
 // A selector byte is 2*is_argmin + negative: the index of the edge's message inside P, so

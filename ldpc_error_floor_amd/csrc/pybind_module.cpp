@@ -135,6 +135,28 @@ PYBIND11_MODULE(_ldpc_nms, m) {
         py::arg("punct_end"), py::arg("short_start"), py::arg("short_end"), py::arg("clip"),
         py::arg("stream") = 0);
     m.def(
+        "collect_frames",
+        [](uintptr_t flags, int64_t B, uint32_t mask, uint32_t want, uintptr_t idx, int64_t cap,
+           uintptr_t count, uintptr_t stream) {
+            check(ldpc_collect_frames(reinterpret_cast<const uint8_t*>(flags), B, mask, want,
+                                      reinterpret_cast<int64_t*>(idx), cap,
+                                      reinterpret_cast<int64_t*>(count),
+                                      reinterpret_cast<void*>(stream)),
+                  "ldpc_collect_frames");
+        },
+        py::arg("flags"), py::arg("B"), py::arg("mask"), py::arg("want"), py::arg("idx"),
+        py::arg("cap"), py::arg("count"), py::arg("stream") = 0);
+    m.def(
+        "gather_rows",
+        [](uintptr_t src, int64_t n_cols, uintptr_t idx, int64_t n, uintptr_t dst, uintptr_t stream) {
+            check(ldpc_gather_rows(reinterpret_cast<const float*>(src), n_cols,
+                                   reinterpret_cast<const int64_t*>(idx), n,
+                                   reinterpret_cast<float*>(dst), reinterpret_cast<void*>(stream)),
+                  "ldpc_gather_rows");
+        },
+        py::arg("src"), py::arg("n_cols"), py::arg("idx"), py::arg("n"), py::arg("dst"),
+        py::arg("stream") = 0);
+    m.def(
         "kernel_info",
         [](Ctx& c, int T, int decoding_type, int q_bit, int target_bits, int kernel) {
             ldpc_decode_params p = make_params(T, decoding_type, q_bit, target_bits, 20.f, kernel);

@@ -155,7 +155,11 @@ class NMSDecoder:
             if counters.dtype != torch.int64 or counters.numel() < 4 or counters.device != dev:
                 raise ValueError("counters must be an int64[4] tensor on the decoder's device")
             res.counters = counters
-        if flags:
+        if isinstance(flags, torch.Tensor):                 # caller-owned uint8 [>= B]
+            if flags.dtype != torch.uint8 or flags.device != dev or flags.numel() < B:
+                raise ValueError("flags tensor must be uint8 on the decoder's device, >= B long")
+            res.flags = flags
+        elif flags:
             res.flags = torch.empty(B, dtype=torch.uint8, device=dev)
         if stream is None:
             stream = torch.cuda.current_stream(dev)
@@ -165,6 +169,31 @@ class NMSDecoder:
                          ptr(res.app), ptr(res.hard), ptr(res.synd), ptr(res.counters),
                          ptr(res.flags), stream.cuda_stream)
         return res
+
+    def collect_uncorrected(self, flags, llr, stream=None):
+        """LLR rows (host float32 [n, N*z], batch order) of the frames wrong at every iteration
+        (``frame_flags`` bit 0 = the reference's ``uncor_flag``), compacted on the GPU by
+        ``ldpc_collect_frames`` + ``ldpc_gather_rows``; only the n rows cross PCIe."""
+        torch = self._torch
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        B = int(flags.shape[0])
+        idx = torch.empty(max(B, 1), dtype=torch.int64, device=self.device)
+        cnt = torch.empty(1, dtype=torch.int64, device=self.device)
+        self._ext.collect_frames(flags.data_ptr(), B, 1, 1, idx.data_ptr(), B, cnt.data_ptr(),
+                                 stream.cuda_stream)
+        stream.synchronize()
+        n = int(cnt.item())
+        if n == 0:
+            return np.zeros((0, self.n_vars), np.float32)
+        sel = torch.sort(idx[:n]).values.contiguous()     # batch order, as the reference writes
+        llr = llr.reshape(llr.shape[0], -1)
+        rows = torch.empty((n, self.n_vars), dtype=torch.float32, device=self.device)
+        for s0 in range(0, n, 65535):
+            s1 = min(n, s0 + 65535)
+            self._ext.gather_rows(llr.data_ptr(), self.n_vars, sel[s0:].data_ptr(), s1 - s0,
+                                  rows[s0:].data_ptr(), stream.cuda_stream)
+        return rows.cpu().numpy()
 
     def awgn(self, B: int, sigma: float, seed: int, offset: int = 0, punct=None, short=None,
              out=None, stream=None):

@@ -18,7 +18,7 @@ import time
 
 import numpy as np
 
-from .channel import create_mix_epoch, read_uncor_llr, write_uncor_file
+from .channel import append_uncor_rows, create_mix_epoch, read_uncor_llr, write_uncor_file
 from .metrics import Counters, calc_ber_fer
 
 __all__ = ["compute_results", "fer_sweep", "shard_range"]
@@ -73,9 +73,14 @@ def shard_range(total: int, rank: int, world: int):
 
 
 def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T=None,
-              punct=(0, 0), short=(0, 0), kernel=None, group=None, progress=None):
+              punct=(0, 0), short=(0, 0), kernel=None, group=None, progress=None,
+              uncor_path=None):
     """Decode ``n_codewords`` per SNR point (split across ranks) with GPU LLRs and device
-    counters.  Returns a list of ``Counters`` (global totals on every rank)."""
+    counters.  Returns a list of ``Counters`` (global totals on every rank).
+
+    ``uncor_path``: append the frames wrong at every iteration to this file in the
+    ``Uncor.txt`` format (``sampling_type == 2``, ``Print_Functions.py:155-156``), collected on
+    the GPU; with several ranks each rank writes ``<uncor_path>.rank<r>``."""
     import torch
     import torch.distributed as dist
     dist_on = dist.is_available() and dist.is_initialized()
@@ -86,13 +91,20 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
     counters = torch.zeros((sigmas.size, 4), dtype=torch.int64, device=dev)
     begin, end = shard_range(int(n_codewords), rank, world)
     llr = torch.empty((batch, decoder.n_vars), dtype=torch.float32, device=dev)
+    flags = torch.empty(batch, dtype=torch.uint8, device=dev) if uncor_path else None
+    upath = uncor_path if (uncor_path is None or world == 1) else f"{uncor_path}.rank{rank}"
     for si, sigma in enumerate(sigmas):
         pos = begin
         while pos < end:
             b = min(batch, end - pos)
             decoder.awgn(b, float(sigma), seed + 7919 * si, offset=pos, punct=punct, short=short,
                          out=llr[:b])
-            decoder.decode(llr[:b], T=T, app=False, counters=counters[si], kernel=kernel)
+            decoder.decode(llr[:b], T=T, app=False, counters=counters[si], kernel=kernel,
+                           flags=None if flags is None else flags[:b])
+            if flags is not None:
+                rows = decoder.collect_uncorrected(flags[:b], llr[:b])
+                if rows.shape[0]:
+                    append_uncor_rows(rows, upath)
             pos += b
             if progress:
                 progress(si, pos - begin, end - begin)

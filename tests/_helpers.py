@@ -40,7 +40,8 @@ class OracleDecoder:
         self.device = torch.device("cpu")
         self.g = nms_oracle.lifted_edges(self.proto, z)
 
-    def decode(self, llr, T=None, app=True, counters=None, target_bits=None, kernel=None, **kw):
+    def decode(self, llr, T=None, app=True, counters=None, target_bits=None, kernel=None,
+               flags=None, **kw):
         T = T or self.T
         x = np.asarray(llr.cpu().numpy() if hasattr(llr, "cpu") else llr, np.float32)
         out = nms_oracle.decode(x.reshape(x.shape[0], -1), self.proto, self.z, self.W.alpha,
@@ -49,7 +50,13 @@ class OracleDecoder:
         a = out["app"][:, :, :nt]
         if counters is not None:
             counters += self.torch.from_numpy(counters_from_app(a))
+        if flags is not None and not isinstance(flags, bool):
+            flags.copy_(self.torch.from_numpy(flags_from_app(a)))
         return SimpleNamespace(app=self.torch.from_numpy(np.ascontiguousarray(a)) if app else None)
+
+    def collect_uncorrected(self, flags, llr):
+        sel = (flags.cpu().numpy() & 1) == 1
+        return np.asarray(llr.cpu().numpy(), np.float32).reshape(llr.shape[0], -1)[sel]
 
     def awgn(self, B, sigma, seed, offset=0, punct=(0, 0), short=(0, 0), out=None, **kw):
         # deterministic per global codeword index (like the GPU Philox stream)

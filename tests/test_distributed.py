@@ -72,3 +72,25 @@ def test_gloo_world2_equals_single_process():
         assert p.exitcode == 0
     assert got[0] == got[1] == single
     assert single[0][1] > 0           # the low-SNR point has frame errors
+
+
+def test_sweep_collects_uncorrected_frames(tmp_path):
+    """fer_sweep(uncor_path=...) appends exactly the frames wrong at every iteration, in the
+    Uncor.txt row format, in stream order (host logic; the GPU compaction is tested on GPU)."""
+    from ldpc_error_floor_amd.channel import write_uncor_file
+    dec = _make_decoder()
+    path = tmp_path / "Uncor.txt"
+    res = fer_sweep(dec, SIGMAS[:1], N_CW, BATCH, seed=1076, uncor_path=str(path))
+    rows = np.loadtxt(path, delimiter="\t", ndmin=2)
+    assert rows.shape == (res[0].frame_err_all, 3 + dec.n_vars)
+    # the same frames through the reference-format writer on host LLRs
+    expect = tmp_path / "expect.txt"
+    for pos in range(0, N_CW, BATCH):
+        b = min(BATCH, N_CW - pos)
+        llr = dec.awgn(b, SIGMAS[0], 1076, offset=pos)
+        flags = torch.zeros(b, dtype=torch.uint8)
+        dec.decode(llr, app=False, flags=flags)
+        uncor = (flags.numpy() & 1).astype(np.float64)
+        if uncor.sum():
+            write_uncor_file(uncor, llr.numpy().reshape(b, dec.N, dec.z), dec.n_vars, str(expect))
+    assert path.read_text() == expect.read_text()

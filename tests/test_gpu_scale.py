@@ -141,3 +141,27 @@ def test_fer_sweep_matches_manual(cuda_device):
         r = res[si]
         assert cnt.cpu().tolist() == [r.bit_err_last, r.frame_err_last, r.frame_err_all, r.loss2]
     assert res[0].fer_last > res[1].fer_last
+
+
+def test_collect_uncorrected_on_device(cuda_device, tmp_path):
+    """ldpc_collect_frames + ldpc_gather_rows: the frames wrong at every iteration, in batch
+    order, and fer_sweep(uncor_path=...) writes one row per such frame."""
+    import torch
+    from ldpc_error_floor_amd.fer import fer_sweep
+    dec, cp = _wman(cuda_device)
+    B = 3001
+    llr = dec.awgn(B, float(cp.sigma(2.0)), seed=11)
+    r = dec.decode(llr, app=False, flags=True)
+    flags = r.flags
+    rows = dec.collect_uncorrected(flags, llr)
+    sel = (flags.cpu().numpy() & 1) == 1
+    assert rows.shape[0] == int(sel.sum()) > 0
+    assert np.array_equal(rows, llr.cpu().numpy()[sel])
+    # no matches -> empty
+    none = torch.zeros(B, dtype=torch.uint8, device=cuda_device)
+    assert dec.collect_uncorrected(none, llr).shape == (0, dec.n_vars)
+    path = tmp_path / "Uncor.txt"
+    res = fer_sweep(dec, [float(cp.sigma(2.0))], 5000, 2048, seed=3, uncor_path=str(path))
+    lines = np.loadtxt(path, delimiter="\t", ndmin=2)
+    assert lines.shape == (res[0].frame_err_all, 3 + dec.n_vars)
+    assert np.all(lines[:, :3] == 0)
