@@ -44,6 +44,7 @@ enum ldpc_status {
 };
 
 enum ldpc_decoding_type {       /* decoding_type of main_Base.py:27 */
+    LDPC_DEC_SP = 0,            /* sum-product: tanh / atanh check update (flood kernel) */
     LDPC_DEC_MS = 1,            /* min-sum fp32, messages clipped to +-clip_llr */
     LDPC_DEC_QMS = 2,           /* quantized min-sum on the q_bit grid */
     LDPC_DEC_MS_NONUDGE = 3     /* min-sum without the 0 -> 1e-4 nudge */

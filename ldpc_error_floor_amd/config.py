@@ -16,7 +16,7 @@ import numpy as np
 __all__ = ["NMSConfig", "ConfigError", "check_params", "DECODING_SP", "DECODING_MS",
            "DECODING_QMS", "DECODING_MS_NONUDGE", "VALID_Q_BITS"]
 
-DECODING_SP = 0          # sum-product (tanh/atanh); not built by this framework yet
+DECODING_SP = 0          # sum-product (tanh/atanh), flood kernel (Main_Functions.py:238-245)
 DECODING_MS = 1          # min-sum, fp32, clip +-clip_LLR
 DECODING_QMS = 2         # quantized min-sum (q_bit grid)
 DECODING_MS_NONUDGE = 3  # min-sum without the 0 -> 1e-4 nudge (Main_Functions.py:229,247)
@@ -77,9 +77,8 @@ class NMSConfig:
     def validate(self):
         self.SNR_Matrix = check_params(self.sampling_type, self.SNR_Matrix, self.sharing,
                                        self.iters_max, self.fixed_iter, self.iter_step)
-        if self.decoding_type not in (DECODING_MS, DECODING_QMS, DECODING_MS_NONUDGE):
-            raise ConfigError(f"decoding_type {self.decoding_type} is not supported "
-                              "(0 = sum-product is not built)")
+        if self.decoding_type not in (DECODING_SP, DECODING_MS, DECODING_QMS, DECODING_MS_NONUDGE):
+            raise ConfigError(f"decoding_type {self.decoding_type} is not supported")
         if self.decoding_type == DECODING_QMS and self.q_bit not in VALID_Q_BITS:
             raise ConfigError(f"q_bit {self.q_bit} not in {VALID_Q_BITS}")
         return self

@@ -16,7 +16,7 @@ import numpy as np
 
 from . import _native
 from .code import TannerGraph
-from .config import DECODING_MS, DECODING_MS_NONUDGE, DECODING_QMS, VALID_Q_BITS
+from .config import DECODING_MS, DECODING_MS_NONUDGE, DECODING_QMS, DECODING_SP, VALID_Q_BITS
 from .weights import DecoderWeights
 
 __all__ = ["NMSDecoder", "Decoder", "DecodeResult", "KERNELS"]
@@ -51,7 +51,7 @@ class NMSDecoder:
                  kernel: str = "auto", B_max: int = 0):
         import torch
         self._torch = torch
-        if decoding_type not in (DECODING_MS, DECODING_QMS, DECODING_MS_NONUDGE):
+        if decoding_type not in (DECODING_SP, DECODING_MS, DECODING_QMS, DECODING_MS_NONUDGE):
             raise ValueError(f"decoding_type {decoding_type} not supported")
         if decoding_type == DECODING_QMS and q_bit not in VALID_Q_BITS:
             raise ValueError(f"q_bit {q_bit} not in {VALID_Q_BITS}")

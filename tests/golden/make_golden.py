@@ -364,6 +364,20 @@ def main():
                      3.0, flat={0: 0.75, 2: 1.0})
         decoder_case(MF, PF, "polar_222_q5_snr3.0", "Polar_64_48", 1, [2, 2, 2], 2, 5, 10, 16,
                      3.0, random_weights=(0.5, 1.0))
+    if want("sp"):
+        # sum-product (decoding_type 0): float, checked with a documented tolerance
+        g_wman = decoder_case(MF, PF, "wman_303_sp_snr2.5", "wman_N0576_R34_z24", 24,
+                              [3, 0, 3], 0, 5, 10, 16, 2.5,
+                              blocks={0: wman_blocks[0][:10], 2: wman_blocks[2][:10]}, g=g_wman)
+        g_wman = decoder_case(MF, PF, "wman_333_sp_snr2.0", "wman_N0576_R34_z24", 24,
+                              [3, 3, 3], 0, 5, 10, 8, 2.0,
+                              blocks={k: wman_blocks[k][:10] for k in (0, 1, 2)}, g=g_wman)
+        _, gb = read_blocks(os.path.join(
+            REF, "Results/5G/5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640_Weight_End50.txt"))
+        decoder_case(MF, PF, "g5bg2_222_sp_snr2.0",
+                     "5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640", 64, [2, 2, 2], 0, 5,
+                     10, 8, 2.0, blocks={k: v[:10] for k, v in gb.items()}, ps=1, pe=128,
+                     ss=513, se=640)
     if want("results"):
         results_anchor(MF, PF)
 

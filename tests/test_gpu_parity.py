@@ -10,6 +10,12 @@ from _helpers import counters_from_app, flags_from_app
 pytestmark = pytest.mark.gpu
 KERNEL_NAMES = ["flood", "fused"]
 MS_ATOL = 1e-3
+# Sum-product (decoding_type 0): tanh/atanh in fp32 differ by ulps between the GPU and numpy,
+# and atanh near the +-(1 - 1e-7) clip amplifies a 1-ulp product difference to ~0.25, which
+# then propagates.  Measured on the SP fixtures: t <= 1 within 1e-6, p99 <= 2e-3 and max
+# <= 0.66 at t = 9, no hard-decision flip.  The bar: t <= 1 within SP_ATOL_EARLY, every
+# iteration p99 <= SP_P99 and max <= SP_MAX, hard decisions exact where |APP_ref| >= SP_HARD.
+SP_ATOL_EARLY, SP_P99, SP_MAX, SP_HARD = 1e-3, 1e-2, 1.0, 0.1
 
 
 def _decoder(c, kernel, device):
@@ -41,6 +47,13 @@ def test_decoder_matches_reference(name, kernel, cuda_device):
     if c["exact"]:
         assert np.array_equal(app, ref), f"max |diff| {np.abs(app - ref).max()}"
         hard_ok = np.ones(c["hard"].shape, bool)
+    elif c["dt"] == 0:
+        d = np.abs(app - ref)
+        np.testing.assert_allclose(app[:2], ref[:2], rtol=0, atol=SP_ATOL_EARLY)
+        for t in range(c["T"]):
+            assert np.percentile(d[t], 99) <= SP_P99 and d[t].max() <= SP_MAX, (t, d[t].max())
+        hard_ok = np.ones(c["hard"].shape, bool)
+        hard_ok[:, :, :c["Nt"] * c["z"]] = np.abs(ref) >= SP_HARD
     else:
         np.testing.assert_allclose(app, ref, rtol=0, atol=MS_ATOL)
         hard_ok = np.ones(c["hard"].shape, bool)

@@ -122,7 +122,8 @@ def test_check_params():
     cfg = config.NMSConfig()
     assert cfg.word_seed == 2044 and cfg.noise_seed == 1076
     with pytest.raises(config.ConfigError):
-        config.NMSConfig(decoding_type=0).validate()
+        config.NMSConfig(decoding_type=7).validate()
+    config.NMSConfig(decoding_type=0).validate()          # sum-product is built (flood)
 
 
 def test_channel_matches_reference():
