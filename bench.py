@@ -7,12 +7,17 @@ AWGN LLRs (3.5 dB, QMS q=5) are generated on the GPU before the timed region.
 ``python bench.py --gpus N --steps K --warmup W``; N > 1 is launched by torch.distributed.run
 (one rank per GPU, weak scaling: every rank decodes its own B codewords).
 
+``--config C3|C4|C5`` runs the SURVEY §8 d companion workloads instead (802.11n, 5G BG2,
+5G BG1); the default C2 line is the one the driver records.
+
 Prints ONE JSON line (rank 0).  Besides the driver's fields it carries:
   roofline      dominant kernel vs HBM: achieved = SURVEY §8 d bytes/codeword x B / kernel
                 time (HIP events on the decode stream); traffic = PMC HBM bytes per launch
                 when profiles/traffic_<kernel>.json exists (see tools/profile.sh), else null
   cpu_baseline  the dense TF-graph-equivalent numpy restatement of the reference decoder
                 (oracle/nms_dense.py) on the C1 sample (B=120, T=20, 3.5 dB), rank 0, N=1
+  e2e_with_rng  the same K steps timed with the on-GPU AWGN generation of each batch inside
+                the timed region (SURVEY §8 d "separately time end-to-end")
 """
 from __future__ import annotations
 
@@ -29,8 +34,24 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
-GRAPH = "wman_N0576_R34_z24"
-WEIGHTS = "C0_wman_N0576_R34_z24_Opt_Weight_End20.txt"
+DATA = os.path.join(ROOT, "ldpc_error_floor_amd", "data")
+
+# SURVEY.md §8 d workloads.  C2 is BASELINE.json's configs[1] (the driver's line).
+CONFIGS = {
+    "C2": dict(label="wman N576 R3/4", graph="wman_N0576_R34_z24", z=24, T=20, sharing=(3, 0, 3),
+               weights="Weights/C0_wman_N0576_R34_z24_Opt_Weight_End20.txt", snr=3.5),
+    "C3": dict(label="802.11n N648 R5/6", graph="802_11n_N648_R56_z27", z=27, T=50,
+               sharing=(3, 3, 3), weights="Results/WIFI/Weights_Iter50.txt", snr=3.5),
+    "C4": dict(label="5G BG2 n1024 R1/2", graph="5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640",
+               z=64, T=20, sharing=(2, 2, 2),
+               weights="Results/5G/5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640_Weight_End50.txt",
+               snr=2.0, punct=(1, 128), short=(513, 640)),
+    "C5": dict(label="5G BG1 n2112 R0.73", graph="5G_LDPC_R0.73_n_dec2304_n2112_k1536_z72_s1537_1584",
+               z=72, T=50, sharing=(3, 0, 3), flat=(0.75, 1.0), snr=3.0, punct=(1, 144),
+               short=(1537, 1584)),
+}
+GRAPH = CONFIGS["C2"]["graph"]
+WEIGHTS = os.path.basename(CONFIGS["C2"]["weights"])
 
 
 def survey_bytes_per_cw(E, N, z, T, ucn=False):
@@ -38,15 +59,24 @@ def survey_bytes_per_cw(E, N, z, T, ucn=False):
     return T * (3 * E * z * 4 + 4 * N * z * 4 + N * z // 8 + (N * z // 8 if ucn else 0))
 
 
-def load_problem(T=20):
+def load_problem(T=None, config="C2"):
+    """(proto, TannerGraph, DecoderWeights, CodeParams) of a SURVEY §8 d workload."""
     from ldpc_error_floor_amd.code import CodeParams, TannerGraph, load_base_graph
-    from ldpc_error_floor_amd.weights import expand_weights, read_weight_file
-    data = os.path.join(ROOT, "ldpc_error_floor_amd", "data")
-    proto = load_base_graph(os.path.join(data, "BaseGraph", GRAPH + ".txt"))
-    g = TannerGraph(proto, 24)
-    wf = read_weight_file(os.path.join(data, "Weights", WEIGHTS))
-    W = expand_weights((3, 0, 3), {0: wf.blocks[0], 2: wf.blocks[2]}, T, g)
-    return proto, g, W, CodeParams(proto, 24)
+    from ldpc_error_floor_amd.weights import expand_weights, flat_weights, read_weight_file
+    c = CONFIGS[config]
+    T = c["T"] if T is None else T
+    z = c["z"]
+    proto = load_base_graph(os.path.join(DATA, "BaseGraph", c["graph"] + ".txt"))
+    g = TannerGraph(proto, z)
+    if "weights" in c:
+        wf = read_weight_file(os.path.join(DATA, c["weights"]))
+        blocks = {k: v for k, v in wf.blocks.items() if c["sharing"][k] > 0}
+        W = expand_weights(c["sharing"], blocks, T, g)
+    else:                         # no trained weights ship for this code: flat [3,0,3]
+        W = flat_weights(g, T, alpha=c["flat"][0], beta=c["flat"][1])
+    ps, pe = c.get("punct", (0, 0))
+    ss, se = c.get("short", (0, 0))
+    return proto, g, W, CodeParams(proto, z, ps, pe, ss, se)
 
 
 def cpu_baseline(proto, g, W, cp, B=120, T=20, snr=3.5):
@@ -89,8 +119,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU per step")
     ap.add_argument("--kernel", default="auto", choices=["auto", "flood", "fused"])
-    ap.add_argument("--snr", type=float, default=3.5)
-    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--snr", type=float, default=None, help="default: the config's SNR")
+    ap.add_argument("--iters", type=int, default=None, help="default: the config's T")
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--all-kernels", action="store_true",
                     help="also time the non-default kernel and report it under 'kernels'")
@@ -108,14 +139,18 @@ def main():
     torch.cuda.set_device(dev)
 
     from ldpc_error_floor_amd.decoder import NMSDecoder
-    T = args.iters
-    proto, g, W, cp = load_problem(T)
-    sigma = float(cp.sigma(args.snr))
+    cfg = CONFIGS[args.config]
+    T = cfg["T"] if args.iters is None else args.iters
+    snr = cfg["snr"] if args.snr is None else args.snr
+    z = cfg["z"]
+    punct, short = cfg.get("punct", (0, 0)), cfg.get("short", (0, 0))
+    proto, g, W, cp = load_problem(T, args.config)
+    sigma = float(cp.sigma(snr))
     B = args.batch
 
-    def run(kernel):
-        dec = NMSDecoder(proto, 24, W, 2, 5, device=dev, kernel=kernel, B_max=B)
-        llr = dec.awgn(B, sigma, seed=1076, offset=rank * B)          # resident in HBM
+    def run(kernel, e2e=False):
+        dec = NMSDecoder(proto, z, W, 2, 5, device=dev, kernel=kernel, B_max=B)
+        llr = dec.awgn(B, sigma, seed=1076, offset=rank * B, punct=punct, short=short)  # in HBM
         counters = torch.zeros(4, dtype=torch.int64, device=dev)
         name = dec.kernel_info(T)[1]
         stream = torch.cuda.current_stream(dev)
@@ -129,7 +164,10 @@ def main():
         counters.zero_()
         t0 = time.perf_counter()
         ev0.record(stream)
-        for _ in range(args.steps):
+        for i in range(args.steps):
+            if e2e:                 # the batch's AWGN generation inside the timed region
+                dec.awgn(B, sigma, seed=1076 + i + 1, offset=rank * B, punct=punct, short=short,
+                         out=llr)
             dec.decode(llr, T=T, app=False, counters=counters)
         ev1.record(stream)
         torch.cuda.synchronize(dev)
@@ -147,20 +185,22 @@ def main():
                     counters=cnt.cpu().tolist(), design_bytes=dec.kernel_info(T)[0])
 
     primary = run(args.kernel)
+    e2e = run(args.kernel, e2e=True)
     extra = {}
     if args.all_kernels:
         for k in ("flood", "fused"):
-            if k != primary["name"]:
-                try:
-                    r = run(k)
-                    extra[r["name"]] = {"codewords_per_s": round(world * B * args.steps / r["elapsed"], 1),
-                                        "ms_per_step": round(1e3 * r["elapsed"] / args.steps, 3)}
-                except RuntimeError as e:
-                    extra[k] = {"error": str(e)}
+            try:
+                r = run(k)
+            except RuntimeError as e:
+                extra[k] = {"error": str(e)}
+                continue
+            if r["name"] != primary["name"]:
+                extra[r["name"]] = {"codewords_per_s": round(world * B * args.steps / r["elapsed"], 1),
+                                    "ms_per_step": round(1e3 * r["elapsed"] / args.steps, 3)}
 
     t = primary["elapsed"]
     value = world * B * args.steps / t
-    bytes_cw = survey_bytes_per_cw(g.E, g.N, 24, T)
+    bytes_cw = survey_bytes_per_cw(g.E, g.N, z, T, ucn=cfg["sharing"][1] > 0)
     achieved = bytes_cw * B / (primary["kernel_ms"] / 1e3) / 1e9
     traffic = None
     safe = "".join(ch if (ch.isalnum() or ch in "_.-") else "_" for ch in primary["name"])
@@ -175,8 +215,13 @@ def main():
             traffic = None
     c = primary["counters"]
     n_frames = world * B * args.steps
+    wdesc = (f"trained weights ({os.path.basename(cfg['weights'])})" if "weights" in cfg
+             else f"flat weights alpha={cfg['flat'][0]} beta={cfg['flat'][1]} (none ship)")
+    pdesc = "".join([f", puncture {punct[0]}-{punct[1]}" if punct[0] else "",
+                     f", shorten {short[0]}-{short[1]}" if short[0] else ""])
+    sh = ",".join(str(x) for x in cfg["sharing"])
     out = {
-        "metric": "decoded codewords/sec, wman N576 R3/4, 20 NMS iters",
+        "metric": f"decoded codewords/sec, {cfg['label']}, {T} NMS iters",
         "value": round(value, 1),
         "unit": "codewords/s",
         "n_gpus": world,
@@ -187,9 +232,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32" if primary["name"] == "flood" else "i32",
-        "data": "synthetic (on-GPU Philox AWGN, all-zero codeword, 3.5 dB, QMS q=5 LLRs)",
-        "config": {"workload": f"{GRAPH} QMS q5 T={T} sharing [3,0,3] trained weights "
-                               f"({WEIGHTS}), B={B} codewords/GPU/step @ {args.snr} dB",
+        "data": f"synthetic (on-GPU Philox AWGN, all-zero codeword, {snr} dB, QMS q=5 LLRs)",
+        "config": {"workload": f"{args.config}: {cfg['graph']} QMS q5 T={T} sharing [{sh}] "
+                               f"{wdesc}{pdesc}, B={B} codewords/GPU/step @ {snr} dB",
                    "batch_per_gpu": B, "iterations": T, "kernel": primary["name"],
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -202,11 +247,13 @@ def main():
                              "time (HIP events); for the fused kernel this is an effective "
                              "figure (its real HBM traffic is design_bytes_per_cw)"},
         "fer_at_snr": {"frames": n_frames, "fer_last": c[1] / n_frames,
-                       "ber_last": c[0] / (n_frames * g.N * 24)},
+                       "ber_last": c[0] / (n_frames * g.N * z)},
     }
+    out["e2e_with_rng"] = {"codewords_per_s": round(world * B * args.steps / e2e["elapsed"], 1),
+                           "ms_per_step": round(1e3 * e2e["elapsed"] / args.steps, 3)}
     if extra:
         out["kernels"] = extra
-    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+    if world == 1 and rank == 0 and not args.no_cpu_baseline and args.config == "C2":
         out["cpu_baseline"] = cpu_baseline(proto, g, W, cp, T=T)
     if rank == 0:
         print(json.dumps(out), flush=True)
