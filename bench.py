@@ -16,8 +16,9 @@ Prints ONE JSON line (rank 0).  Besides the driver's fields it carries:
                 when profiles/traffic_<kernel>.json exists (see tools/profile.sh), else null
   cpu_baseline  the dense TF-graph-equivalent numpy restatement of the reference decoder
                 (oracle/nms_dense.py) on the C1 sample (B=120, T=20, 3.5 dB), rank 0, N=1
-  e2e_with_rng  the same K steps timed with the on-GPU AWGN generation of each batch inside
-                the timed region (SURVEY §8 d "separately time end-to-end")
+  e2e_with_rng  K steps that each draw a fresh AWGN batch inside the timed region
+                (ldpc_decode_awgn: generated in the decoder's prologue; SURVEY §8 d
+                "separately time end-to-end with GPU RNG and counters")
 """
 from __future__ import annotations
 
@@ -165,10 +166,11 @@ def main():
         t0 = time.perf_counter()
         ev0.record(stream)
         for i in range(args.steps):
-            if e2e:                 # the batch's AWGN generation inside the timed region
-                dec.awgn(B, sigma, seed=1076 + i + 1, offset=rank * B, punct=punct, short=short,
-                         out=llr)
-            dec.decode(llr, T=T, app=False, counters=counters)
+            if e2e:                 # a fresh AWGN batch per step, generated by the decoder
+                dec.decode_awgn(B, sigma, seed=1076 + i + 1, offset=rank * B, punct=punct,
+                                short=short, T=T, counters=counters)
+            else:
+                dec.decode(llr, T=T, app=False, counters=counters)
         ev1.record(stream)
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()

@@ -108,11 +108,30 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
    writes llr_dev [B][n_vars] f32 = Q(2(sigma*n - 1)/sigma^2) with punctured (1-based bits
    punct_start..punct_end, 0 = none) -> 0 and shortened -> -clip_llr.  n ~ N(0,1) from a
    counter-based Philox stream indexed by (seed, offset + b, element): shards generated with
-   their global codeword offset reproduce the single-GPU stream. */
+   their global codeword offset reproduce the single-GPU stream.  fp32 arithmetic with a 53-bit
+   uniform under the logarithm (tails to ~8.6 sigma); see csrc/ldpc_awgn.h. */
 int ldpc_channel_awgn(float* llr_dev, int64_t B, int32_t n_vars, double sigma, uint64_t seed,
                       int64_t offset, int32_t decoding_type, int32_t q_bit, int32_t punct_start,
                       int32_t punct_end, int32_t short_start, int32_t short_end, float clip_llr,
                       void* stream);
+
+/* In-decoder channel for throughput sweeps (SURVEY §8 f rank 1): the LLRs of the B codewords
+   are generated by the same Philox AWGN generator as ldpc_channel_awgn (same seed, global
+   codeword offset, puncture/shorten) and decoded without touching HBM (fused v5 generates them
+   in the kernel prologue; other kernels generate into a context buffer first).  The result is
+   identical to ldpc_channel_awgn followed by ldpc_decode.  Replaces create_mix_epoch +
+   sess.run in the compute_results loop (Print_Functions.py:29-72, :130-165). */
+typedef struct ldpc_channel_params {
+    double sigma;                 /* noise standard deviation (SNR -> sigma: init_parameter) */
+    uint64_t seed;
+    int64_t offset;               /* global index of the batch's first codeword */
+    int32_t punct_start, punct_end, short_start, short_end;   /* 1-based, 0 = none */
+    int32_t reserved[4];
+} ldpc_channel_params;
+
+int ldpc_decode_awgn(ldpc_ctx* ctx, int64_t B, const ldpc_decode_params* params,
+                     const ldpc_channel_params* channel, const ldpc_decode_outputs* outputs,
+                     void* stream);
 
 /* Uncorrected-frame collection for the on-device sweep (replaces the host selection in
    compute_results -> write_uncor_file, Print_Functions.py:155-156 and :120-126).

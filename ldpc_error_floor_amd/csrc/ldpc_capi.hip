@@ -5,6 +5,7 @@
 #include <new>
 #include <vector>
 
+#include "ldpc_awgn.h"
 #include "ldpc_internal.h"
 #include "ldpc_fused.h"
 
@@ -40,6 +41,9 @@ struct ldpc_ctx {
     int32_t* biterr = nullptr;
     // fused workspace
     FusedWorkspace fused{};
+    // LLR buffer for ldpc_decode_awgn when the kernel cannot generate in its prologue
+    float* llr_scratch = nullptr;
+    int64_t llr_scratch_n = 0;
 };
 
 namespace {
@@ -351,8 +355,51 @@ int ldpc_ctx_destroy(ldpc_ctx* c) {
     dev_free(c->ch); dev_free(c->Tv); dev_free(c->c2v); dev_free(c->hd);
     dev_free(c->wrong); dev_free(c->anypos); dev_free(c->biterr);
     fused_free(c->fused);
+    if (c->llr_scratch) (void)hipFree(c->llr_scratch);
     delete c;
     return LDPC_OK;
+}
+
+static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
+                       const ldpc_decode_outputs* o, void* stream, const AwgnParams* gen);
+
+int ldpc_decode(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
+                const ldpc_decode_outputs* o, void* stream) {
+    if (!llr_dev) return LDPC_ERR_ARG;
+    return decode_impl(c, llr_dev, B, p, o, stream, nullptr);
+}
+
+int ldpc_decode_awgn(ldpc_ctx* c, int64_t B, const ldpc_decode_params* p,
+                     const ldpc_channel_params* ch, const ldpc_decode_outputs* o, void* stream) {
+    if (!c || !p || !ch || !(ch->sigma > 0.0) || ch->offset < 0) return LDPC_ERR_ARG;
+    if (B <= 0 || B > c->B_max) return LDPC_ERR_STATE;
+    const AwgnParams a = make_awgn(ch->sigma, ch->seed, ch->offset, p->decoding_type, p->q_bit,
+                                   ch->punct_start, ch->punct_end, ch->short_start, ch->short_end,
+                                   p->clip_llr);
+    int st = decode_impl(c, nullptr, B, p, o, stream, &a);
+    if (st != LDPC_ERR_UNSUPPORTED) return st;
+    // this kernel reads its LLRs: generate them into the context's buffer, then decode
+    ldpc_graph* g = c->g;
+    const int64_t n = c->B_max * (int64_t)g->N * g->z;
+    if (c->llr_scratch_n < n) {
+        DeviceGuard dg(g->device);
+        if (c->llr_scratch) (void)hipFree(c->llr_scratch);
+        c->llr_scratch = nullptr;
+        c->llr_scratch_n = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&c->llr_scratch), (size_t)n * sizeof(float)) != hipSuccess) {
+            (void)hipGetLastError();
+            return LDPC_ERR_OOM;
+        }
+        c->llr_scratch_n = n;
+    }
+    {
+        DeviceGuard dg(g->device);
+        st = ldpc_channel_awgn(c->llr_scratch, B, g->N * g->z, ch->sigma, ch->seed, ch->offset,
+                               p->decoding_type, p->q_bit, ch->punct_start, ch->punct_end,
+                               ch->short_start, ch->short_end, p->clip_llr, stream);
+    }
+    if (st != LDPC_OK) return st;
+    return decode_impl(c, c->llr_scratch, B, p, o, stream, nullptr);
 }
 
 int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* bytes_per_cw,
@@ -392,9 +439,9 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
     return LDPC_OK;
 }
 
-int ldpc_decode(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
-                const ldpc_decode_outputs* o, void* stream) {
-    if (!c || !p || !llr_dev) return LDPC_ERR_ARG;
+static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
+                       const ldpc_decode_outputs* o, void* stream, const AwgnParams* gen) {
+    if (!c || !p || (!llr_dev && !gen)) return LDPC_ERR_ARG;
     ldpc_graph* g = c->g;
     if (B <= 0 || B > c->B_max || p->T <= 0 || p->T > c->T_max) return LDPC_ERR_STATE;
     if (g->T_w < p->T || !g->d_alpha || !g->d_beta) return LDPC_ERR_STATE;
@@ -414,6 +461,7 @@ int ldpc_decode(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_
     if (kern != LDPC_KERNEL_FLOOD && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_ARG;
     if (kern == LDPC_KERNEL_FUSED && !fused_supported(g->dev, mode, p->T))
         return LDPC_ERR_UNSUPPORTED;
+    if (gen && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_UNSUPPORTED;   // caller falls back
 
     const int ntiles = (int)((B + TILE - 1) / TILE);
     const bool count = out.counters || out.frame_flags;
@@ -432,6 +480,7 @@ int ldpc_decode(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_
     b.wrong = c->wrong;
     b.anypos = c->anypos;
     b.biterr = c->biterr;
+    b.awgn = gen;
     const bool want_bits = out.hard_bits || out.synd_bits;
 
     if (count && kern == LDPC_KERNEL_FLOOD) {

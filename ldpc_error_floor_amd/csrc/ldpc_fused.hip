@@ -461,6 +461,7 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
     if (fused_version() >= 5 && fused5_supported(g, b.T))
         return fused5_decode(g, b, ws, llr, mode_qmax(mode), step, (int)cu, per_edge_w != 0, hd_out,
                              counters, flags, s);
+    if (b.awgn) return LDPC_ERR_UNSUPPORTED;          // in-kernel channel: v5 only
     if (fused_version() == 4 && fused4_supported(g, b.T, mode_qmax(mode), per_edge_w != 0))
         return fused4_decode(g, b, llr, mode_qmax(mode), step, (int)cu, hd_out, counters, flags, s);
     if (fused_version() >= 3 && fused3_supported(g, b.T)) {

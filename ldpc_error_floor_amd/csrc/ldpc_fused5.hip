@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "ldpc_awgn.h"
 #include "ldpc_fused.h"
 
 namespace ldpc {
@@ -64,6 +65,8 @@ struct F5Args {
     int Mp;            // proto rows
     const float* betas;        // [T][N] beta / step (setup kernel)
     const uint16_t* qtab;      // [T][Mp][qmax+2] weight table (setup kernel), LUT builds only
+    int gen;                   // 1: LLRs from the in-kernel AWGN channel (awgn), llr unused
+    AwgnParams awgn;
     uint32_t zmagic;
     int ablate;        // diagnostic only (LDPC_DIAG_ABLATE): 1 skip CN pass 1, 2 skip pass 2, 4 skip VN
 };
@@ -148,6 +151,17 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     {
         float* scr = reinterpret_cast<float*>(W);            // [CW][nv+1]
         const int rl = nv + 1;
+        if (a.gen) {
+            // in-kernel channel: the same generator as ldpc_channel_awgn (ldpc_awgn.h)
+            const int npairs = (nv + 1) >> 1;
+            for (int i = tid; i < CW * npairs; i += NT) {
+                const int r = i / npairs, pr = i - r * npairs;
+                float l[2] = {0.f, 0.f};
+                if (r < nvalid) awgn_pair(a.awgn, b0 + r, pr, l);
+                scr[r * rl + 2 * pr] = l[0];
+                if (2 * pr + 1 < nv) scr[r * rl + 2 * pr + 1] = l[1];
+            }
+        } else
         for (int v0 = 0; v0 < nv; v0 += NT) {
             const int v = v0 + tid;
             float x[CW];
@@ -723,6 +737,10 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     a.nfull = g.n_vars * sh.cw / 64;
     a.cpw = (a.nfull + p.nw - 1) / p.nw;
     a.Mp = g.M;
+    if (b.awgn) {
+        a.gen = 1;
+        a.awgn = *reinterpret_cast<const AwgnParams*>(b.awgn);
+    }
     a.zmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.z - 1) / (uint64_t)g.z);
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // timing only
     // shared tables: one small launch per decode instead of per-workgroup dependent loads

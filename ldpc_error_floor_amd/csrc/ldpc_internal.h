@@ -59,6 +59,8 @@ struct Bufs {
     int hd_all;                // 1: hd kept for every iteration (slots T+1), 0: ring of 2
     int store_hd, count;
     float clip;
+    const void* awgn;          // AwgnParams* (ldpc_awgn.h): generate the LLRs in the fused
+                               // prologue instead of reading them (fused v5 only), or null
 };
 
 // hard decisions of iteration s (s = -1: prologue's lw_0) live in slot s+1 (or ring (s+1)&1)

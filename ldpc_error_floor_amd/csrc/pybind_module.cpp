@@ -117,6 +117,36 @@ PYBIND11_MODULE(_ldpc_nms, m) {
         py::arg("app") = 0, py::arg("hard") = 0, py::arg("synd") = 0, py::arg("counters") = 0,
         py::arg("flags") = 0, py::arg("stream") = 0);
     m.def(
+        "decode_awgn",
+        [](Ctx& c, int64_t B, int T, int decoding_type, int q_bit, int target_bits, float clip,
+           int kernel, double sigma, uint64_t seed, int64_t offset, int ps, int pe, int ss, int se,
+           uintptr_t app, uintptr_t counters, uintptr_t flags, uintptr_t stream) {
+            ldpc_decode_params p = make_params(T, decoding_type, q_bit, target_bits, clip, kernel);
+            ldpc_channel_params ch{};
+            ch.sigma = sigma;
+            ch.seed = seed;
+            ch.offset = offset;
+            ch.punct_start = ps;
+            ch.punct_end = pe;
+            ch.short_start = ss;
+            ch.short_end = se;
+            ldpc_decode_outputs o{};
+            o.app_all = reinterpret_cast<float*>(app);
+            o.counters = reinterpret_cast<int64_t*>(counters);
+            o.frame_flags = reinterpret_cast<uint8_t*>(flags);
+            int st;
+            {
+                py::gil_scoped_release nogil;
+                st = ldpc_decode_awgn(c.h, B, &p, &ch, &o, reinterpret_cast<void*>(stream));
+            }
+            check(st, "ldpc_decode_awgn");
+        },
+        py::arg("ctx"), py::arg("B"), py::arg("T"), py::arg("decoding_type"), py::arg("q_bit"),
+        py::arg("target_bits"), py::arg("clip"), py::arg("kernel"), py::arg("sigma"),
+        py::arg("seed"), py::arg("offset"), py::arg("punct_start"), py::arg("punct_end"),
+        py::arg("short_start"), py::arg("short_end"), py::arg("app") = 0, py::arg("counters") = 0,
+        py::arg("flags") = 0, py::arg("stream") = 0);
+    m.def(
         "channel_awgn",
         [](uintptr_t llr, int64_t B, int n_vars, double sigma, uint64_t seed, int64_t offset,
            int decoding_type, int q_bit, int ps, int pe, int ss, int se, float clip,

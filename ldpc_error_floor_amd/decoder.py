@@ -170,6 +170,43 @@ class NMSDecoder:
                          ptr(res.flags), stream.cuda_stream)
         return res
 
+    def decode_awgn(self, B: int, sigma: float, seed: int, offset: int = 0, punct=None, short=None,
+                    T: Optional[int] = None, app: bool = False, counters=None, flags=None,
+                    kernel: Optional[str] = None, stream=None) -> DecodeResult:
+        """Decode B codewords whose LLRs come from the on-GPU AWGN channel, generated inside
+        the decoder (``ldpc_decode_awgn``): identical to ``decode(awgn(...))`` without the
+        LLRs ever being written to HBM.  ``counters`` / ``flags`` as in ``decode``."""
+        torch = self._torch
+        T = self.T if T is None else int(T)
+        punct = getattr(self, "punct", (0, 0)) if punct is None else punct
+        short = getattr(self, "short", (0, 0)) if short is None else short
+        ctx = self._ensure_ctx(int(B), T)
+        dev = self.device
+        res = DecodeResult()
+        if app:
+            res.app = torch.empty((T, B, self.target_bits), dtype=torch.float32, device=dev)
+        if counters is True:
+            counters = torch.zeros(4, dtype=torch.int64, device=dev)
+        if counters is not None:
+            if counters.dtype != torch.int64 or counters.numel() < 4 or counters.device != dev:
+                raise ValueError("counters must be an int64[4] tensor on the decoder's device")
+            res.counters = counters
+        if isinstance(flags, torch.Tensor):
+            if flags.dtype != torch.uint8 or flags.device != dev or flags.numel() < B:
+                raise ValueError("flags tensor must be uint8 on the decoder's device, >= B long")
+            res.flags = flags
+        elif flags:
+            res.flags = torch.empty(B, dtype=torch.uint8, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        ptr = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
+        self._ext.decode_awgn(ctx, int(B), T, self.decoding_type, self.q_bit, self.target_bits,
+                              self.clip, KERNELS[kernel or self.kernel], float(sigma), int(seed),
+                              int(offset), int(punct[0]), int(punct[1]), int(short[0]),
+                              int(short[1]), ptr(res.app), ptr(res.counters), ptr(res.flags),
+                              stream.cuda_stream)
+        return res
+
     def collect_uncorrected(self, flags, llr, stream=None):
         """LLR rows (host float32 [n, N*z], batch order) of the frames wrong at every iteration
         (``frame_flags`` bit 0 = the reference's ``uncor_flag``), compacted on the GPU by

@@ -90,21 +90,28 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
     dev = decoder.device
     counters = torch.zeros((sigmas.size, 4), dtype=torch.int64, device=dev)
     begin, end = shard_range(int(n_codewords), rank, world)
-    llr = torch.empty((batch, decoder.n_vars), dtype=torch.float32, device=dev)
+    fused_channel = uncor_path is None and hasattr(decoder, "decode_awgn")
+    llr = None if fused_channel else torch.empty((batch, decoder.n_vars), dtype=torch.float32,
+                                                 device=dev)
     flags = torch.empty(batch, dtype=torch.uint8, device=dev) if uncor_path else None
     upath = uncor_path if (uncor_path is None or world == 1) else f"{uncor_path}.rank{rank}"
     for si, sigma in enumerate(sigmas):
         pos = begin
         while pos < end:
             b = min(batch, end - pos)
-            decoder.awgn(b, float(sigma), seed + 7919 * si, offset=pos, punct=punct, short=short,
-                         out=llr[:b])
-            decoder.decode(llr[:b], T=T, app=False, counters=counters[si], kernel=kernel,
-                           flags=None if flags is None else flags[:b])
-            if flags is not None:
-                rows = decoder.collect_uncorrected(flags[:b], llr[:b])
-                if rows.shape[0]:
-                    append_uncor_rows(rows, upath)
+            if fused_channel:
+                # LLRs generated inside the decoder (ldpc_decode_awgn): no HBM round trip
+                decoder.decode_awgn(b, float(sigma), seed + 7919 * si, offset=pos, punct=punct,
+                                    short=short, T=T, counters=counters[si], kernel=kernel)
+            else:
+                decoder.awgn(b, float(sigma), seed + 7919 * si, offset=pos, punct=punct,
+                             short=short, out=llr[:b])
+                decoder.decode(llr[:b], T=T, app=False, counters=counters[si], kernel=kernel,
+                               flags=None if flags is None else flags[:b])
+                if flags is not None:
+                    rows = decoder.collect_uncorrected(flags[:b], llr[:b])
+                    if rows.shape[0]:
+                        append_uncor_rows(rows, upath)
             pos += b
             if progress:
                 progress(si, pos - begin, end - begin)

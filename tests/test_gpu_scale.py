@@ -165,3 +165,40 @@ def test_collect_uncorrected_on_device(cuda_device, tmp_path):
     lines = np.loadtxt(path, delimiter="\t", ndmin=2)
     assert lines.shape == (res[0].frame_err_all, 3 + dec.n_vars)
     assert np.all(lines[:, :3] == 0)
+
+
+@pytest.mark.parametrize("case", ["wman_fused", "wman_flood", "bg2_fused", "wman_sp"])
+def test_decode_awgn_equals_awgn_then_decode(cuda_device, case):
+    """ldpc_decode_awgn (LLRs generated inside the decoder, or into a context buffer for the
+    flood kernel) == ldpc_channel_awgn + ldpc_decode, bit for bit, on a ragged sharded batch."""
+    import torch
+    from ldpc_error_floor_amd.code import CodeParams, TannerGraph, load_base_graph
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    from ldpc_error_floor_amd.weights import expand_weights, read_weight_file
+    if case.startswith("wman"):
+        dec, cp = _wman(cuda_device, kernel="flood" if case == "wman_flood" else "auto")
+        punct, short, snr = (0, 0), (0, 0), 2.0
+        if case == "wman_sp":
+            dec = NMSDecoder(dec.graph.proto, 24, dec.weights, 0, 5, device=cuda_device)
+    else:
+        name = "5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640"
+        proto = load_base_graph(os.path.join(DATA, "BaseGraph", name + ".txt"))
+        g = TannerGraph(proto, 64)
+        wf = read_weight_file(os.path.join(DATA, "Results", "5G", name + "_Weight_End50.txt"))
+        W = expand_weights((2, 2, 2), wf.blocks, 20, g)
+        dec = NMSDecoder(proto, 64, W, 2, 5, device=cuda_device)
+        punct, short, snr = (1, 128), (513, 640), 2.0
+        cp = CodeParams(proto, 64, 1, 128, 513, 640)
+    B, off, seed = 1500 + 37, 4096 + 5, 99
+    sigma = float(cp.sigma(snr))
+    llr = dec.awgn(B, sigma, seed, offset=off, punct=punct, short=short)
+    ref = dec.decode(llr, app=True, counters=True, flags=True)
+    got = dec.decode_awgn(B, sigma, seed, offset=off, punct=punct, short=short, app=True,
+                          counters=True, flags=True)
+    assert torch.equal(got.app, ref.app)
+    assert torch.equal(got.counters, ref.counters)
+    assert torch.equal(got.flags, ref.flags)
+    cnt = torch.zeros(4, dtype=torch.int64, device=cuda_device)        # counters-only build
+    dec.decode_awgn(B, sigma, seed, offset=off, punct=punct, short=short, counters=cnt)
+    assert torch.equal(cnt, ref.counters)
+    assert 0 < int(ref.counters[1]) < B
