@@ -133,10 +133,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL; LDPC_BENCH_BACKEND=gloo rehearses the multi-rank code path
+    # with several ranks on the same GPU (the driver's runs use the default)
+    backend = os.environ.get("LDPC_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    gpu = local if backend == "nccl" else local % max(ndev, 1)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     from ldpc_error_floor_amd.decoder import NMSDecoder
