@@ -122,6 +122,8 @@ class NMSDecoder:
             llr = torch.from_numpy(np.ascontiguousarray(np.asarray(llr, np.float32)))
         llr = llr.to(device=self.device, dtype=torch.float32)
         B = llr.shape[0]
+        if B == 0:
+            return llr.reshape(0, self.n_vars)
         llr = llr.reshape(B, -1).contiguous()
         if llr.shape[1] != self.n_vars:
             raise ValueError(f"llr has {llr.shape[1]} bits per codeword, graph has {self.n_vars}")
@@ -140,6 +142,8 @@ class NMSDecoder:
             raise ValueError(f"T={T} exceeds the {self.T} iterations the weights cover")
         llr = self._as_llr(llr)
         B = int(llr.shape[0])
+        if B == 0:
+            return self._empty_result(T, nt, hard, synd, counters, flags, app)
         ctx = self._ensure_ctx(B, T)
         res = DecodeResult()
         dev = self.device
@@ -170,6 +174,26 @@ class NMSDecoder:
                          ptr(res.flags), stream.cuda_stream)
         return res
 
+    def _empty_result(self, T, nt, hard, synd, counters, flags, app):
+        """An empty batch decodes to empty outputs; a caller's counters are left unchanged."""
+        torch = self._torch
+        dev = self.device
+        res = DecodeResult()
+        if app:
+            res.app = torch.empty((T, 0, nt), dtype=torch.float32, device=dev)
+        if hard:
+            res.hard = torch.empty((T, 0, (self.n_vars + 31) // 32), dtype=torch.int32, device=dev)
+        if synd:
+            res.synd = torch.empty((T, 0, (self.n_checks + 31) // 32), dtype=torch.int32, device=dev)
+        if counters is True:
+            counters = torch.zeros(4, dtype=torch.int64, device=dev)
+        res.counters = counters if counters is not None else None
+        if isinstance(flags, torch.Tensor):
+            res.flags = flags[:0]
+        elif flags:
+            res.flags = torch.empty(0, dtype=torch.uint8, device=dev)
+        return res
+
     def decode_awgn(self, B: int, sigma: float, seed: int, offset: int = 0, punct=None, short=None,
                     T: Optional[int] = None, app: bool = False, counters=None, flags=None,
                     kernel: Optional[str] = None, stream=None) -> DecodeResult:
@@ -180,6 +204,8 @@ class NMSDecoder:
         T = self.T if T is None else int(T)
         punct = getattr(self, "punct", (0, 0)) if punct is None else punct
         short = getattr(self, "short", (0, 0)) if short is None else short
+        if int(B) == 0:
+            return self._empty_result(T, self.target_bits, False, False, counters, flags, app)
         ctx = self._ensure_ctx(int(B), T)
         dev = self.device
         res = DecodeResult()

@@ -202,3 +202,16 @@ def test_decode_awgn_equals_awgn_then_decode(cuda_device, case):
     dec.decode_awgn(B, sigma, seed, offset=off, punct=punct, short=short, counters=cnt)
     assert torch.equal(cnt, ref.counters)
     assert 0 < int(ref.counters[1]) < B
+
+
+def test_empty_batch(cuda_device):
+    """B = 0: empty outputs, caller's counters untouched (decode and decode_awgn)."""
+    import torch
+    dec, cp = _wman(cuda_device)
+    cnt = torch.tensor([1, 2, 3, 4], dtype=torch.int64, device=cuda_device)
+    r = dec.decode(torch.empty((0, dec.n_vars), device=cuda_device), app=True, hard=True,
+                   counters=cnt, flags=True)
+    assert r.app.shape == (dec.T, 0, dec.target_bits) and r.flags.numel() == 0
+    assert cnt.tolist() == [1, 2, 3, 4]
+    r = dec.decode_awgn(0, float(cp.sigma(2.0)), 1, counters=cnt, flags=True)
+    assert cnt.tolist() == [1, 2, 3, 4] and r.flags.numel() == 0
