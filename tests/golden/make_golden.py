@@ -315,7 +315,7 @@ def main():
         weight_loader_cases(MF)
     g_wman = None
     if want("wman_303_q5"):
-        for snr in (2.0, 3.5):
+        for snr in (2.0, 2.5, 3.5):
             g_wman = decoder_case(MF, PF, f"wman_303_q5_snr{snr}", "wman_N0576_R34_z24", 24,
                                   [3, 0, 3], 2, 5, 20, 24, snr,
                                   blocks={0: wman_blocks[0], 2: wman_blocks[2]}, g=g_wman)

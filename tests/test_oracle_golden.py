@@ -25,7 +25,9 @@ def test_oracle_matches_reference(name):
 
 def test_fixture_inventory():
     # the SURVEY §8 c list: wman base, post cascade, MS, all q_bits, 802.11n, 5G BG2, z=1
-    need = {"wman_303_q5_snr2.0", "wman_303_q5_snr3.5", "wman_333_post_snr2.0",
+    need = {"wman_303_q5_snr2.0", "wman_303_q5_snr2.5", "wman_303_q5_snr3.5",
+            "wman_333_post_snr2.0", "wman_303_sp_snr2.5", "wman_333_sp_snr2.0",
+            "g5bg2_222_sp_snr2.0",
             "wman_303_ms_snr2.5", "wman_222_q6", "wman_222_qm5", "wman_222_q4", "wman_222_q3",
             "wifi_333_q5_snr3.0", "g5bg2_222_q5_snr2.0", "mackay_333_q5_snr2.5",
             "polar_222_q5_snr3.0"}
