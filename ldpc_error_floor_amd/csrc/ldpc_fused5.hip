@@ -595,13 +595,16 @@ __global__ void k_f5_tables(const float* __restrict__ alpha, const float* __rest
 // ---- shapes ------------------------------------------------------------------------------
 struct Shape5 {
     int cw, maxg, maxdeg;
+    bool autosel;  // considered by plan5 (else only via LDPC_F5_SHAPE=<index>)
 };
 constexpr Shape5 kShapes5[] = {
-    {16, 3, 16},   // wman-like (z=24, deg 14-15)
-    {16, 3, 24},   // 802.11n-like (deg 22)
-    {8, 5, 16},    // 5G BG2-like (z=64, deg <= 10)
-    {64, 3, 8},    // z=1 sparse (MacKay)
-    {64, 2, 32},   // z=1 dense rows (BCH)
+    {16, 3, 16, true},    // wman-like (z=24, deg 14-15)
+    {16, 3, 24, true},    // 802.11n-like (deg 22)
+    {8, 5, 16, true},     // 5G BG2-like (z=64, deg <= 10)
+    {64, 3, 8, true},     // z=1 sparse (MacKay)
+    {64, 2, 32, true},    // z=1 dense rows (BCH)
+    // measured and dropped: {8, 2, 16} at 8 waves/SIMD (64 VGPRs) ran 28.3 ms vs 21.3 ms for
+    // {16, 3, 16} on wman -- twice the per-workgroup fixed cost per codeword
 };
 
 size_t f5_lds(int nv, int cw, int T, int N) {
@@ -616,8 +619,11 @@ struct Plan5 {
 Plan5 plan5(const DevGraph& g, int T) {
     Plan5 best;
     double best_score = 0;
+    const char* force = getenv("LDPC_F5_SHAPE");
+    const int forced = force ? atoi(force) : -1;
     for (int si = 0; si < (int)(sizeof(kShapes5) / sizeof(kShapes5[0])); ++si) {
         const Shape5& sh = kShapes5[si];
+        if (forced >= 0 ? si != forced : !sh.autosel) continue;
         if ((g.z == 1) != (sh.cw == 64)) continue;
         if (g.max_cdeg > sh.maxdeg) continue;
         const int slots = 64 / sh.cw;
