@@ -24,8 +24,10 @@
 //
 // Per-edge weights (sharing types with one weight per edge) keep raw minima in P (16 bit
 // each) and quantize per edge at decode; this path is correct but not tuned.
+#include <algorithm>
 #include <climits>
 #include <type_traits>
+#include <vector>
 #include <cstdio>
 #include <cstdlib>
 
@@ -39,7 +41,9 @@ namespace {
 constexpr int F5_BIG_U = 1023;               // "no other edge": value 10000 (Main_Functions.py:248)
 constexpr size_t F5_LDS_MAX = 160 * 1024;
 constexpr uint32_t F5_SBIAS = 16384;         // S field bias (bits 14..0)
-constexpr uint32_t F5_DUMMY_W = (16383u << 16) | F5_SBIAS;
+// padding edges read this word: Tv = 96 gives a V->C value in [65, 127] for any message
+// (|m| <= 31), positive, never below qmax and inside the 8-bit range pass 1 works in
+constexpr uint32_t F5_DUMMY_W = (96u << 16) | F5_SBIAS;
 constexpr float F5_MAGIC = 12582912.0f;                 // 1.5 * 2^23
 constexpr int F5_MAGIC_BITS = 0x4B400000;              // bit pattern of F5_MAGIC
 constexpr int F5_APP0 = F5_MAGIC_BITS + (int)F5_SBIAS;  // APP == 0 in the VN's biased domain
@@ -65,6 +69,9 @@ struct F5Args {
     int Mp;            // proto rows
     const float* betas;        // [T][N] beta / step (setup kernel)
     const uint16_t* qtab;      // [T][Mp][qmax+2] weight table (setup kernel), LUT builds only
+    const uint32_t* gad;       // [ngroups][NPK][64] packed edge byte addresses (k_f5_gad)
+    const uint4* grow;         // [ngroups] {r0 | deg << 16 | row << 24, lane-valid mask lo, hi, 0}
+    unsigned long long* stamps;   // diagnostic (LDPC_DIAG_STAMPS): [block][8] s_memtime marks
     int gen;                   // 1: LLRs from the in-kernel AWGN channel (awgn), llr unused
     AwgnParams awgn;
     uint32_t zmagic;
@@ -84,6 +91,50 @@ __device__ __forceinline__ int q_mag5(int m, float w, float step, float inv, int
     float x = mv * w;                          // fl32(|o| * w)
     x = (x > 0.f) ? x : 0.f;                   // x * [x > 0]
     return q_units5(x, inv, qmax);
+}
+
+// 16-bit VOP2 forms: full issue rate on gfx950 where the 32-bit min / max / shift-left and
+// every SDWA / VOP3 form take twice the cycles (tools/valu_table.hip); the high half of the
+// result is zeroed.
+__device__ __forceinline__ uint32_t max_i16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_max_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t min_u16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// the low / high 16-bit byte address of a packed pair (LDS base 0)
+__device__ __forceinline__ uint32_t lo16(uint32_t x) {
+    uint32_t r;
+    asm("v_and_b32 %0, 0xffff, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ uint32_t hi16(uint32_t x) {
+    uint32_t r;
+    asm("v_lshrrev_b32 %0, 16, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+// (Tv - m) * 256 sign-extended: Tv = signed high half of the W word, m = signed byte POS of r.
+// Exact while |Tv - m| <= 127 (Tv is kept within +-2 qmax, |m| <= qmax <= 31).
+template <int POS>
+__device__ __forceinline__ uint32_t sub_d256(uint32_t w, uint32_t r) {
+    uint32_t d;
+    if constexpr (POS == 0)
+        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_0"
+            : "=v"(d) : "v"(w), "v"(r));
+    else if constexpr (POS == 1)
+        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_1"
+            : "=v"(d) : "v"(w), "v"(r));
+    else if constexpr (POS == 2)
+        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_2"
+            : "=v"(d) : "v"(w), "v"(r));
+    else
+        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_3"
+            : "=v"(d) : "v"(w), "v"(r));
+    return d;
 }
 
 __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
@@ -113,6 +164,12 @@ struct Sel {
         return n;
     }
 };
+
+// diagnostic phase marks: wave 0 lane 0 of each workgroup records s_memrealtime (100 MHz)
+#define F5_STAMP(i)                                                                         \
+    do {                                                                                    \
+        if (a.stamps && tid == 0) a.stamps[(size_t)blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 
 template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW, bool OUT, bool LUT>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(CW == 16 && MAXDEG == 16 ? 6 : 1)))
@@ -147,6 +204,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     const float inv = a.inv, step = a.step;
     const int z = a.z;
 
+    F5_STAMP(0);
     // ---- prologue: coalesced LLR block -> padded scratch -> CH[v][cw]; beta; W = Tv_0 | hd ----
     {
         float* scr = reinterpret_cast<float*>(W);            // [CW][nv+1]
@@ -190,11 +248,12 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         if (tid < CW) W[total + tid] = F5_DUMMY_W;
     }
 
+    F5_STAMP(1);
     // ---- per-group edge addresses (bytes, 16-bit packed), row info, lane validity ----------
+    // (built once per decode by k_f5_gad; one coalesced load per packed word)
     uint32_t gad[MAXG][NPK];
     uint32_t grow[MAXG];
     bool gval[MAXG];
-    const uint32_t dummy_byte = (uint32_t)(total + cw) * 4u;
 #pragma unroll
     for (int gi = 0; gi < MAXG; ++gi) {
         grow[gi] = 0;
@@ -203,28 +262,17 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         for (int p = 0; p < NPK; ++p) gad[gi][p] = 0;
         const int grp = wave + gi * NWV;
         if (grp < a.ngroups) {
-            const int i = grp / a.hstep;
-            const int hg = grp - i * a.hstep;
-            const int r0 = a.row_ptr[i];
-            const int deg = a.row_ptr[i + 1] - r0;
-            const int h = hg * SLOTS + slot;
-            gval[gi] = h < z;
-            const int hl = (h < z) ? h : hg * SLOTS;
-            grow[gi] = (uint32_t)r0 | ((uint32_t)deg << 16) | ((uint32_t)i << 24);
+            const uint32_t* gt = a.gad + (size_t)grp * NPK * 64 + lane;
 #pragma unroll
-            for (int k = 0; k < MAXDEG; ++k) {
-                uint32_t byte = dummy_byte;
-                if (k < deg) {
-                    int hs = hl + a.pe_shift[r0 + k];
-                    hs = (hs >= z) ? hs - z : hs;
-                    byte = (uint32_t)(((a.pe_col[r0 + k] * z + hs) << LOGCW) + cw) * 4u;
-                }
-                gad[gi][k >> 1] |= (k & 1) ? (byte << 16) : byte;
-            }
+            for (int p = 0; p < NPK; ++p) gad[gi][p] = gt[p * 64];
+            const uint4 r = a.grow[grp];
+            grow[gi] = r.x;
+            gval[gi] = (((lane < 32) ? r.y : r.z) >> (lane & 31)) & 1u;
         }
     }
     __syncthreads();
 
+    F5_STAMP(2);
     // check state: P (messages / raw minima), SEL (per-edge fields), ucn (syndrome, PEW only)
     uint32_t P[MAXG], SEL[MAXG][NSEL];
     int UC[MAXG];
@@ -253,6 +301,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     };
 
     for (int t = 0; t < a.T; ++t) {
+        if (t < 22) F5_STAMP(8 + t);
         if (tid == 0 && t > 0) {        // fold iteration t-1's frame flags (its VN phase is done)
             RED[1] &= RED[0];
             RED[0] = 0;
@@ -285,7 +334,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     const int k = c8 + j;
                     if (k < MAXDEG && (full || k < deg)) {
                         const uint32_t pk = gad[gi][k >> 1];
-                        const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
+                        const uint32_t addr = (k & 1) ? hi16(pk) : lo16(pk);
                         wv[j] = *reinterpret_cast<const uint32_t*>(smem + addr);
                     }
                 }
@@ -295,13 +344,26 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     const int k = c8 + j;
                     if (k < MAXDEG) {
                         if (full || k < deg) {
-                            const int cold = msg(gi, k, j < 4 ? R0 : R1, atp, aup, r0);
-                            const int d = (int)(short)(wv[j] >> 16) - cold;      // V->C before Q
-                            const uint32_t key = ((uint32_t)max(d, -d) << 8) | SL::code(k);
+                            // V->C before Q, times 256: d256 = (Tv - m) << 8, sign-extended
+                            uint32_t d256;
+                            if constexpr (PEW) {
+                                const int cold = msg(gi, k, j < 4 ? R0 : R1, atp, aup, r0);
+                                d256 = sub_d256<0>(wv[j], (uint32_t)cold);
+                            } else {
+                                const uint32_t R = j < 4 ? R0 : R1;
+                                switch (SL::pos(k)) {
+                                    case 0: d256 = sub_d256<0>(wv[j], R); break;
+                                    case 1: d256 = sub_d256<1>(wv[j], R); break;
+                                    case 2: d256 = sub_d256<2>(wv[j], R); break;
+                                    default: d256 = sub_d256<3>(wv[j], R); break;
+                                }
+                            }
+                            // key = |d| << 8 | code, all in the low 16 bits
+                            const uint32_t key = max_i16(d256, 0u - d256) | SL::code(k);
                             // append the byte of sign copies of d to the edge's selector word
-                            NG[k / 4] = __builtin_amdgcn_alignbit(NG[k / 4], (uint32_t)d, 24);
+                            NG[k / 4] = __builtin_amdgcn_alignbit(NG[k / 4], d256, 24);
                             const uint32_t o1 = c1;
-                            c1 = min(o1, key);
+                            c1 = min_u16(o1, key);
                             c2 = med3u(o1, c2, key);
                             if (UCN) syn ^= (wv[j] >> 15) & 1u;
                         } else {
@@ -366,6 +428,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 P[gi] = gval[gi] ? p : 0u;    // duplicate stand-in check: no messages
             }
         }
+        if (t == 0) F5_STAMP(5);
         // ======== check nodes: pass 2 (scatter C->V into S) =================================
 #pragma unroll
         for (int gi = 0; gi < MAXG; ++gi) {
@@ -382,7 +445,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     const int k = c8 + j;
                     if (k < MAXDEG && (full || k < deg)) {
                         const uint32_t pk = gad[gi][k >> 1];
-                        const uint32_t addr = (k & 1) ? (pk >> 16) : (pk & 0xFFFFu);
+                        const uint32_t addr = (k & 1) ? hi16(pk) : lo16(pk);
                         const int c = msg(gi, k, j < 4 ? R0 : R1, at, au, r0);
                         atomicAdd(reinterpret_cast<uint32_t*>(smem + addr), (uint32_t)c);
                     }
@@ -394,6 +457,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             }
         }
         __syncthreads();
+        if (t == 0) F5_STAMP(6);
         // ======== variable nodes ===========================================================
         const bool last = (t == a.T - 1);
         const float* bnext = BETA + (size_t)(last ? t : t + 1) * a.N;
@@ -411,6 +475,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             const bool zuni = (z % SLOTS) == 0;
             const uint32_t cvalid = (cw < nvalid) ? 1u : 0u;
             const int tb = a.target_bits;
+            const int tlo = F5_APP0 - 2 * qmax, thi = F5_APP0 + 2 * qmax;
             // one loop body per (last iteration, whole word is target) pair; 4 chunks per trip
             // with the reads issued first.  Reads past c_end stay inside LDS and are unused.
             auto vn_loop = [&](auto lastc, auto fullc, auto zunic) __attribute__((always_inline)) {
@@ -455,7 +520,9 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                             amax = max(amax, appt);
                             if (!LAST) {
                                 const float yb = __builtin_amdgcn_fmed3f(chv[j] * bv[j], -qmf, qmf);
-                                const int tb2 = __float_as_int(yb + F5_MAGIC) + s;   // Tv + biases
+                                // Tv + biases, Tv kept within +-2 qmax (pass 1's 8-bit range;
+                                // min(|Tv - m|, qmax) and the sign of Tv - m are unchanged)
+                                const int tb2 = min(max(__float_as_int(yb + F5_MAGIC) + s, tlo), thi);
                                 // W = (Tv << 16) | S bias, Tv = tb2 - F5_MAGIC_BITS - S bias
                                 uint32_t wn = (uint32_t)tb2 * 65536u + F5_WBIAS;
                                 if (UCN) wn |= (appb >= F5_APP0) ? 0x8000u : 0u;
@@ -490,7 +557,8 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     const int appt = ((int)v < a.target_bits) ? app : INT_MIN;
                     amax = max(amax, appt == INT_MIN ? INT_MIN : appt + F5_APP0);
                     if (!last) {
-                        const int tn = q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], qmf) + s + sb;
+                        const int tn = min(max(q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], qmf) + s + sb,
+                                               -2 * qmax), 2 * qmax);
                         W[e] = ((uint32_t)tn << 16) | (((uint32_t)~app >> 16) & 0x8000u) | F5_SBIAS;
                     } else {
                         nbits += (uint32_t)(appt >= 0 && appt != INT_MIN) & (uint32_t)cvalid;
@@ -510,7 +578,8 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 int app = q_units5(ch, inv, qmax) + S;                   // Q(xa) + sum C2V
                 app = min(max(app, -a.clip_u), a.clip_u);                // clip +-clip_LLR
                 if (!last) {
-                    const int tn = q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], (float)qmax) + S;
+                    const int tn = min(max(q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], (float)qmax) + S,
+                                           -2 * qmax), 2 * qmax);
                     W[e] = ((uint32_t)tn << 16) | ((uint32_t)(app >= 0) << 15) | F5_SBIAS;
                 }
                 if ((int)v < a.target_bits) {
@@ -546,6 +615,13 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             if (lane == 0 && nb) atomicAdd(&RED[3], (unsigned long long)nb);
         }
         __syncthreads();
+    }
+    F5_STAMP(30);
+    if (a.stamps && tid == 0) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        a.stamps[(size_t)blockIdx.x * 32 + 31] = ((unsigned long long)xcc << 32) | hw;
     }
     if (tid == 0) {
         const unsigned long long wl = RED[0] & valid_cw;
@@ -589,6 +665,44 @@ __global__ void k_f5_tables(const float* __restrict__ alpha, const float* __rest
         const float w = alpha[(size_t)tt * E + row_ptr[row]];
         const int q = q_mag5(m > qmax ? F5_BIG_U : m, w, step, inv, qmax);
         qtab[f] = (uint16_t)(((uint32_t)q & 0xFFu) | (((uint32_t)(-q) & 0xFFu) << 8));
+    }
+}
+
+// Edge addresses per (check group, lane): lane = slot * CW + cw serves circulant row
+// h = hg * SLOTS + slot of proto row i (grp = i * hstep + hg); edge k of that row reads
+// W[(pe_col * z + (h + shift) mod z) * CW + cw], packed as byte offsets two per word.  Lanes
+// with h >= z (last group of a row) mirror slot 0's row and are masked out of the results.
+__global__ void k_f5_gad(const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ pe_col,
+                         const int32_t* __restrict__ pe_shift, int ngroups, int hstep, int z,
+                         int logcw, int maxdeg, int npk, int total, uint32_t* gad, uint4* grow) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= ngroups * 64) return;
+    const int grp = f >> 6, lane = f & 63;
+    const int cwn = 1 << logcw, slots = 64 >> logcw;
+    const int slot = lane >> logcw, cw = lane & (cwn - 1);
+    const int i = grp / hstep, hg = grp - i * hstep;
+    const int r0 = row_ptr[i], deg = row_ptr[i + 1] - r0;
+    const int h = hg * slots + slot;
+    const int hl = (h < z) ? h : hg * slots;
+    for (int p = 0; p < npk; ++p) {
+        uint32_t word = 0;
+        for (int j = 0; j < 2; ++j) {
+            const int k = 2 * p + j;
+            uint32_t byte = (uint32_t)(total + cw) * 4u;              // dummy word of this cw
+            if (k < deg && k < maxdeg) {
+                int hs = hl + pe_shift[r0 + k];
+                hs = (hs >= z) ? hs - z : hs;
+                byte = (uint32_t)(((pe_col[r0 + k] * z + hs) << logcw) + cw) * 4u;
+            }
+            word |= byte << (16 * j);
+        }
+        gad[((size_t)grp * npk + p) * 64 + lane] = word;
+    }
+    if (lane == 0) {
+        uint32_t lo = 0, hi = 0;
+        for (int l = 0; l < 64; ++l)
+            if (hg * slots + (l >> logcw) < z) (l < 32 ? lo : hi) |= 1u << (l & 31);
+        grow[grp] = make_uint4((uint32_t)r0 | ((uint32_t)deg << 16) | ((uint32_t)i << 24), lo, hi, 0u);
     }
 }
 
@@ -688,6 +802,21 @@ int launch5s(const F5Args& a, int nblocks, int nw, size_t lds, bool lut, const f
                : launch5k<CW, MAXG, MAXDEG, false, false>(a, nblocks, nw, lds, lut, alpha, nullptr, s);
 }
 
+// LDPC_DIAG_STAMPS=<file>: raw per-workgroup marks of one launch, [nblocks][32] u64 (100 MHz
+// s_memrealtime: 0 start, 1 after the LLR/CH prologue, 2 after the edge-address setup, 5 after
+// iteration 0's pass 1, 6 after its pass-2 barrier, 8 + t start of iteration t, 30 end; slot 31
+// = XCC_ID << 32 | HW_ID), appended to <file>.  Analysis: tools/stamps.py.
+void report_stamps(const unsigned long long* d, int nblocks, hipStream_t s, const char* path) {
+    std::vector<unsigned long long> h((size_t)nblocks * 32);
+    if (hipStreamSynchronize(s) != hipSuccess ||
+        hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    if (FILE* f = fopen(path, "ab")) {
+        fwrite(h.data(), 8, h.size(), f);
+        fclose(f);
+    }
+}
+
 }  // namespace
 
 bool fused5_supported(const DevGraph& g, int T) { return plan5(g, T).shape >= 0; }
@@ -705,7 +834,7 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
                   int qmax, float step, int clip_u, bool per_edge_w, uint64_t* hd_out,
                   int64_t* counters, uint8_t* flags, hipStream_t s) {
     Plan5 p = plan5(g, b.T);
-    if (p.shape < 0) return LDPC_ERR_UNSUPPORTED;
+    if (p.shape < 0 || qmax > 31) return LDPC_ERR_UNSUPPORTED;   // pass 1's 8-bit V->C range
     const Shape5& sh = kShapes5[p.shape];
     // weight table (uniform row weights, no UCN set): only if it costs no workgroup slot per CU
     bool lut = !per_edge_w && b.alpha_ucn == nullptr && g.M < 256 &&
@@ -751,7 +880,11 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // timing only
     // shared tables: one small launch per decode instead of per-workgroup dependent loads
     const size_t nbeta = (size_t)b.T * g.N, nqt = (size_t)b.T * g.M * (qmax + 2);
-    const size_t tbytes = ((nbeta * 4 + 255) & ~(size_t)255) + nqt * 2;
+    const int npk = (sh.maxdeg + 1) / 2;
+    const size_t off_qt = (nbeta * 4 + 255) & ~(size_t)255;
+    const size_t off_gad = (off_qt + nqt * 2 + 255) & ~(size_t)255;
+    const size_t off_grow = off_gad + (size_t)p.ngroups * npk * 64 * 4;
+    const size_t tbytes = off_grow + (size_t)p.ngroups * 16;
     if (tbytes > ws.tables_bytes) {
         if (ws.tables) (void)hipFree(ws.tables);
         ws.tables = nullptr;
@@ -763,27 +896,44 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
         ws.tables_bytes = tbytes;
     }
     float* betas = reinterpret_cast<float*>(ws.tables);
-    uint16_t* qtab = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(ws.tables) +
-                                                 ((nbeta * 4 + 255) & ~(size_t)255));
+    uint16_t* qtab = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(ws.tables) + off_qt);
+    uint32_t* gad = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws.tables) + off_gad);
+    uint4* grow = reinterpret_cast<uint4*>(reinterpret_cast<char*>(ws.tables) + off_grow);
     {
         const size_t nthr = std::max(nbeta, lut ? nqt : (size_t)0);
         hipLaunchKernelGGL(k_f5_tables, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s,
                            b.alpha, b.beta, g.row_ptr, b.T, g.M, g.E, g.N, qmax, step, 1.0f / step,
                            betas, lut ? qtab : nullptr);
+        const int lcw = sh.cw == 64 ? 6 : sh.cw == 32 ? 5 : sh.cw == 16 ? 4 : 3;
+        hipLaunchKernelGGL(k_f5_gad, dim3((unsigned)((p.ngroups * 64 + 255) / 256)), dim3(256), 0, s,
+                           g.row_ptr, g.pe_col, g.pe_shift, p.ngroups, p.hstep, g.z, lcw, sh.maxdeg,
+                           npk, g.n_vars * sh.cw, gad, grow);
         if (hipGetLastError() != hipSuccess) return LDPC_ERR_HIP;
     }
     a.betas = betas;
     a.qtab = qtab;
+    a.gad = gad;
+    a.grow = grow;
     const int nblocks = (int)((b.B + sh.cw - 1) / sh.cw);
     const float* au = b.alpha_ucn;
+    const char* diag = getenv("LDPC_DIAG_STAMPS");   // timing investigation only
+    if (diag && (hipMalloc(&a.stamps, (size_t)nblocks * 32 * sizeof(unsigned long long)) != hipSuccess ||
+                 hipMemsetAsync(a.stamps, 0, (size_t)nblocks * 32 * 8, s) != hipSuccess))
+        return LDPC_ERR_OOM;
+    int rc;
     switch (p.shape) {
-        case 0: return launch5s<16, 3, 16>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s);
-        case 1: return launch5s<16, 3, 24>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s);
-        case 2: return launch5s<8, 5, 16>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s);
-        case 3: return launch5s<64, 3, 8>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s);
-        case 4: return launch5s<64, 2, 32>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s);
-        default: return LDPC_ERR_UNSUPPORTED;
+        case 0: rc = launch5s<16, 3, 16>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 1: rc = launch5s<16, 3, 24>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 2: rc = launch5s<8, 5, 16>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 3: rc = launch5s<64, 3, 8>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 4: rc = launch5s<64, 2, 32>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        default: rc = LDPC_ERR_UNSUPPORTED;
     }
+    if (diag) {
+        if (rc == LDPC_OK) report_stamps(a.stamps, nblocks, s, diag);
+        (void)hipFree(a.stamps);
+    }
+    return rc;
 }
 
 }  // namespace ldpc

@@ -44,6 +44,28 @@ __global__ void __launch_bounds__(256) k_mix(uint32_t* out, uint32_t seed, unsig
                 asm volatile("v_med3_u32 %0, %1, %0, %2" : "+v"(a[j]) : "v"(b[j]), "v"(k));
             } else if (MIX == 6) {     // dependent chain of v_add (one chain per lane)
                 asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[0]) : "v"(b[j]));
+            } else if (MIX == 7) {     // VOP3 encoding of the same add
+                asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 8) {     // VOP2 with a 32-bit literal (8-byte instruction)
+                asm volatile("v_add_u32 %0, 0x12345, %0" : "+v"(a[j]));
+            } else if (MIX == 9) {     // packed 16-bit (VOP3P)
+                asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 10) {    // VOP2 with an SGPR operand
+                asm volatile("v_and_b32 %0, %1, %0" : "+v"(a[j]) : "s"(seed));
+            } else if (MIX == 11) {    // v_lshrrev (VOP2) + v_and (VOP2, SGPR): the unpack pair
+                asm volatile("v_lshrrev_b32 %0, 16, %0" : "+v"(a[j]));
+            } else if (MIX == 12) {    // VOP1 move
+                asm volatile("v_not_b32 %0, %0" : "+v"(a[j]));
+            } else if (MIX == 13) {    // v_min_u32 VOP2 / v_max_i32 mix
+                asm volatile("v_min_u32 %0, %0, %1" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 14) {    // v_pk_min_u16 (VOP3P)
+                asm volatile("v_pk_min_u16 %0, %0, %1" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 15) {    // v_cndmask (VOP2, vcc)
+                asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 16) {    // v_add3 (VOP3, 3 operands)
+                asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+            } else if (MIX == 17) {    // DPP row_shr (VOP2 + DPP word)
+                asm volatile("v_add_u32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(a[j]) : "v"(b[j]));
             }
         }
     }
@@ -87,7 +109,7 @@ int main() {
     printf("%s  CUs %d  clock %.3f GHz (device max; the measured rate uses it)\n", p.name, ncu, clk);
     uint32_t* d;
     hipMalloc(&d, (size_t)ncu * 8 * 256 * 4 * 4);
-    for (int w : {1, 2, 4, 6, 8}) {
+    for (int w : {2, 6}) {
         run<0>("v_add_u32", 1, w, ncu, clk, d);
         run<1>("v_med3_u32", 1, w, ncu, clk, d);
         run<2>("v_sub_u32_sdwa", 1, w, ncu, clk, d);
@@ -95,6 +117,17 @@ int main() {
         run<4>("v_alignbit_b32", 1, w, ncu, clk, d);
         run<5>("pass-1 edge (7 ops)", 7, w, ncu, clk, d);
         run<6>("dependent v_add chain", 1, w, ncu, clk, d);
+        run<7>("v_add_u32_e64 (VOP3)", 1, w, ncu, clk, d);
+        run<8>("v_add_u32 literal", 1, w, ncu, clk, d);
+        run<9>("v_pk_add_u16", 1, w, ncu, clk, d);
+        run<10>("v_and_b32 sgpr", 1, w, ncu, clk, d);
+        run<11>("v_lshrrev_b32 imm", 1, w, ncu, clk, d);
+        run<12>("v_not_b32 (VOP1)", 1, w, ncu, clk, d);
+        run<13>("v_min_u32", 1, w, ncu, clk, d);
+        run<14>("v_pk_min_u16", 1, w, ncu, clk, d);
+        run<15>("v_cndmask_b32 vcc", 1, w, ncu, clk, d);
+        run<16>("v_add3_u32", 1, w, ncu, clk, d);
+        run<17>("v_add_u32_dpp", 1, w, ncu, clk, d);
     }
     hipFree(d);
     return 0;
