@@ -106,7 +106,9 @@ __device__ __forceinline__ uint32_t min_u16(uint32_t a, uint32_t b) {
     asm("v_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
-// the low / high 16-bit byte address of a packed pair (LDS base 0)
+// LDS word at a byte address (the decoder's dynamic LDS starts at 0: k_fused5 checks)
+typedef __attribute__((address_space(3))) uint32_t LdsU32;
+// the low / high 16-bit byte address of a packed pair
 __device__ __forceinline__ uint32_t lo16(uint32_t x) {
     uint32_t r;
     asm("v_and_b32 %0, 0xffff, %1" : "=v"(r) : "v"(x));
@@ -189,6 +191,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         smem + ((((size_t)total + CW) * 4 + (size_t)total * 4 + (size_t)a.T * a.N * 4 + 15) & ~(size_t)15));
     uint16_t* QT = reinterpret_cast<uint16_t*>(RED + 8);                          // [T][Mp][qmax+2]
 
+    if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();   // edge addresses are LDS-absolute
     const int tid = threadIdx.x;
     const int NT = blockDim.x;
     const int NWV = NT >> 6;
@@ -335,29 +338,39 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     if (k < MAXDEG && (full || k < deg)) {
                         const uint32_t pk = gad[gi][k >> 1];
                         const uint32_t addr = (k & 1) ? hi16(pk) : lo16(pk);
-                        wv[j] = *reinterpret_cast<const uint32_t*>(smem + addr);
+                        wv[j] = *reinterpret_cast<const LdsU32*>(addr);
                     }
                 }
                 const uint32_t R0 = perm_word(gi, c8 / 4), R1 = perm_word(gi, c8 / 4 + 1);
+                // V->C before Q, times 256: d256 = (Tv - m) << 8, sign-extended.  All eight
+                // first: an SDWA result with a sub-dword dst_sel read by the very next
+                // instruction costs a wait state.
+                uint32_t dd[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int k = c8 + j;
+                    if (k < MAXDEG && (full || k < deg)) {
+                        if constexpr (PEW) {
+                            const int cold = msg(gi, k, j < 4 ? R0 : R1, atp, aup, r0);
+                            dd[j] = sub_d256<0>(wv[j], (uint32_t)cold);
+                        } else {
+                            const uint32_t R = j < 4 ? R0 : R1;
+                            switch (SL::pos(k)) {
+                                case 0: dd[j] = sub_d256<0>(wv[j], R); break;
+                                case 1: dd[j] = sub_d256<1>(wv[j], R); break;
+                                case 2: dd[j] = sub_d256<2>(wv[j], R); break;
+                                default: dd[j] = sub_d256<3>(wv[j], R); break;
+                            }
+                        }
+                        if (UCN) syn ^= (wv[j] >> 15) & 1u;
+                    }
+                }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int k = c8 + j;
                     if (k < MAXDEG) {
                         if (full || k < deg) {
-                            // V->C before Q, times 256: d256 = (Tv - m) << 8, sign-extended
-                            uint32_t d256;
-                            if constexpr (PEW) {
-                                const int cold = msg(gi, k, j < 4 ? R0 : R1, atp, aup, r0);
-                                d256 = sub_d256<0>(wv[j], (uint32_t)cold);
-                            } else {
-                                const uint32_t R = j < 4 ? R0 : R1;
-                                switch (SL::pos(k)) {
-                                    case 0: d256 = sub_d256<0>(wv[j], R); break;
-                                    case 1: d256 = sub_d256<1>(wv[j], R); break;
-                                    case 2: d256 = sub_d256<2>(wv[j], R); break;
-                                    default: d256 = sub_d256<3>(wv[j], R); break;
-                                }
-                            }
+                            const uint32_t d256 = dd[j];
                             // key = |d| << 8 | code, all in the low 16 bits
                             const uint32_t key = max_i16(d256, 0u - d256) | SL::code(k);
                             // append the byte of sign copies of d to the edge's selector word
@@ -365,7 +378,6 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                             const uint32_t o1 = c1;
                             c1 = min_u16(o1, key);
                             c2 = med3u(o1, c2, key);
-                            if (UCN) syn ^= (wv[j] >> 15) & 1u;
                         } else {
                             NG[k / 4] <<= 8;                                     // positive
                         }
@@ -447,7 +459,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                         const uint32_t pk = gad[gi][k >> 1];
                         const uint32_t addr = (k & 1) ? hi16(pk) : lo16(pk);
                         const int c = msg(gi, k, j < 4 ? R0 : R1, at, au, r0);
-                        atomicAdd(reinterpret_cast<uint32_t*>(smem + addr), (uint32_t)c);
+                        __atomic_fetch_add(reinterpret_cast<LdsU32*>(addr), (uint32_t)c, __ATOMIC_RELAXED);
                     }
                 }
             };
