@@ -49,6 +49,12 @@ constexpr int F5_MAGIC_BITS = 0x4B400000;              // bit pattern of F5_MAGI
 constexpr int F5_APP0 = F5_MAGIC_BITS + (int)F5_SBIAS;  // APP == 0 in the VN's biased domain
 // (Tv + F5_APP0) * 2^16 + F5_WBIAS == (Tv << 16) | F5_SBIAS  (mod 2^32)
 constexpr uint32_t F5_WBIAS = F5_SBIAS - (uint32_t)F5_APP0 * 65536u;
+// APP path magic: 1.5 * 2^23 + 2^22 - S bias, same binade, so Q(y) + APP bits land at
+// F5_APPH + APP with F5_APPH = 0x4B800000: APP >= 0 exactly when bit 23 is set (an OR over
+// entries then answers "any hard decision 1")
+constexpr float F5_MAGIC_A = 16760832.0f;
+constexpr int F5_APPH = 0x4B800000;
+static_assert(12582912 + 4194304 - (int)F5_SBIAS == 16760832, "APP magic");
 
 struct F5Args {
     const float* llr;
@@ -139,6 +145,13 @@ __device__ __forceinline__ uint32_t sub_d256(uint32_t w, uint32_t r) {
     return d;
 }
 
+// min(max(a, lo), hi) on the low 16 bits, bounds uniform (SGPR)
+__device__ __forceinline__ uint32_t clamp_i16(uint32_t a, uint32_t lo, uint32_t hi) {
+    uint32_t r;
+    asm("v_max_i16 %0, %1, %2" : "=v"(r) : "s"(lo), "v"(a));
+    asm("v_min_i16 %0, %1, %2" : "=v"(r) : "s"(hi), "v"(r));
+    return r;
+}
 __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t r;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -481,13 +494,16 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             // counters only.  A wave owns the contiguous 64-entry chunks [c_beg, c_end); with
             // SLOTS | z a chunk lies in one proto column, so beta is wave-uniform.  Only the
             // hard-decision sign matters here, and clipping never changes a sign.
-            int amax = INT_MIN;                       // max APP over the target entries
+            int amax = INT_MIN;                       // max APP over the target entries (last)
+            uint32_t aor = 0;                         // OR of F5_APPH-biased APPs (bit 23)
             const int c_beg = wave * a.cpw;
             const int c_end = min(c_beg + a.cpw, a.nfull);
             const bool zuni = (z % SLOTS) == 0;
             const uint32_t cvalid = (cw < nvalid) ? 1u : 0u;
             const int tb = a.target_bits;
-            const int tlo = F5_APP0 - 2 * qmax, thi = F5_APP0 + 2 * qmax;
+            // Tv clamp bounds as the low 16 bits of Tv + F5_APP0 (= 16384 + Tv)
+            const uint32_t tlo = (uint32_t)(F5_APP0 - 2 * qmax) & 0xFFFFu;
+            const uint32_t thi = (uint32_t)(F5_APP0 + 2 * qmax) & 0xFFFFu;
             // one loop body per (last iteration, whole word is target) pair; 4 chunks per trip
             // with the reads issued first.  Reads past c_end stay inside LDS and are unused.
             auto vn_loop = [&](auto lastc, auto fullc, auto zunic) __attribute__((always_inline)) {
@@ -521,26 +537,34 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                             // the integer sits in the low mantissa bits: bits - F5_MAGIC_BITS
                             const int s = (int)(wv[j] & 0x7FFFu);                     // S + bias
                             const float yc = __builtin_amdgcn_fmed3f(chv[j] * inv, -qmf, qmf);
-                            const int qc = __float_as_int(yc + F5_MAGIC);
-                            // APP + F5_MAGIC_BITS + S bias: the sign test is against that offset
+                            const int qc = __float_as_int(yc + F5_MAGIC_A);
+                            // APP + F5_APPH: bit 23 set iff APP >= 0
                             const int appb = qc + s;
-                            int appt = appb;
-                            if (!FULLT) {
-                                const int v = ((c + j) * 64 + lane) >> LOGCW;
-                                appt = (v < tb) ? appb : INT_MIN;
-                            }
-                            amax = max(amax, appt);
-                            if (!LAST) {
+                            if (LAST) {
+                                int appt = appb;
+                                if (!FULLT) {
+                                    const int v = ((c + j) * 64 + lane) >> LOGCW;
+                                    appt = (v < tb) ? appb : INT_MIN;
+                                }
+                                amax = max(amax, appt);
+                                nbits += (uint32_t)(appt >= F5_APPH) & cvalid;
+                            } else {
+                                if (FULLT) {
+                                    aor |= (uint32_t)appb;
+                                } else {
+                                    const int v = ((c + j) * 64 + lane) >> LOGCW;
+                                    aor |= (v < tb) ? (uint32_t)appb : 0u;
+                                }
                                 const float yb = __builtin_amdgcn_fmed3f(chv[j] * bv[j], -qmf, qmf);
                                 // Tv + biases, Tv kept within +-2 qmax (pass 1's 8-bit range;
                                 // min(|Tv - m|, qmax) and the sign of Tv - m are unchanged)
-                                const int tb2 = min(max(__float_as_int(yb + F5_MAGIC) + s, tlo), thi);
+                                // (16-bit clamp: only the low half of Tv + F5_APP0 reaches W)
+                                const uint32_t tb2 = clamp_i16((uint32_t)(__float_as_int(yb + F5_MAGIC) + s),
+                                                               tlo, thi);
                                 // W = (Tv << 16) | S bias, Tv = tb2 - F5_MAGIC_BITS - S bias
-                                uint32_t wn = (uint32_t)tb2 * 65536u + F5_WBIAS;
-                                if (UCN) wn |= (appb >= F5_APP0) ? 0x8000u : 0u;
+                                uint32_t wn = tb2 * 65536u + F5_WBIAS;
+                                if (UCN) wn |= ((uint32_t)appb >> 8) & 0x8000u;
                                 const_cast<uint32_t*>(Wr)[j * 64] = wn;
-                            } else {
-                                nbits += (uint32_t)(appt >= F5_APP0) & cvalid;
                             }
                         }
                     }
@@ -567,7 +591,8 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     const float ch = CH[e];
                     const int app = q_scaled5(ch * inv, qmf) + s + sb;
                     const int appt = ((int)v < a.target_bits) ? app : INT_MIN;
-                    amax = max(amax, appt == INT_MIN ? INT_MIN : appt + F5_APP0);
+                    amax = max(amax, appt == INT_MIN ? INT_MIN : appt + F5_APPH);
+                    aor |= (appt == INT_MIN) ? 0u : (uint32_t)(appt + F5_APPH);
                     if (!last) {
                         const int tn = min(max(q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], qmf) + s + sb,
                                                -2 * qmax), 2 * qmax);
@@ -577,8 +602,8 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     }
                 }
             }
-            any_hd = amax >= F5_APP0;
-            any_pos = amax > F5_APP0;
+            any_hd = last ? (amax >= F5_APPH) : ((aor >> 23) & 1u);
+            any_pos = amax > F5_APPH;
         } else {
         for (int r = 0; r < ((a.ablate & 4) ? 0 : a.nent); ++r) {
             const int e = tid + r * NT;
