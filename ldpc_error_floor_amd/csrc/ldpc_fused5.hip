@@ -340,29 +340,33 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
 #pragma unroll
             for (int w = 0; w < NSEL; ++w) NG[w] = 0;
             uint32_t syn = 0;
-            // one chunk of 8 edges, straight-line: padding slots (k >= deg) read the dummy word
-            // (|v2c| never minimal, positive sign).  Skipping them behind scalar branches was
-            // measured slower: the branches split the chunk's schedule.
-            auto chunk1 = [&](const int c8, const bool full) __attribute__((always_inline)) {
+            // one chunk of up to 8 edges, straight-line.  NE = edges present (compile time):
+            // 6 and 7 cover rows ending inside the chunk; other short chunks run as 8 and their
+            // padding slots (k >= deg) read the dummy word (|v2c| never below qmax, positive
+            // sign).  Skipping slots behind scalar branches was measured slower: the branches
+            // split the chunk's schedule.
+            auto chunk1 = [&](const int c8, auto ne) __attribute__((always_inline)) {
+                constexpr int NE = decltype(ne)::value;
                 uint32_t wv[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
+                for (int j = 0; j < NE; ++j) {
                     const int k = c8 + j;
-                    if (k < MAXDEG && (full || k < deg)) {
+                    if (k < MAXDEG) {
                         const uint32_t pk = gad[gi][k >> 1];
                         const uint32_t addr = (k & 1) ? hi16(pk) : lo16(pk);
                         wv[j] = *reinterpret_cast<const LdsU32*>(addr);
                     }
                 }
-                const uint32_t R0 = perm_word(gi, c8 / 4), R1 = perm_word(gi, c8 / 4 + 1);
-                // V->C before Q, times 256: d256 = (Tv - m) << 8, sign-extended.  All eight
+                const uint32_t R0 = perm_word(gi, c8 / 4);
+                const uint32_t R1 = (NE > 4) ? perm_word(gi, c8 / 4 + 1) : 0u;
+                // V->C before Q, times 256: d256 = (Tv - m) << 8, sign-extended.  All of them
                 // first: an SDWA result with a sub-dword dst_sel read by the very next
                 // instruction costs a wait state.
                 uint32_t dd[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
+                for (int j = 0; j < NE; ++j) {
                     const int k = c8 + j;
-                    if (k < MAXDEG && (full || k < deg)) {
+                    if (k < MAXDEG) {
                         if constexpr (PEW) {
                             const int cold = msg(gi, k, j < 4 ? R0 : R1, atp, aup, r0);
                             dd[j] = sub_d256<0>(wv[j], (uint32_t)cold);
@@ -379,35 +383,48 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
+                for (int j = 0; j < NE; ++j) {
                     const int k = c8 + j;
                     if (k < MAXDEG) {
-                        if (full || k < deg) {
-                            const uint32_t d256 = dd[j];
-                            // key = |d| << 8 | code, all in the low 16 bits
-                            const uint32_t key = max_i16(d256, 0u - d256) | SL::code(k);
-                            // append the byte of sign copies of d to the edge's selector word
-                            NG[k / 4] = __builtin_amdgcn_alignbit(NG[k / 4], d256, 24);
-                            const uint32_t o1 = c1;
-                            c1 = min_u16(o1, key);
-                            c2 = med3u(o1, c2, key);
-                        } else {
-                            NG[k / 4] <<= 8;                                     // positive
-                        }
+                        const uint32_t d256 = dd[j];
+                        // key = |d| << 8 | code, all in the low 16 bits
+                        const uint32_t key = max_i16(d256, 0u - d256) | SL::code(k);
+                        // append the byte of sign copies of d to the edge's selector word
+                        NG[k / 4] = __builtin_amdgcn_alignbit(NG[k / 4], d256, 24);
+                        const uint32_t o1 = c1;
+                        c1 = min_u16(o1, key);
+                        c2 = med3u(o1, c2, key);
                     }
                 }
+                // absent slots of the chunk enter as positive (zero) sign bytes
+#pragma unroll
+                for (int w = 0; w < NSEL; ++w) {
+                    int n = 0;
+#pragma unroll
+                    for (int j = NE; j < 8; ++j) n += (c8 + j < MAXDEG && (c8 + j) / 4 == w);
+                    if (n > 0) NG[w] = (n >= 4) ? 0u : (NG[w] << (8 * n));
+                }
             };
+            using N8 = std::integral_constant<int, 8>;
+            using N7 = std::integral_constant<int, 7>;
+            using N6 = std::integral_constant<int, 6>;
 #pragma unroll
             for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
-                if (c8 < deg) {
-                    chunk1(c8, true);
-                } else {
-                    // chunk skipped (deg <= c8): its edges enter as positive (zero) sign fields
+                const int n = deg - c8;
+                if (n >= 8 || n < 6) {
+                    if (n > 0) chunk1(c8, N8{});
+                    else {
+                        // chunk skipped (deg <= c8): its edges enter as positive (zero) sign fields
 #pragma unroll
-                    for (int w = 0; w < NSEL; ++w) {
-                        const int n = SL::in_chunk(w, c8);
-                        if (n > 0) NG[w] = (n >= 4) ? 0u : (NG[w] << (8 * n));
+                        for (int w = 0; w < NSEL; ++w) {
+                            const int nn = SL::in_chunk(w, c8);
+                            if (nn > 0) NG[w] = (nn >= 4) ? 0u : (NG[w] << (8 * nn));
+                        }
                     }
+                } else if (n == 7) {
+                    chunk1(c8, N7{});
+                } else {
+                    chunk1(c8, N6{});
                 }
             }
             // ---- new state: quantized minima, selector bytes, argmin bit ----
@@ -463,12 +480,16 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
             const int r0 = (int)(ri & 0xFFFFu);
             const int deg = (int)((ri >> 16) & 0xFFu);
-            auto chunk2 = [&](const int c8, const bool full) __attribute__((always_inline)) {
-                const uint32_t R0 = perm_word(gi, c8 / 4), R1 = perm_word(gi, c8 / 4 + 1);
+            // whole 8-edge chunks: padding slots add into the dummy word.  (Pass 1's 6- and
+            // 7-edge chunk shapes here measured 2.5% slower on wman than the plain chunks.)
+            auto chunk2 = [&](const int c8, auto ne) __attribute__((always_inline)) {
+                constexpr int NE = decltype(ne)::value;
+                const uint32_t R0 = perm_word(gi, c8 / 4);
+                const uint32_t R1 = (NE > 4) ? perm_word(gi, c8 / 4 + 1) : 0u;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
+                for (int j = 0; j < NE; ++j) {
                     const int k = c8 + j;
-                    if (k < MAXDEG && (full || k < deg)) {
+                    if (k < MAXDEG) {
                         const uint32_t pk = gad[gi][k >> 1];
                         const uint32_t addr = (k & 1) ? hi16(pk) : lo16(pk);
                         const int c = msg(gi, k, j < 4 ? R0 : R1, at, au, r0);
@@ -476,9 +497,11 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     }
                 }
             };
+            using N8 = std::integral_constant<int, 8>;
 #pragma unroll
             for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
-                if (c8 < deg) chunk2(c8, true);
+                const int n = deg - c8;
+                if (n > 0) chunk2(c8, N8{});
             }
         }
         __syncthreads();
