@@ -74,7 +74,9 @@ struct F5Args {
     int nfull, cpw;    // VN: full 64-entry chunks, chunks per wave
     int Mp;            // proto rows
     const float* betas;        // [T][N] beta / step (setup kernel)
-    const uint16_t* qtab;      // [T][Mp][qmax+2] weight table (setup kernel), LUT builds only
+    const uint16_t* qtab;      // [T][qslice] weight tables (setup kernel), LUT builds only
+    int qslice;                // halfwords per iteration: [alpha | alpha_ucn][Mp][qmax+2], even
+    int qucn;                  // halfword offset of the alpha_ucn table inside a slice
     const uint32_t* gad;       // [ngroups][NPK][64] packed edge byte addresses (k_f5_gad)
     const uint4* grow;         // [ngroups] {r0 | deg << 16 | row << 24, lane-valid mask lo, hi, 0}
     unsigned long long* stamps;   // diagnostic (LDPC_DIAG_STAMPS): [block][8] s_memtime marks
@@ -186,13 +188,20 @@ struct Sel {
         if (a.stamps && tid == 0) a.stamps[(size_t)blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
+// occupancy target (waves per SIMD) of a shape: the VGPR budget that lets the planned number of
+// workgroups share a CU (plan5 assumes the same figure)
+constexpr int f5_wpe(int cw, int maxg, int maxdeg) {
+    return (cw == 16 && maxdeg == 16) ? 6 : (cw == 4) ? 7 : (cw == 8 && maxg == 2) ? 6 : 1;
+}
+constexpr int f5_logcw(int cw) { return cw == 64 ? 6 : cw == 32 ? 5 : cw == 16 ? 4 : cw == 8 ? 3 : 2; }
+
 template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW, bool OUT, bool LUT>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(CW == 16 && MAXDEG == 16 ? 6 : 1)))
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(f5_wpe(CW, MAXG, MAXDEG))))
 k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ alpha_ucn) {
     using SL = Sel<MAXDEG>;
     constexpr int NSEL = SL::NSEL;
     constexpr int SLOTS = 64 / CW;
-    constexpr int LOGCW = (CW == 64) ? 6 : (CW == 32) ? 5 : (CW == 16) ? 4 : 3;
+    constexpr int LOGCW = f5_logcw(CW);
     constexpr int NPK = (MAXDEG + 1) / 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nv = a.n_vars;
@@ -202,7 +211,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     float* BETA = CH + total;                                                     // [T*N]
     unsigned long long* RED = reinterpret_cast<unsigned long long*>(
         smem + ((((size_t)total + CW) * 4 + (size_t)total * 4 + (size_t)a.T * a.N * 4 + 15) & ~(size_t)15));
-    uint16_t* QT = reinterpret_cast<uint16_t*>(RED + 8);                          // [T][Mp][qmax+2]
+    uint16_t* QT = reinterpret_cast<uint16_t*>(RED + 8);                          // [2][qslice]
 
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();   // edge addresses are LDS-absolute
     const int tid = threadIdx.x;
@@ -210,7 +219,6 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     const int NWV = NT >> 6;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int slot = lane >> LOGCW;
     const int cw = lane & (CW - 1);
     const int64_t b0 = (int64_t)blockIdx.x * CW;
     const int64_t nvalid = (b0 + CW <= a.B) ? CW : (a.B - b0);
@@ -249,9 +257,10 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         // beta / step and the weight table come precomputed (k_f5_tables): plain copies
         for (int f = tid; f < a.T * a.N; f += NT) BETA[f] = a.betas[f];
         if (tid < 8) RED[tid] = (tid == 1) ? ~0ull : 0ull;
-        if constexpr (LUT) {
-            const int nqt = a.T * a.Mp * (qmax + 2);
-            for (int f = tid; f < nqt; f += NT) QT[f] = a.qtab[f];
+        if constexpr (LUT) {       // iteration 0's slice; slice t+1 is copied during VN t
+            const int nw32 = a.qslice >> 1;
+            for (int f = tid; f < nw32; f += NT)
+                reinterpret_cast<uint32_t*>(QT)[f] = reinterpret_cast<const uint32_t*>(a.qtab)[f];
         }
         __syncthreads();
         for (int e = tid; e < total; e += NT) CH[e] = scr[(e & (CW - 1)) * rl + (e >> LOGCW)];
@@ -324,6 +333,13 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         }
         const float* at = alpha + (size_t)t * a.E;
         const float* au = UCN ? alpha_ucn + (size_t)t * a.E : nullptr;
+        // the next iteration's weight-table slice, loaded now, stored to LDS in the VN phase
+        // (double buffer: slice t+1 goes where slice t-1 was, which pass 1 of t no longer reads)
+        uint32_t qnext = 0;
+        if constexpr (LUT) {
+            if (t + 1 < a.T && tid < (a.qslice >> 1))
+                qnext = reinterpret_cast<const uint32_t*>(a.qtab + (size_t)(t + 1) * a.qslice)[tid];
+        }
         const float* atp = alpha + (size_t)(t > 0 ? t - 1 : 0) * a.E;
         const float* aup = UCN ? alpha_ucn + (size_t)(t > 0 ? t - 1 : 0) * a.E : nullptr;
         // ======== check nodes: pass 1 (read Tv, fold minima and signs) + new state ==========
@@ -339,7 +355,14 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             uint32_t NG[NSEL];
 #pragma unroll
             for (int w = 0; w < NSEL; ++w) NG[w] = 0;
-            uint32_t syn = 0;
+            uint32_t syn = 0;     // UCN: XOR of the edges' W words (bit 15: previous hard decisions)
+            // this row's weights as scalar loads issued ahead of the chunks (a per-lane choice
+            // between two global addresses would be a vector load waited on in the state update)
+            float wa = 0.f, wu = 0.f;
+            if constexpr (!PEW && !LUT) {
+                wa = at[r0];
+                if constexpr (UCN) wu = au[r0];
+            }
             // one chunk of up to 8 edges, straight-line.  NE = edges present (compile time):
             // 6 and 7 cover rows ending inside the chunk; other short chunks run as 8 and their
             // padding slots (k >= deg) read the dummy word (|v2c| never below qmax, positive
@@ -379,7 +402,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                                 default: dd[j] = sub_d256<3>(wv[j], R); break;
                             }
                         }
-                        if (UCN) syn ^= (wv[j] >> 15) & 1u;
+                        if (UCN) syn ^= wv[j];
                     }
                 }
 #pragma unroll
@@ -405,26 +428,26 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     if (n > 0) NG[w] = (n >= 4) ? 0u : (NG[w] << (8 * n));
                 }
             };
-            using N8 = std::integral_constant<int, 8>;
-            using N7 = std::integral_constant<int, 7>;
-            using N6 = std::integral_constant<int, 6>;
 #pragma unroll
             for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
                 const int n = deg - c8;
-                if (n >= 8 || n < 6) {
-                    if (n > 0) chunk1(c8, N8{});
-                    else {
-                        // chunk skipped (deg <= c8): its edges enter as positive (zero) sign fields
+                // a row ending inside the chunk runs the shape with exactly its edges (shapes
+                // below 6 only where a shape's rows are that short: 5G-like graphs)
+                if (n >= 8) chunk1(c8, std::integral_constant<int, 8>{});
+                else if (n == 7) chunk1(c8, std::integral_constant<int, 7>{});
+                else if (n == 6) chunk1(c8, std::integral_constant<int, 6>{});
+                else if (CW <= 8 && n == 5) chunk1(c8, std::integral_constant<int, 5>{});
+                else if (CW <= 8 && n == 4) chunk1(c8, std::integral_constant<int, 4>{});
+                else if (CW <= 8 && n == 3) chunk1(c8, std::integral_constant<int, 3>{});
+                else if (CW <= 8 && n == 2) chunk1(c8, std::integral_constant<int, 2>{});
+                else if (n > 0) chunk1(c8, std::integral_constant<int, 8>{});
+                else {
+                    // chunk skipped (deg <= c8): its edges enter as positive (zero) sign fields
 #pragma unroll
-                        for (int w = 0; w < NSEL; ++w) {
-                            const int nn = SL::in_chunk(w, c8);
-                            if (nn > 0) NG[w] = (nn >= 4) ? 0u : (NG[w] << (8 * nn));
-                        }
+                    for (int w = 0; w < NSEL; ++w) {
+                        const int nn = SL::in_chunk(w, c8);
+                        if (nn > 0) NG[w] = (nn >= 4) ? 0u : (NG[w] << (8 * nn));
                     }
-                } else if (n == 7) {
-                    chunk1(c8, N7{});
-                } else {
-                    chunk1(c8, N6{});
                 }
             }
             // ---- new state: quantized minima, selector bytes, argmin bit ----
@@ -436,6 +459,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             }
             // message sign = V->C sign XOR (count of positives odd): applied to P as a byte
             // swap inside each half; for PEW (P holds magnitudes) to the selector bytes
+            if constexpr (UCN) syn = (syn >> 15) & 1u;
             const bool podd = ((uint32_t)deg + nbit) & 1u;
             const uint32_t code = c1 & 255u;
             const uint32_t onebit = 1u << (code & 31u);
@@ -455,11 +479,12 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     // [+m, -m] byte pairs of Q(relu(m*w)) for this iteration and proto row
                     const int ib = (deg < 2) ? qmax + 1 : min((int)(c2 >> 8), qmax);
                     const int row = (int)((ri >> 24) & 0xFFu);
-                    const uint16_t* qt = QT + (t * a.Mp + row) * (qmax + 2);
+                    const uint16_t* qt = QT + (t & 1) * a.qslice + ((UCN && syn) ? a.qucn : 0) +
+                                         row * (qmax + 2);
                     p = (uint32_t)qt[m1] | ((uint32_t)qt[ib] << 16);
                 } else {
                     const int m2 = (deg < 2) ? F5_BIG_U : min((int)(c2 >> 8), qmax);
-                    const float w = (UCN && syn) ? au[r0] : at[r0];
+                    const float w = (UCN && syn) ? wu : wa;
                     const int mA = q_mag5(m1, w, step, inv, qmax);
                     const int mB = q_mag5(m2, w, step, inv, qmax);
                     const uint32_t pa = ((uint32_t)mA & 0xFFu) | (((uint32_t)(-mA) & 0xFFu) << 8);
@@ -508,6 +533,10 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         if (t == 0) F5_STAMP(6);
         // ======== variable nodes ===========================================================
         const bool last = (t == a.T - 1);
+        if constexpr (LUT) {
+            if (!last && tid < (a.qslice >> 1))
+                reinterpret_cast<uint32_t*>(QT + ((t + 1) & 1) * a.qslice)[tid] = qnext;
+        }
         const float* bnext = BETA + (size_t)(last ? t : t + 1) * a.N;
         uint32_t any_hd = 0, any_pos = 0, nbits = 0;
         const float qmf = (float)qmax;
@@ -710,21 +739,27 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
 
 // Per-decode tables shared by every workgroup:
 //   betas[t][n] = beta[t][n] / step  (a power of two: fl32(ch*beta)/step == fl32(ch*(beta/step)))
-//   qtab[t][row][m] = [+q, -q] bytes, q = Q(relu(|o| * alpha_t,row)), |o| = m grid units
-//                     (m = qmax+1 stands for "no other edge", the 10000 value)
-__global__ void k_f5_tables(const float* __restrict__ alpha, const float* __restrict__ beta,
-                            const int32_t* __restrict__ row_ptr, int T, int Mp, int E, int N,
-                            int qmax, float step, float inv, float* betas, uint16_t* qtab) {
+//   qtab[t][tab][row][m] = [+q, -q] bytes, q = Q(relu(|o| * w)), |o| = m grid units
+//                     (m = qmax+1 stands for "no other edge", the 10000 value), w = alpha_t,row
+//                     (tab 0) or alpha_ucn_t,row (tab 1, UCN only); qslice halfwords per t
+__global__ void k_f5_tables(const float* __restrict__ alpha, const float* __restrict__ alpha_ucn,
+                            const float* __restrict__ beta, const int32_t* __restrict__ row_ptr,
+                            int T, int Mp, int E, int N, int qmax, float step, float inv,
+                            int qslice, float* betas, uint16_t* qtab) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f < T * N) betas[f] = beta[f] * inv;
     const int nq = qmax + 2;
-    if (qtab && f < T * Mp * nq) {
-        const int m = f % nq;
-        const int tr = f / nq;
-        const int tt = tr / Mp, row = tr - tt * Mp;
-        const float w = alpha[(size_t)tt * E + row_ptr[row]];
-        const int q = q_mag5(m > qmax ? F5_BIG_U : m, w, step, inv, qmax);
-        qtab[f] = (uint16_t)(((uint32_t)q & 0xFFu) | (((uint32_t)(-q) & 0xFFu) << 8));
+    if (qtab && f < T * qslice) {
+        const int tt = f / qslice, rem = f - tt * qslice;
+        const int tab = rem / (Mp * nq), r2 = rem - tab * (Mp * nq);
+        const int row = r2 / nq, m = r2 - row * nq;
+        uint16_t v = 0;
+        if (tab == 0 || (tab == 1 && alpha_ucn)) {
+            const float w = (tab ? alpha_ucn : alpha)[(size_t)tt * E + row_ptr[row]];
+            const int q = q_mag5(m > qmax ? F5_BIG_U : m, w, step, inv, qmax);
+            v = (uint16_t)(((uint32_t)q & 0xFFu) | (((uint32_t)(-q) & 0xFFu) << 8));
+        }
+        qtab[f] = v;
     }
 }
 
@@ -777,6 +812,8 @@ constexpr Shape5 kShapes5[] = {
     {8, 5, 16, true},     // 5G BG2-like (z=64, deg <= 10)
     {64, 3, 8, true},     // z=1 sparse (MacKay)
     {64, 2, 32, true},    // z=1 dense rows (BCH)
+    {4, 3, 12, true},     // 5G BG2-like at two workgroups per CU (z=64: 16 slots, 4 codewords)
+    {8, 2, 24, true},     // 802.11n-like at three workgroups per CU
     // measured and dropped: {8, 2, 16} at 8 waves/SIMD (64 VGPRs) ran 28.3 ms vs 21.3 ms for
     // {16, 3, 16} on wman -- twice the per-workgroup fixed cost per codeword
 };
@@ -808,11 +845,17 @@ Plan5 plan5(const DevGraph& g, int T) {
         const size_t lds = f5_lds(g.n_vars, sh.cw, T, g.N);
         if (lds > F5_LDS_MAX) continue;
         if ((size_t)g.n_vars * sh.cw * 4 + sh.cw * 4 >= 65536) continue;    // 16-bit addresses
+        // resident workgroups per CU: LDS and the shape's VGPR budget (f5_wpe waves per SIMD;
+        // a workgroup puts ceil(nw/4) waves on its busiest SIMD and the next workgroup starts
+        // on the same SIMD: measured, a 14-wave group at 7 waves/SIMD runs alone).  VALU issue
+        // saturates around 6 waves per SIMD, so waves beyond 24 per CU earn nothing.
         const int wg_lds = (int)(F5_LDS_MAX / lds);
-        const int wg_waves = 32 / nw;
+        const int wpe = std::max(f5_wpe(sh.cw, sh.maxg, sh.maxdeg), 4);
+        const int wg_waves = wpe / ((nw + 3) / 4);
         const int wgs = std::max(1, std::min(wg_lds, wg_waves));
         const double eff = (double)g.max_cdeg / (double)(((g.max_cdeg + 7) / 8) * 8);
-        const double score = (double)(wgs * nw) * eff + 1e-3 * sh.cw;
+        const double util = (double)g.z / (double)(hstep * slots);    // lanes on real checks
+        const double score = (double)std::min(wgs * nw, 24) * eff * util + 1e-3 * sh.cw;
         if (score > best_score) {
             best_score = score;
             best.shape = si;
@@ -843,7 +886,7 @@ int launch5o(const F5Args& a, int nblocks, int nw, size_t lds, const float* alph
 template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW>
 int launch5k(const F5Args& a, int nblocks, int nw, size_t lds, bool lut, const float* alpha,
              const float* alpha_ucn, hipStream_t s) {
-    constexpr bool CANLUT = !UCN && !PEW;
+    constexpr bool CANLUT = !PEW;
     const bool out = a.app_out || a.hd_out;
     if (CANLUT && lut)
         return out ? launch5o<CW, MAXG, MAXDEG, UCN, PEW, true, CANLUT>(a, nblocks, nw, lds, alpha, alpha_ucn, s)
@@ -896,11 +939,14 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     Plan5 p = plan5(g, b.T);
     if (p.shape < 0 || qmax > 31) return LDPC_ERR_UNSUPPORTED;   // pass 1's 8-bit V->C range
     const Shape5& sh = kShapes5[p.shape];
-    // weight table (uniform row weights, no UCN set): only if it costs no workgroup slot per CU
-    bool lut = !per_edge_w && b.alpha_ucn == nullptr && g.M < 256 &&
+    // weight tables (uniform row weights): only if they cost no workgroup slot per CU
+    // per-iteration slices of the weight tables, double-buffered in LDS
+    const int qucn = g.M * (qmax + 2);
+    const int qslice = ((b.alpha_ucn ? 2 : 1) * qucn + 1) & ~1;
+    bool lut = !per_edge_w && g.M < 256 && (qslice >> 1) <= 64 * p.nw &&
                getenv("LDPC_F5_NOLUT") == nullptr;
     if (lut) {
-        const size_t lds_lut = p.lds + (((size_t)b.T * g.M * (qmax + 2) * 2 + 15) & ~(size_t)15);
+        const size_t lds_lut = p.lds + (((size_t)2 * qslice * 2 + 15) & ~(size_t)15);
         if (lds_lut > F5_LDS_MAX || F5_LDS_MAX / lds_lut < F5_LDS_MAX / p.lds) lut = false;
         else p.lds = lds_lut;
     }
@@ -939,7 +985,7 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     a.zmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.z - 1) / (uint64_t)g.z);
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // timing only
     // shared tables: one small launch per decode instead of per-workgroup dependent loads
-    const size_t nbeta = (size_t)b.T * g.N, nqt = (size_t)b.T * g.M * (qmax + 2);
+    const size_t nbeta = (size_t)b.T * g.N, nqt = (size_t)b.T * qslice;
     const int npk = (sh.maxdeg + 1) / 2;
     const size_t off_qt = (nbeta * 4 + 255) & ~(size_t)255;
     const size_t off_gad = (off_qt + nqt * 2 + 255) & ~(size_t)255;
@@ -962,9 +1008,9 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     {
         const size_t nthr = std::max(nbeta, lut ? nqt : (size_t)0);
         hipLaunchKernelGGL(k_f5_tables, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s,
-                           b.alpha, b.beta, g.row_ptr, b.T, g.M, g.E, g.N, qmax, step, 1.0f / step,
-                           betas, lut ? qtab : nullptr);
-        const int lcw = sh.cw == 64 ? 6 : sh.cw == 32 ? 5 : sh.cw == 16 ? 4 : 3;
+                           b.alpha, b.alpha_ucn, b.beta, g.row_ptr, b.T, g.M, g.E, g.N, qmax, step,
+                           1.0f / step, qslice, betas, lut ? qtab : nullptr);
+        const int lcw = f5_logcw(sh.cw);
         hipLaunchKernelGGL(k_f5_gad, dim3((unsigned)((p.ngroups * 64 + 255) / 256)), dim3(256), 0, s,
                            g.row_ptr, g.pe_col, g.pe_shift, p.ngroups, p.hstep, g.z, lcw, sh.maxdeg,
                            npk, g.n_vars * sh.cw, gad, grow);
@@ -972,6 +1018,8 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     }
     a.betas = betas;
     a.qtab = qtab;
+    a.qslice = qslice;
+    a.qucn = qucn;
     a.gad = gad;
     a.grow = grow;
     const int nblocks = (int)((b.B + sh.cw - 1) / sh.cw);
@@ -987,6 +1035,8 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
         case 2: rc = launch5s<8, 5, 16>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
         case 3: rc = launch5s<64, 3, 8>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
         case 4: rc = launch5s<64, 2, 32>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 5: rc = launch5s<4, 3, 12>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 6: rc = launch5s<8, 2, 24>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
         default: rc = LDPC_ERR_UNSUPPORTED;
     }
     if (diag) {

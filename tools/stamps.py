@@ -36,7 +36,10 @@ def main():
     ph("it0 pass2+sync", 5, 6)
     ph("it0 VN+sync", 6, 9)
     T = a.T
-    its = [s[:, 9 + t] - s[:, 8 + t] for t in range(T - 1)] + [s[:, 30] - s[:, 8 + T - 1]]
+    TS = min(T, 22)                      # the kernel stamps iteration starts t < 22 only
+    its = [s[:, 9 + t] - s[:, 8 + t] for t in range(TS - 1)]
+    if TS == T:
+        its.append(s[:, 30] - s[:, 8 + T - 1])
     print("iteration means (us):", " ".join(f"{us(x.mean()):.2f}" for x in its))
     ph("whole", 0, 30)
     span = s[:, 30].max() - t0
@@ -67,7 +70,7 @@ def main():
     print("first blocks on one CU (start, end, us from launch start; hw id):")
     for b in idx:
         print(f"  block {b:6d}  {us(s[b, 0] - t0):9.2f} -> {us(s[b, 30] - t0):9.2f}  "
-              f"it starts " + " ".join(f"{us(s[b, 8 + t] - t0):.1f}" for t in range(0, T, 4))
+              f"it starts " + " ".join(f"{us(s[b, 8 + t] - t0):.1f}" for t in range(0, min(T, 22), 4))
               + f"  hw {int(hw[b]) & 0xFFFFFFFF:08x}")
 
 
