@@ -191,7 +191,8 @@ struct Sel {
 // occupancy target (waves per SIMD) of a shape: the VGPR budget that lets the planned number of
 // workgroups share a CU (plan5 assumes the same figure)
 constexpr int f5_wpe(int cw, int maxg, int maxdeg) {
-    return (cw == 16 && maxdeg == 16) ? 6 : (cw == 4) ? 7 : (cw == 8 && maxg == 2) ? 6 : 1;
+    return (cw == 16 && maxdeg == 16) ? 6 : (cw == 4 && maxg == 4) ? 4 : (cw == 4) ? 7
+         : (cw == 8 && maxg == 2) ? 6 : 1;
 }
 constexpr int f5_logcw(int cw) { return cw == 64 ? 6 : cw == 32 ? 5 : cw == 16 ? 4 : cw == 8 ? 3 : 2; }
 
@@ -208,9 +209,9 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     const int total = nv * CW;
     uint32_t* W = reinterpret_cast<uint32_t*>(smem);                              // [nv*CW + CW]
     float* CH = reinterpret_cast<float*>(smem + ((size_t)total + CW) * 4);        // [nv*CW]
-    float* BETA = CH + total;                                                     // [T*N]
+    float* BETA = CH + total;                     // [2][N]: beta_t / step in slot t & 1
     unsigned long long* RED = reinterpret_cast<unsigned long long*>(
-        smem + ((((size_t)total + CW) * 4 + (size_t)total * 4 + (size_t)a.T * a.N * 4 + 15) & ~(size_t)15));
+        smem + ((((size_t)total + CW) * 4 + (size_t)total * 4 + (size_t)2 * a.N * 4 + 15) & ~(size_t)15));
     uint16_t* QT = reinterpret_cast<uint16_t*>(RED + 8);                          // [2][qslice]
 
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();   // edge addresses are LDS-absolute
@@ -255,7 +256,8 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 if (v < nv) scr[r * rl + v] = x[r];
         }
         // beta / step and the weight table come precomputed (k_f5_tables): plain copies
-        for (int f = tid; f < a.T * a.N; f += NT) BETA[f] = a.betas[f];
+        // beta_0 and beta_1; slice t+1 (t >= 1) is copied during iteration t's check phase
+        for (int f = tid; f < min(a.T, 2) * a.N; f += NT) BETA[f] = a.betas[f];
         if (tid < 8) RED[tid] = (tid == 1) ? ~0ull : 0ull;
         if constexpr (LUT) {       // iteration 0's slice; slice t+1 is copied during VN t
             const int nw32 = a.qslice >> 1;
@@ -340,6 +342,11 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             if (t + 1 < a.T && tid < (a.qslice >> 1))
                 qnext = reinterpret_cast<const uint32_t*>(a.qtab + (size_t)(t + 1) * a.qslice)[tid];
         }
+        // beta_{t+1} for this iteration's VN phase, stored to LDS before the pass-2 barrier
+        // (its slot last held beta_{t-1}, read by the VN phase of iteration t-2)
+        const bool bcopy = t >= 1 && t + 1 < a.T && tid < a.N;
+        float bload = 0.f;
+        if (bcopy) bload = a.betas[(size_t)(t + 1) * a.N + tid];
         const float* atp = alpha + (size_t)(t > 0 ? t - 1 : 0) * a.E;
         const float* aup = UCN ? alpha_ucn + (size_t)(t > 0 ? t - 1 : 0) * a.E : nullptr;
         // ======== check nodes: pass 1 (read Tv, fold minima and signs) + new state ==========
@@ -529,6 +536,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 if (n > 0) chunk2(c8, N8{});
             }
         }
+        if (bcopy) BETA[((t + 1) & 1) * a.N + tid] = bload;
         __syncthreads();
         if (t == 0) F5_STAMP(6);
         // ======== variable nodes ===========================================================
@@ -537,7 +545,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             if (!last && tid < (a.qslice >> 1))
                 reinterpret_cast<uint32_t*>(QT + ((t + 1) & 1) * a.qslice)[tid] = qnext;
         }
-        const float* bnext = BETA + (size_t)(last ? t : t + 1) * a.N;
+        const float* bnext = BETA + (size_t)((t + 1) & 1) * a.N;     // unused when last
         uint32_t any_hd = 0, any_pos = 0, nbits = 0;
         const float qmf = (float)qmax;
         const int sb = -(int)F5_SBIAS;
@@ -767,15 +775,41 @@ __global__ void k_f5_tables(const float* __restrict__ alpha, const float* __rest
 // h = hg * SLOTS + slot of proto row i (grp = i * hstep + hg); edge k of that row reads
 // W[(pe_col * z + (h + shift) mod z) * CW + cw], packed as byte offsets two per word.  Lanes
 // with h >= z (last group of a row) mirror slot 0's row and are masked out of the results.
+//
+// Table position s is what wave s % nw runs as its group s / nw.  bal = 0: position s is group
+// s.  bal = 1 (graphs with very unequal row degrees): groups are ranked by row degree, heaviest
+// first, and dealt to the waves in snake order (round r left to right when r is even, right to
+// left when odd), so every wave's edge count is within one row's degree of the others'.
+__device__ int f5_group_of(int s, const int32_t* __restrict__ row_ptr, int M, int hstep,
+                           int ngroups, int nw, int bal) {
+    if (!bal) return s;
+    const int r = s / nw, w = s - r * nw;
+    const int nr = min(nw, ngroups - r * nw);               // groups dealt in round r
+    const int rank = r * nw + ((r & 1) ? nr - 1 - w : w);
+    // rank of group (i, hg) = hstep * #rows heavier than i (ties: lower row first) + hg
+    for (int i = 0; i < M; ++i) {
+        const int di = row_ptr[i + 1] - row_ptr[i];
+        int before = 0;
+        for (int i2 = 0; i2 < M; ++i2) {
+            const int d2 = row_ptr[i2 + 1] - row_ptr[i2];
+            before += (d2 > di || (d2 == di && i2 < i));
+        }
+        if (rank >= before * hstep && rank < (before + 1) * hstep) return i * hstep + (rank - before * hstep);
+    }
+    return s;
+}
+
 __global__ void k_f5_gad(const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ pe_col,
-                         const int32_t* __restrict__ pe_shift, int ngroups, int hstep, int z,
-                         int logcw, int maxdeg, int npk, int total, uint32_t* gad, uint4* grow) {
+                         const int32_t* __restrict__ pe_shift, int M, int ngroups, int hstep, int z,
+                         int logcw, int maxdeg, int npk, int total, int nw, int bal, uint32_t* gad,
+                         uint4* grow) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= ngroups * 64) return;
     const int grp = f >> 6, lane = f & 63;
     const int cwn = 1 << logcw, slots = 64 >> logcw;
     const int slot = lane >> logcw, cw = lane & (cwn - 1);
-    const int i = grp / hstep, hg = grp - i * hstep;
+    const int rg = f5_group_of(grp, row_ptr, M, hstep, ngroups, nw, bal);
+    const int i = rg / hstep, hg = rg - i * hstep;
     const int r0 = row_ptr[i], deg = row_ptr[i + 1] - r0;
     const int h = hg * slots + slot;
     const int hl = (h < z) ? h : hg * slots;
@@ -805,21 +839,24 @@ __global__ void k_f5_gad(const int32_t* __restrict__ row_ptr, const int32_t* __r
 struct Shape5 {
     int cw, maxg, maxdeg;
     bool autosel;  // considered by plan5 (else only via LDPC_F5_SHAPE=<index>)
+    bool bal;      // deal groups to waves by row degree (k_f5_gad); LDPC_F5_BALANCE=0/1 overrides
 };
 constexpr Shape5 kShapes5[] = {
-    {16, 3, 16, true},    // wman-like (z=24, deg 14-15)
-    {16, 3, 24, true},    // 802.11n-like (deg 22)
-    {8, 5, 16, true},     // 5G BG2-like (z=64, deg <= 10)
-    {64, 3, 8, true},     // z=1 sparse (MacKay)
-    {64, 2, 32, true},    // z=1 dense rows (BCH)
-    {4, 3, 12, true},     // 5G BG2-like at two workgroups per CU (z=64: 16 slots, 4 codewords)
-    {8, 2, 24, true},     // 802.11n-like at three workgroups per CU
+    {16, 3, 16, true, false},    // wman-like (z=24, deg 14-15)
+    {16, 3, 24, true, false},    // 802.11n-like (deg 22)
+    {8, 5, 16, true, false},     // 5G BG2-like (z=64, deg <= 10)
+    {64, 3, 8, true, false},     // z=1 sparse (MacKay)
+    {64, 2, 32, true, false},    // z=1 dense rows (BCH)
+    {4, 3, 12, true, false},     // 5G BG2-like at two workgroups per CU (z=64: 16 slots, 4 codewords)
+    {8, 2, 24, true, false},     // 802.11n-like at three workgroups per CU
+    {4, 4, 20, true, true},      // 5G BG1-like (n = 2304 variables, deg 3-19, z = 72), one WG per CU
     // measured and dropped: {8, 2, 16} at 8 waves/SIMD (64 VGPRs) ran 28.3 ms vs 21.3 ms for
     // {16, 3, 16} on wman -- twice the per-workgroup fixed cost per codeword
 };
 
 size_t f5_lds(int nv, int cw, int T, int N) {
-    return ((((size_t)nv * cw + cw) * 4 + (size_t)nv * cw * 4 + (size_t)T * N * 4 + 15) & ~(size_t)15) + 8 * 8;
+    (void)T;
+    return ((((size_t)nv * cw + cw) * 4 + (size_t)nv * cw * 4 + (size_t)2 * N * 4 + 15) & ~(size_t)15) + 8 * 8;
 }
 
 struct Plan5 {
@@ -842,6 +879,7 @@ Plan5 plan5(const DevGraph& g, int T) {
         const int ngroups = g.M * hstep;
         const int nw = (ngroups + sh.maxg - 1) / sh.maxg;
         if (nw > 16 || nw < 1) continue;
+        if (g.N > 64 * nw) continue;                                    // beta slice copy
         const size_t lds = f5_lds(g.n_vars, sh.cw, T, g.N);
         if (lds > F5_LDS_MAX) continue;
         if ((size_t)g.n_vars * sh.cw * 4 + sh.cw * 4 >= 65536) continue;    // 16-bit addresses
@@ -1011,9 +1049,11 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
                            b.alpha, b.alpha_ucn, b.beta, g.row_ptr, b.T, g.M, g.E, g.N, qmax, step,
                            1.0f / step, qslice, betas, lut ? qtab : nullptr);
         const int lcw = f5_logcw(sh.cw);
+        const char* be = getenv("LDPC_F5_BALANCE");
+        const bool bal = be ? atoi(be) != 0 : sh.bal;
         hipLaunchKernelGGL(k_f5_gad, dim3((unsigned)((p.ngroups * 64 + 255) / 256)), dim3(256), 0, s,
-                           g.row_ptr, g.pe_col, g.pe_shift, p.ngroups, p.hstep, g.z, lcw, sh.maxdeg,
-                           npk, g.n_vars * sh.cw, gad, grow);
+                           g.row_ptr, g.pe_col, g.pe_shift, g.M, p.ngroups, p.hstep, g.z, lcw,
+                           sh.maxdeg, npk, g.n_vars * sh.cw, p.nw, bal ? 1 : 0, gad, grow);
         if (hipGetLastError() != hipSuccess) return LDPC_ERR_HIP;
     }
     a.betas = betas;
@@ -1037,6 +1077,7 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
         case 4: rc = launch5s<64, 2, 32>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
         case 5: rc = launch5s<4, 3, 12>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
         case 6: rc = launch5s<8, 2, 24>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 7: rc = launch5s<4, 4, 20>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
         default: rc = LDPC_ERR_UNSUPPORTED;
     }
     if (diag) {

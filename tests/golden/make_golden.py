@@ -355,6 +355,12 @@ def main():
         decoder_case(MF, PF, "g5bg2_222_q5_snr2.0",
                      "5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640", 64, [2, 2, 2], 2, 5,
                      20, 8, 2.0, blocks=gb, ps=1, pe=128, ss=513, se=640)
+    if want("g5bg1"):
+        # 5G BG1 n2112: no weights ship for it; random per-iteration scalars
+        # so beta changes every iteration (check degree 19, z = 72, puncture + shorten)
+        decoder_case(MF, PF, "g5bg1_303_q5_snr3.0",
+                     "5G_LDPC_R0.73_n_dec2304_n2112_k1536_z72_s1537_1584", 72, [3, 0, 3], 2,
+                     5, 12, 8, 3.0, random_weights=(0.5, 1.2), ps=1, pe=144, ss=1537, se=1584)
     if want("z1"):
         decoder_case(MF, PF, "mackay_333_q5_snr2.5", "MACKAY_N96_K48", 1, [3, 3, 3], 2, 5, 20,
                      16, 2.5, flat={0: 0.75, 1: 0.5, 2: 1.0})

@@ -125,7 +125,7 @@ def test_file_level_decoder_matches_reference(cuda_device):
 # every fused v5 shape (kShapes5 in ldpc_fused5.hip), forced with LDPC_F5_SHAPE, on every exact
 # QMS fixture it fits: APP export build and counters-only build, bit-exact
 F5_SHAPES = {0: "cw16,g3,d16", 1: "cw16,g3,d24", 2: "cw8,g5,d16", 3: "cw64,g3,d8",
-             4: "cw64,g2,d32", 5: "cw4,g3,d12", 6: "cw8,g2,d24"}
+             4: "cw64,g2,d32", 5: "cw4,g3,d12", 6: "cw8,g2,d24", 7: "cw4,g4,d20"}
 
 
 @pytest.mark.parametrize("shape", sorted(F5_SHAPES))
@@ -151,3 +151,25 @@ def test_fused5_every_shape_bit_exact(shape, cuda_device, monkeypatch):
         assert np.array_equal(cnt.cpu().numpy(), counters_from_app(c["app"])), name
         ran.append(name)
     assert ran, f"no fixture fits fused5 shape {F5_SHAPES[shape]}"
+
+
+@pytest.mark.parametrize("balance", ["0", "1"])
+def test_fused5_group_dealing_bit_exact(balance, cuda_device, monkeypatch):
+    """k_f5_gad's two group-to-wave mappings (identity, degree-ranked snake) on every exact
+    QMS fixture with the automatically chosen shape."""
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    monkeypatch.setenv("LDPC_F5_BALANCE", balance)
+    ran = 0
+    for name in DECODER_CASES:
+        c = load_case(name)
+        if not c["exact"] or c["dt"] != 2:
+            continue
+        Nt = c["Nt"] if c["Nt"] < c["g"].N else 0
+        dec = NMSDecoder(c["g"].proto, c["z"], c["W"], c["dt"], c["q"], target_node=Nt,
+                         device=cuda_device, kernel="fused")
+        if not dec.supports("fused") or not dec.kernel_info()[1].startswith("fused5["):
+            continue
+        app = dec.decode(c["llr"], app=True).app.cpu().numpy()
+        assert np.array_equal(app, c["app"]), (name, np.abs(app - c["app"]).max())
+        ran += 1
+    assert ran >= 5
