@@ -44,6 +44,9 @@ constexpr uint32_t F5_SBIAS = 16384;         // S field bias (bits 14..0)
 // padding edges read this word: Tv = 96 gives a V->C value in [65, 127] for any message
 // (|m| <= 31), positive, never below qmax and inside the 8-bit range pass 1 works in
 constexpr uint32_t F5_DUMMY_W = (96u << 16) | F5_SBIAS;
+// one dummy word per lane (after W): padding slots of different lanes never add into the same
+// LDS word, so their pass-2 atomics do not serialise
+constexpr int F5_NDUMMY = 64;
 constexpr float F5_MAGIC = 12582912.0f;                 // 1.5 * 2^23
 constexpr int F5_MAGIC_BITS = 0x4B400000;              // bit pattern of F5_MAGIC
 constexpr int F5_APP0 = F5_MAGIC_BITS + (int)F5_SBIAS;  // APP == 0 in the VN's biased domain
@@ -208,10 +211,10 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     const int nv = a.n_vars;
     const int total = nv * CW;
     uint32_t* W = reinterpret_cast<uint32_t*>(smem);                              // [nv*CW + CW]
-    float* CH = reinterpret_cast<float*>(smem + ((size_t)total + CW) * 4);        // [nv*CW]
+    float* CH = reinterpret_cast<float*>(smem + ((size_t)total + F5_NDUMMY) * 4); // [nv*CW]
     float* BETA = CH + total;                     // [2][N]: beta_t / step in slot t & 1
     unsigned long long* RED = reinterpret_cast<unsigned long long*>(
-        smem + ((((size_t)total + CW) * 4 + (size_t)total * 4 + (size_t)2 * a.N * 4 + 15) & ~(size_t)15));
+        smem + ((((size_t)total + F5_NDUMMY) * 4 + (size_t)total * 4 + (size_t)2 * a.N * 4 + 15) & ~(size_t)15));
     uint16_t* QT = reinterpret_cast<uint16_t*>(RED + 8);                          // [2][qslice]
 
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();   // edge addresses are LDS-absolute
@@ -272,7 +275,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             const int t0 = q_scaled5(CH[e] * BETA[__umulhi(v, a.zmagic)], (float)qmax);  // lw_0
             W[e] = ((uint32_t)t0 << 16) | ((uint32_t)(t0 >= 0) << 15) | F5_SBIAS;     // hd_{-1}
         }
-        if (tid < CW) W[total + tid] = F5_DUMMY_W;
+        if (tid < F5_NDUMMY) W[total + tid] = F5_DUMMY_W;
     }
 
     F5_STAMP(1);
@@ -447,6 +450,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 else if (CW <= 8 && n == 4) chunk1(c8, std::integral_constant<int, 4>{});
                 else if (CW <= 8 && n == 3) chunk1(c8, std::integral_constant<int, 3>{});
                 else if (CW <= 8 && n == 2) chunk1(c8, std::integral_constant<int, 2>{});
+                else if (CW <= 8 && n == 1) chunk1(c8, std::integral_constant<int, 1>{});
                 else if (n > 0) chunk1(c8, std::integral_constant<int, 8>{});
                 else {
                     // chunk skipped (deg <= c8): its edges enter as positive (zero) sign fields
@@ -512,8 +516,9 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
             const int r0 = (int)(ri & 0xFFFFu);
             const int deg = (int)((ri >> 16) & 0xFFu);
-            // whole 8-edge chunks: padding slots add into the dummy word.  (Pass 1's 6- and
-            // 7-edge chunk shapes here measured 2.5% slower on wman than the plain chunks.)
+            // whole 8-edge chunks, padding slots adding into the lane's dummy word (exact 6- and
+            // 7-edge chunks measured 2.5% slower on wman (CW 16) and 4% slower on 5G BG2 (CW 8));
+            // CW 4 (5G BG1, degrees 3..19, a third of the slots would be padding): exact chunks
             auto chunk2 = [&](const int c8, auto ne) __attribute__((always_inline)) {
                 constexpr int NE = decltype(ne)::value;
                 const uint32_t R0 = perm_word(gi, c8 / 4);
@@ -533,7 +538,14 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
 #pragma unroll
             for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
                 const int n = deg - c8;
-                if (n > 0) chunk2(c8, N8{});
+                if (CW > 4 || n >= 8) { if (n > 0) chunk2(c8, N8{}); }
+                else if (n == 7) chunk2(c8, std::integral_constant<int, 7>{});
+                else if (n == 6) chunk2(c8, std::integral_constant<int, 6>{});
+                else if (n == 5) chunk2(c8, std::integral_constant<int, 5>{});
+                else if (n == 4) chunk2(c8, std::integral_constant<int, 4>{});
+                else if (n == 3) chunk2(c8, std::integral_constant<int, 3>{});
+                else if (n == 2) chunk2(c8, std::integral_constant<int, 2>{});
+                else if (n == 1) chunk2(c8, std::integral_constant<int, 1>{});
             }
         }
         if (bcopy) BETA[((t + 1) & 1) * a.N + tid] = bload;
@@ -549,7 +561,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         uint32_t any_hd = 0, any_pos = 0, nbits = 0;
         const float qmf = (float)qmax;
         const int sb = -(int)F5_SBIAS;
-        if (tid < CW) W[total + tid] = F5_DUMMY_W;    // pass-2 adds of padding edges
+        if (tid < F5_NDUMMY) W[total + tid] = F5_DUMMY_W;    // pass-2 adds of padding edges
         if constexpr (!OUT) {
             // counters only.  A wave owns the contiguous 64-entry chunks [c_beg, c_end); with
             // SLOTS | z a chunk lies in one proto column, so beta is wave-uniform.  Only the
@@ -817,7 +829,7 @@ __global__ void k_f5_gad(const int32_t* __restrict__ row_ptr, const int32_t* __r
         uint32_t word = 0;
         for (int j = 0; j < 2; ++j) {
             const int k = 2 * p + j;
-            uint32_t byte = (uint32_t)(total + cw) * 4u;              // dummy word of this cw
+            uint32_t byte = (uint32_t)(total + lane) * 4u;            // dummy word of this lane
             if (k < deg && k < maxdeg) {
                 int hs = hl + pe_shift[r0 + k];
                 hs = (hs >= z) ? hs - z : hs;
@@ -849,14 +861,14 @@ constexpr Shape5 kShapes5[] = {
     {64, 2, 32, true, false},    // z=1 dense rows (BCH)
     {4, 3, 12, true, false},     // 5G BG2-like at two workgroups per CU (z=64: 16 slots, 4 codewords)
     {8, 2, 24, true, false},     // 802.11n-like at three workgroups per CU
-    {4, 4, 20, true, true},      // 5G BG1-like (n = 2304 variables, deg 3-19, z = 72), one WG per CU
+    {4, 4, 20, true, false},     // 5G BG1-like (n = 2304 variables, deg 3-19, z = 72), one WG per CU
     // measured and dropped: {8, 2, 16} at 8 waves/SIMD (64 VGPRs) ran 28.3 ms vs 21.3 ms for
     // {16, 3, 16} on wman -- twice the per-workgroup fixed cost per codeword
 };
 
 size_t f5_lds(int nv, int cw, int T, int N) {
     (void)T;
-    return ((((size_t)nv * cw + cw) * 4 + (size_t)nv * cw * 4 + (size_t)2 * N * 4 + 15) & ~(size_t)15) + 8 * 8;
+    return ((((size_t)nv * cw + F5_NDUMMY) * 4 + (size_t)nv * cw * 4 + (size_t)2 * N * 4 + 15) & ~(size_t)15) + 8 * 8;
 }
 
 struct Plan5 {
@@ -882,7 +894,7 @@ Plan5 plan5(const DevGraph& g, int T) {
         if (g.N > 64 * nw) continue;                                    // beta slice copy
         const size_t lds = f5_lds(g.n_vars, sh.cw, T, g.N);
         if (lds > F5_LDS_MAX) continue;
-        if ((size_t)g.n_vars * sh.cw * 4 + sh.cw * 4 >= 65536) continue;    // 16-bit addresses
+        if (((size_t)g.n_vars * sh.cw + F5_NDUMMY) * 4 > 65536) continue;    // 16-bit addresses
         // resident workgroups per CU: LDS and the shape's VGPR budget (f5_wpe waves per SIMD;
         // a workgroup puts ceil(nw/4) waves on its busiest SIMD and the next workgroup starts
         // on the same SIMD: measured, a 14-wave group at 7 waves/SIMD runs alone).  VALU issue
