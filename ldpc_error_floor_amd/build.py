@@ -26,7 +26,16 @@ ARCH = os.environ.get("LDPC_OFFLOAD_ARCH", "gfx950")
 HIP_SOURCES = ["ldpc_capi.hip", "ldpc_flood.hip", "ldpc_fused.hip", "ldpc_fused3.hip",
                "ldpc_fused4.hip", "ldpc_fused5.hip", "ldpc_channel.hip",
                "ldpc_collect.hip"]
-HEADERS = ["ldpc_internal.h", "ldpc_fused.h"]
+HEADERS = ["ldpc_internal.h", "ldpc_fused.h", "ldpc_fused5_kernel.h", "ldpc_awgn.h"]
+# ldpc_fused5_shape.hip is compiled once per kShapes5 entry (-DF5_SHAPE=i), in parallel
+F5_SHAPE_SRC = "ldpc_fused5_shape.hip"
+
+
+def _f5_shape_count():
+    import re
+    src = open(os.path.join(CSRC, "ldpc_fused5_kernel.h")).read()
+    body = src.split("constexpr Shape5 kShapes5[] = {", 1)[1].split("\n};", 1)[0]
+    return len(re.findall(r"^\s*\{", body, re.M))
 LIB = os.path.join(PKG, "libldpc_nms.so")
 EXT = os.path.join(PKG, "_ldpc_nms" + sysconfig.get_config_var("EXT_SUFFIX"))
 
@@ -57,14 +66,20 @@ def build(force=False, jobs=4, verbose=False):
     hipcc = _hipcc()
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "ldpc_nms.h")]
     flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-             "-I" + INCLUDE, "-I" + CSRC, "-Wall", "-Wno-unused-result"]
+             "-I" + INCLUDE, "-I" + CSRC, "-Wall", "-Wno-unused-result",
+             # the fused kernels' per-group loops must unroll completely (register-resident
+             # per-group state); the default pragma threshold gives up on the wide shapes
+             "-mllvm", "-pragma-unroll-threshold=500000"]
     objs, jobs_list = [], []
-    for src in HIP_SOURCES:
+    units = [(src, src.replace(".hip", ".o"), []) for src in HIP_SOURCES]
+    units += [(F5_SHAPE_SRC, f"ldpc_fused5_s{i}.o", [f"-DF5_SHAPE={i}"])
+              for i in range(_f5_shape_count())]
+    for src, obj, defs in units:
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD, src.replace(".hip", ".o"))
+        o = os.path.join(BUILD, obj)
         objs.append(o)
         if force or _newer(o, [s] + hdrs):
-            jobs_list.append([hipcc] + flags + ["-c", s, "-o", o])
+            jobs_list.append([hipcc] + flags + defs + ["-c", s, "-o", o])
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         for r in ex.map(_run, jobs_list):
             if verbose and r.stderr:
@@ -85,7 +100,7 @@ def build(force=False, jobs=4, verbose=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("--jobs", type=int, default=4)
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
     a = ap.parse_args()
     lib, ext = build(force=a.force, jobs=a.jobs, verbose=True)
     print(lib)

@@ -276,6 +276,7 @@ int ldpc_graph_create(const int32_t* proto, int32_t M, int32_t N, int32_t z, int
     d.pe_shift = p; p += g->E;
     d.col_ptr = p; p += N + 1;
     d.col_pe = p;
+    d.h_row_ptr = g->row_ptr.data();
     *out = g;
     return LDPC_OK;
 }

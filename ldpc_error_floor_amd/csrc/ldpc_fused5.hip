@@ -1,761 +1,17 @@
-// ldpc_fused5.hip — fused QMS decoder, v5: byte-packed check state, 2-op message decode.
-//
-// Same semantics and work mapping as v3 (ldpc_fused3.hip: one workgroup owns CW codewords for
-// all T iterations, lane = slot*CW + cw, a wave's slots take consecutive checks of one proto
-// row, per-edge LDS addresses precomputed and packed 2x16 bit).  What changes is how a check's
-// compressed min-sum state is held and decoded, which sets the VALU count per edge:
-//
-//  * P   — one VGPR holding the check's four possible output messages as signed bytes
-//          [+mA, -mA, +mB, -mB] (mA: min over all edges, mB: second minimum, both already
-//          weighted and quantized, in grid units);
-//  * SEL — one selector byte per edge, four edges per VGPR: byte = 2*is_argmin + negative,
-//          the index of the edge's message inside P.  v_perm_b32(P, P, SEL[w]) yields four
-//          edges' messages, and pass 1 subtracts a message straight from its byte with an
-//          SDWA sign-extended source: a quarter op per edge to decode (v3: 5 ops).
-//  * pass 1 folds V->C magnitudes with one v_min + one v_med3 per edge (running first/second
-//    minimum of key = |v2c| << 8 | edge code), and the V->C signs with one v_alignbit per
-//    edge, which appends the top byte of v2c (8 copies of its sign) to a SEL-shaped word;
-//    the quantizer clamp moves after the minimum (clamp is monotonic);
-//  * W[v][cw] = Tv (bits 31..16, signed) | hd (bit 15) | S + 2^14 (bits 14..0): pass 1 reads Tv
-//    with an SDWA sign-extended word select, pass 2 adds the message without a shift;
-//  * an edge slot past a check's degree points at a per-codeword dummy word whose Tv is
-//    +16383: its |v2c| never wins a minimum, its sign is positive, its hd bit is 0, and pass 2
-//    adds into it harmlessly (the VN phase resets it), so partial chunks need no masks.
-//
-// Per-edge weights (sharing types with one weight per edge) keep raw minima in P (16 bit
-// each) and quantize per edge at decode; this path is correct but not tuned.
+// ldpc_fused5.hip — fused QMS decoder v5: per-decode tables, shape planning and dispatch.
+// The kernel is in ldpc_fused5_kernel.h; each shape is compiled in its own translation unit
+// (ldpc_fused5_shape.hip, -DF5_SHAPE=<index>) so the shapes build in parallel.
 #include <algorithm>
 #include <climits>
-#include <type_traits>
-#include <vector>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
-#include "ldpc_awgn.h"
-#include "ldpc_fused.h"
+#include "ldpc_fused5_kernel.h"
 
 namespace ldpc {
 
-namespace {
-
-constexpr int F5_BIG_U = 1023;               // "no other edge": value 10000 (Main_Functions.py:248)
-constexpr size_t F5_LDS_MAX = 160 * 1024;
-constexpr uint32_t F5_SBIAS = 16384;         // S field bias (bits 14..0)
-// padding edges read this word: Tv = 96 gives a V->C value in [65, 127] for any message
-// (|m| <= 31), positive, never below qmax and inside the 8-bit range pass 1 works in
-constexpr uint32_t F5_DUMMY_W = (96u << 16) | F5_SBIAS;
-// one dummy word per lane (after W): padding slots of different lanes never add into the same
-// LDS word, so their pass-2 atomics do not serialise
-constexpr int F5_NDUMMY = 64;
-constexpr float F5_MAGIC = 12582912.0f;                 // 1.5 * 2^23
-constexpr int F5_MAGIC_BITS = 0x4B400000;              // bit pattern of F5_MAGIC
-constexpr int F5_APP0 = F5_MAGIC_BITS + (int)F5_SBIAS;  // APP == 0 in the VN's biased domain
-// (Tv + F5_APP0) * 2^16 + F5_WBIAS == (Tv << 16) | F5_SBIAS  (mod 2^32)
-constexpr uint32_t F5_WBIAS = F5_SBIAS - (uint32_t)F5_APP0 * 65536u;
-// APP path magic: 1.5 * 2^23 + 2^22 - S bias, same binade, so Q(y) + APP bits land at
-// F5_APPH + APP with F5_APPH = 0x4B800000: APP >= 0 exactly when bit 23 is set (an OR over
-// entries then answers "any hard decision 1")
-constexpr float F5_MAGIC_A = 16760832.0f;
-constexpr int F5_APPH = 0x4B800000;
-static_assert(12582912 + 4194304 - (int)F5_SBIAS == 16760832, "APP magic");
-
-struct F5Args {
-    const float* llr;
-    const float* beta;
-    float* app_out;
-    uint64_t* hd_out;
-    int64_t* counters;
-    uint8_t* flags;
-    const int32_t* row_ptr;
-    const int32_t* pe_col;
-    const int32_t* pe_shift;
-    int64_t B;
-    int ntiles, T, target_bits, clip_u, qmax;
-    float inv, step;
-    int n_vars, N, E, z;
-    int hstep, ngroups, nent;
-    int nfull, cpw;    // VN: full 64-entry chunks, chunks per wave
-    int Mp;            // proto rows
-    const float* betas;        // [T][N] beta / step (setup kernel)
-    const uint16_t* qtab;      // [T][qslice] weight tables (setup kernel), LUT builds only
-    int qslice;                // halfwords per iteration: [alpha | alpha_ucn][Mp][qmax+2], even
-    int qucn;                  // halfword offset of the alpha_ucn table inside a slice
-    const uint32_t* gad;       // [ngroups][NPK][64] packed edge byte addresses (k_f5_gad)
-    const uint4* grow;         // [ngroups] {r0 | deg << 16 | row << 24, lane-valid mask lo, hi, 0}
-    unsigned long long* stamps;   // diagnostic (LDPC_DIAG_STAMPS): [block][8] s_memtime marks
-    int gen;                   // 1: LLRs from the in-kernel AWGN channel (awgn), llr unused
-    AwgnParams awgn;
-    uint32_t zmagic;
-    int ablate;        // diagnostic only (LDPC_DIAG_ABLATE): 1 skip CN pass 1, 2 skip pass 2, 4 skip VN
-};
-
-__device__ __forceinline__ int q_units5(float x, float inv, int qmax) {
-    return (int)__builtin_amdgcn_fmed3f(rintf(x * inv), -(float)qmax, (float)qmax);
-}
-// Q(x) in grid units when x is already scaled by the (power-of-two) inverse step
-__device__ __forceinline__ int q_scaled5(float xs, float qm) {
-    return (int)__builtin_amdgcn_fmed3f(rintf(xs), -qm, qm);
-}
-// quantized C->V magnitude: Q(relu(|o| * w)), |o| in grid units (>= F5_BIG_U: the 10000 rule)
-__device__ __forceinline__ int q_mag5(int m, float w, float step, float inv, int qmax) {
-    const float mv = (m >= F5_BIG_U) ? 10000.0f : (float)m * step;
-    float x = mv * w;                          // fl32(|o| * w)
-    x = (x > 0.f) ? x : 0.f;                   // x * [x > 0]
-    return q_units5(x, inv, qmax);
-}
-
-// 16-bit VOP2 forms: full issue rate on gfx950 where the 32-bit min / max / shift-left and
-// every SDWA / VOP3 form take twice the cycles (tools/valu_table.hip); the high half of the
-// result is zeroed.
-__device__ __forceinline__ uint32_t max_i16(uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_max_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ uint32_t min_u16(uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-// LDS word at a byte address (the decoder's dynamic LDS starts at 0: k_fused5 checks)
-typedef __attribute__((address_space(3))) uint32_t LdsU32;
-// the low / high 16-bit byte address of a packed pair
-__device__ __forceinline__ uint32_t lo16(uint32_t x) {
-    uint32_t r;
-    asm("v_and_b32 %0, 0xffff, %1" : "=v"(r) : "v"(x));
-    return r;
-}
-__device__ __forceinline__ uint32_t hi16(uint32_t x) {
-    uint32_t r;
-    asm("v_lshrrev_b32 %0, 16, %1" : "=v"(r) : "v"(x));
-    return r;
-}
-// (Tv - m) * 256 sign-extended: Tv = signed high half of the W word, m = signed byte POS of r.
-// Exact while |Tv - m| <= 127 (Tv is kept within +-2 qmax, |m| <= qmax <= 31).
-template <int POS>
-__device__ __forceinline__ uint32_t sub_d256(uint32_t w, uint32_t r) {
-    uint32_t d;
-    if constexpr (POS == 0)
-        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_0"
-            : "=v"(d) : "v"(w), "v"(r));
-    else if constexpr (POS == 1)
-        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_1"
-            : "=v"(d) : "v"(w), "v"(r));
-    else if constexpr (POS == 2)
-        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_2"
-            : "=v"(d) : "v"(w), "v"(r));
-    else
-        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_3"
-            : "=v"(d) : "v"(w), "v"(r));
-    return d;
-}
-
-// min(max(a, lo), hi) on the low 16 bits, bounds uniform (SGPR)
-__device__ __forceinline__ uint32_t clamp_i16(uint32_t a, uint32_t lo, uint32_t hi) {
-    uint32_t r;
-    asm("v_max_i16 %0, %1, %2" : "=v"(r) : "s"(lo), "v"(a));
-    asm("v_min_i16 %0, %1, %2" : "=v"(r) : "s"(hi), "v"(r));
-    return r;
-}
-__device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t r;
-    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-
-// ---- SEL layout: edge k -> byte of word k/4, counted from the last inserted edge ------------
-// A selector byte is 2*is_argmin + negative: the index of the edge's message inside P, so
-// v_perm_b32(P, P, SEL[w]) yields the messages of four edges at once.
-template <int MAXDEG>
-struct Sel {
-    static constexpr int NSEL = (MAXDEG + 3) / 4;
-    static constexpr int nins(int w) { return (MAXDEG - 4 * w) < 4 ? (MAXDEG - 4 * w) : 4; }
-    static constexpr int pos(int k) { return nins(k / 4) - 1 - (k % 4); }
-    static constexpr uint32_t code(int k) { return ((uint32_t)(k / 4) << 5) | (uint32_t)(8 * pos(k) + 1); }
-    static constexpr uint32_t bmask(int w) {
-        uint32_t m = 0;
-        for (int i = 0; i < nins(w); ++i) m |= 1u << (8 * i);
-        return m;
-    }
-    // number of edges of word w inside chunk [c8, c8+8)
-    static constexpr int in_chunk(int w, int c8) {
-        int n = 0;
-        for (int k = c8; k < c8 + 8 && k < MAXDEG; ++k) n += (k / 4 == w);
-        return n;
-    }
-};
-
-// diagnostic phase marks: wave 0 lane 0 of each workgroup records s_memrealtime (100 MHz)
-#define F5_STAMP(i)                                                                         \
-    do {                                                                                    \
-        if (a.stamps && tid == 0) a.stamps[(size_t)blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
-
-// occupancy target (waves per SIMD) of a shape: the VGPR budget that lets the planned number of
-// workgroups share a CU (plan5 assumes the same figure)
-constexpr int f5_wpe(int cw, int maxg, int maxdeg) {
-    return (cw == 16 && maxdeg == 16) ? 6 : (cw == 4 && maxg == 4) ? 4 : (cw == 4) ? 7
-         : (cw == 8 && maxg == 2) ? 6 : 1;
-}
-constexpr int f5_logcw(int cw) { return cw == 64 ? 6 : cw == 32 ? 5 : cw == 16 ? 4 : cw == 8 ? 3 : 2; }
-
-template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW, bool OUT, bool LUT>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(f5_wpe(CW, MAXG, MAXDEG))))
-k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ alpha_ucn) {
-    using SL = Sel<MAXDEG>;
-    constexpr int NSEL = SL::NSEL;
-    constexpr int SLOTS = 64 / CW;
-    constexpr int LOGCW = f5_logcw(CW);
-    constexpr int NPK = (MAXDEG + 1) / 2;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int nv = a.n_vars;
-    const int total = nv * CW;
-    uint32_t* W = reinterpret_cast<uint32_t*>(smem);                              // [nv*CW + CW]
-    float* CH = reinterpret_cast<float*>(smem + ((size_t)total + F5_NDUMMY) * 4); // [nv*CW]
-    float* BETA = CH + total;                     // [2][N]: beta_t / step in slot t & 1
-    unsigned long long* RED = reinterpret_cast<unsigned long long*>(
-        smem + ((((size_t)total + F5_NDUMMY) * 4 + (size_t)total * 4 + (size_t)2 * a.N * 4 + 15) & ~(size_t)15));
-    uint16_t* QT = reinterpret_cast<uint16_t*>(RED + 8);                          // [2][qslice]
-
-    if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();   // edge addresses are LDS-absolute
-    const int tid = threadIdx.x;
-    const int NT = blockDim.x;
-    const int NWV = NT >> 6;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int cw = lane & (CW - 1);
-    const int64_t b0 = (int64_t)blockIdx.x * CW;
-    const int64_t nvalid = (b0 + CW <= a.B) ? CW : (a.B - b0);
-    const unsigned long long cwmask = (CW == 64) ? ~0ull : ((1ull << CW) - 1);
-    const unsigned long long valid_cw = (nvalid >= 64) ? ~0ull : ((1ull << nvalid) - 1);
-    const int qmax = a.qmax;
-    const float inv = a.inv, step = a.step;
-    const int z = a.z;
-
-    F5_STAMP(0);
-    // ---- prologue: coalesced LLR block -> padded scratch -> CH[v][cw]; beta; W = Tv_0 | hd ----
-    {
-        float* scr = reinterpret_cast<float*>(W);            // [CW][nv+1]
-        const int rl = nv + 1;
-        if (a.gen) {
-            // in-kernel channel: the same generator as ldpc_channel_awgn (ldpc_awgn.h)
-            const int npairs = (nv + 1) >> 1;
-            for (int i = tid; i < CW * npairs; i += NT) {
-                const int r = i / npairs, pr = i - r * npairs;
-                float l[2] = {0.f, 0.f};
-                if (r < nvalid) awgn_pair(a.awgn, b0 + r, pr, l);
-                scr[r * rl + 2 * pr] = l[0];
-                if (2 * pr + 1 < nv) scr[r * rl + 2 * pr + 1] = l[1];
-            }
-        } else
-        for (int v0 = 0; v0 < nv; v0 += NT) {
-            const int v = v0 + tid;
-            float x[CW];
-#pragma unroll
-            for (int r = 0; r < CW; ++r)
-                x[r] = (v < nv && r < nvalid) ? a.llr[(b0 + r) * nv + v] : 0.f;
-#pragma unroll
-            for (int r = 0; r < CW; ++r)
-                if (v < nv) scr[r * rl + v] = x[r];
-        }
-        // beta / step and the weight table come precomputed (k_f5_tables): plain copies
-        // beta_0 and beta_1; slice t+1 (t >= 1) is copied during iteration t's check phase
-        for (int f = tid; f < min(a.T, 2) * a.N; f += NT) BETA[f] = a.betas[f];
-        if (tid < 8) RED[tid] = (tid == 1) ? ~0ull : 0ull;
-        if constexpr (LUT) {       // iteration 0's slice; slice t+1 is copied during VN t
-            const int nw32 = a.qslice >> 1;
-            for (int f = tid; f < nw32; f += NT)
-                reinterpret_cast<uint32_t*>(QT)[f] = reinterpret_cast<const uint32_t*>(a.qtab)[f];
-        }
-        __syncthreads();
-        for (int e = tid; e < total; e += NT) CH[e] = scr[(e & (CW - 1)) * rl + (e >> LOGCW)];
-        __syncthreads();
-        for (int e = tid; e < total; e += NT) {
-            const uint32_t v = (uint32_t)e >> LOGCW;
-            const int t0 = q_scaled5(CH[e] * BETA[__umulhi(v, a.zmagic)], (float)qmax);  // lw_0
-            W[e] = ((uint32_t)t0 << 16) | ((uint32_t)(t0 >= 0) << 15) | F5_SBIAS;     // hd_{-1}
-        }
-        if (tid < F5_NDUMMY) W[total + tid] = F5_DUMMY_W;
-    }
-
-    F5_STAMP(1);
-    // ---- per-group edge addresses (bytes, 16-bit packed), row info, lane validity ----------
-    // (built once per decode by k_f5_gad; one coalesced load per packed word)
-    uint32_t gad[MAXG][NPK];
-    uint32_t grow[MAXG];
-    bool gval[MAXG];
-#pragma unroll
-    for (int gi = 0; gi < MAXG; ++gi) {
-        grow[gi] = 0;
-        gval[gi] = false;
-#pragma unroll
-        for (int p = 0; p < NPK; ++p) gad[gi][p] = 0;
-        const int grp = wave + gi * NWV;
-        if (grp < a.ngroups) {
-            const uint32_t* gt = a.gad + (size_t)grp * NPK * 64 + lane;
-#pragma unroll
-            for (int p = 0; p < NPK; ++p) gad[gi][p] = gt[p * 64];
-            const uint4 r = a.grow[grp];
-            grow[gi] = r.x;
-            gval[gi] = (((lane < 32) ? r.y : r.z) >> (lane & 31)) & 1u;
-        }
-    }
-    __syncthreads();
-
-    F5_STAMP(2);
-    // check state: P (messages / raw minima), SEL (per-edge fields), ucn (syndrome, PEW only)
-    uint32_t P[MAXG], SEL[MAXG][NSEL];
-    int UC[MAXG];
-#pragma unroll
-    for (int gi = 0; gi < MAXG; ++gi) {
-        P[gi] = 0;
-        UC[gi] = 0;
-#pragma unroll
-        for (int w = 0; w < NSEL; ++w) SEL[gi][w] = 0;
-    }
-
-    // C->V message of edge k, given R = v_perm(P, P, SEL[k/4]) (the word's four messages)
-    auto msg = [&](const int gi, const int k, const uint32_t R, const float* wt, const float* wtu,
-                   const int r0) __attribute__((always_inline)) -> int {
-        if constexpr (!PEW) {
-            return (int)(signed char)(R >> (8 * SL::pos(k)));
-        } else {
-            const int m = (int)((R >> (8 * SL::pos(k))) & 0xFFu);        // 255: no other edge
-            const float w = (UCN && UC[gi]) ? wtu[r0 + k] : wt[r0 + k];
-            const int mq = q_mag5(m == 255 ? F5_BIG_U : m, w, step, inv, qmax);
-            return ((SEL[gi][k / 4] >> (8 * SL::pos(k))) & 1u) ? -mq : mq;
-        }
-    };
-    auto perm_word = [&](const int gi, const int w) __attribute__((always_inline)) -> uint32_t {
-        return (w < NSEL) ? __builtin_amdgcn_perm(P[gi], P[gi], SEL[gi][w < NSEL ? w : 0]) : 0u;
-    };
-
-    for (int t = 0; t < a.T; ++t) {
-        if (t < 22) F5_STAMP(8 + t);
-        if (tid == 0 && t > 0) {        // fold iteration t-1's frame flags (its VN phase is done)
-            RED[1] &= RED[0];
-            RED[0] = 0;
-        }
-        const float* at = alpha + (size_t)t * a.E;
-        const float* au = UCN ? alpha_ucn + (size_t)t * a.E : nullptr;
-        // the next iteration's weight-table slice, loaded now, stored to LDS in the VN phase
-        // (double buffer: slice t+1 goes where slice t-1 was, which pass 1 of t no longer reads)
-        uint32_t qnext = 0;
-        if constexpr (LUT) {
-            if (t + 1 < a.T && tid < (a.qslice >> 1))
-                qnext = reinterpret_cast<const uint32_t*>(a.qtab + (size_t)(t + 1) * a.qslice)[tid];
-        }
-        // beta_{t+1} for this iteration's VN phase, stored to LDS before the pass-2 barrier
-        // (its slot last held beta_{t-1}, read by the VN phase of iteration t-2)
-        const bool bcopy = t >= 1 && t + 1 < a.T && tid < a.N;
-        float bload = 0.f;
-        if (bcopy) bload = a.betas[(size_t)(t + 1) * a.N + tid];
-        const float* atp = alpha + (size_t)(t > 0 ? t - 1 : 0) * a.E;
-        const float* aup = UCN ? alpha_ucn + (size_t)(t > 0 ? t - 1 : 0) * a.E : nullptr;
-        // ======== check nodes: pass 1 (read Tv, fold minima and signs) + new state ==========
-#pragma unroll
-        for (int gi = 0; gi < MAXG; ++gi) {
-            const int grp = wave + gi * NWV;
-            if (grp >= a.ngroups) break;
-            if (a.ablate & 1) continue;
-            const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
-            const int r0 = (int)(ri & 0xFFFFu);
-            const int deg = (int)((ri >> 16) & 0xFFu);
-            uint32_t c1 = 0xFFFFFFFFu, c2 = 0xFFFFFFFFu;
-            uint32_t NG[NSEL];
-#pragma unroll
-            for (int w = 0; w < NSEL; ++w) NG[w] = 0;
-            uint32_t syn = 0;     // UCN: XOR of the edges' W words (bit 15: previous hard decisions)
-            // this row's weights as scalar loads issued ahead of the chunks (a per-lane choice
-            // between two global addresses would be a vector load waited on in the state update)
-            float wa = 0.f, wu = 0.f;
-            if constexpr (!PEW && !LUT) {
-                wa = at[r0];
-                if constexpr (UCN) wu = au[r0];
-            }
-            // one chunk of up to 8 edges, straight-line.  NE = edges present (compile time):
-            // 6 and 7 cover rows ending inside the chunk; other short chunks run as 8 and their
-            // padding slots (k >= deg) read the dummy word (|v2c| never below qmax, positive
-            // sign).  Skipping slots behind scalar branches was measured slower: the branches
-            // split the chunk's schedule.
-            auto chunk1 = [&](const int c8, auto ne) __attribute__((always_inline)) {
-                constexpr int NE = decltype(ne)::value;
-                uint32_t wv[8];
-#pragma unroll
-                for (int j = 0; j < NE; ++j) {
-                    const int k = c8 + j;
-                    if (k < MAXDEG) {
-                        const uint32_t pk = gad[gi][k >> 1];
-                        const uint32_t addr = (k & 1) ? hi16(pk) : lo16(pk);
-                        wv[j] = *reinterpret_cast<const LdsU32*>(addr);
-                    }
-                }
-                const uint32_t R0 = perm_word(gi, c8 / 4);
-                const uint32_t R1 = (NE > 4) ? perm_word(gi, c8 / 4 + 1) : 0u;
-                // V->C before Q, times 256: d256 = (Tv - m) << 8, sign-extended.  All of them
-                // first: an SDWA result with a sub-dword dst_sel read by the very next
-                // instruction costs a wait state.
-                uint32_t dd[8];
-#pragma unroll
-                for (int j = 0; j < NE; ++j) {
-                    const int k = c8 + j;
-                    if (k < MAXDEG) {
-                        if constexpr (PEW) {
-                            const int cold = msg(gi, k, j < 4 ? R0 : R1, atp, aup, r0);
-                            dd[j] = sub_d256<0>(wv[j], (uint32_t)cold);
-                        } else {
-                            const uint32_t R = j < 4 ? R0 : R1;
-                            switch (SL::pos(k)) {
-                                case 0: dd[j] = sub_d256<0>(wv[j], R); break;
-                                case 1: dd[j] = sub_d256<1>(wv[j], R); break;
-                                case 2: dd[j] = sub_d256<2>(wv[j], R); break;
-                                default: dd[j] = sub_d256<3>(wv[j], R); break;
-                            }
-                        }
-                        if (UCN) syn ^= wv[j];
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < NE; ++j) {
-                    const int k = c8 + j;
-                    if (k < MAXDEG) {
-                        const uint32_t d256 = dd[j];
-                        // key = |d| << 8 | code, all in the low 16 bits
-                        const uint32_t key = max_i16(d256, 0u - d256) | SL::code(k);
-                        // append the byte of sign copies of d to the edge's selector word
-                        NG[k / 4] = __builtin_amdgcn_alignbit(NG[k / 4], d256, 24);
-                        const uint32_t o1 = c1;
-                        c1 = min_u16(o1, key);
-                        c2 = med3u(o1, c2, key);
-                    }
-                }
-                // absent slots of the chunk enter as positive (zero) sign bytes
-#pragma unroll
-                for (int w = 0; w < NSEL; ++w) {
-                    int n = 0;
-#pragma unroll
-                    for (int j = NE; j < 8; ++j) n += (c8 + j < MAXDEG && (c8 + j) / 4 == w);
-                    if (n > 0) NG[w] = (n >= 4) ? 0u : (NG[w] << (8 * n));
-                }
-            };
-#pragma unroll
-            for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
-                const int n = deg - c8;
-                // a row ending inside the chunk runs the shape with exactly its edges (shapes
-                // below 6 only where a shape's rows are that short: 5G-like graphs)
-                if (n >= 8) chunk1(c8, std::integral_constant<int, 8>{});
-                else if (n == 7) chunk1(c8, std::integral_constant<int, 7>{});
-                else if (n == 6) chunk1(c8, std::integral_constant<int, 6>{});
-                else if (CW <= 8 && n == 5) chunk1(c8, std::integral_constant<int, 5>{});
-                else if (CW <= 8 && n == 4) chunk1(c8, std::integral_constant<int, 4>{});
-                else if (CW <= 8 && n == 3) chunk1(c8, std::integral_constant<int, 3>{});
-                else if (CW <= 8 && n == 2) chunk1(c8, std::integral_constant<int, 2>{});
-                else if (CW <= 8 && n == 1) chunk1(c8, std::integral_constant<int, 1>{});
-                else if (n > 0) chunk1(c8, std::integral_constant<int, 8>{});
-                else {
-                    // chunk skipped (deg <= c8): its edges enter as positive (zero) sign fields
-#pragma unroll
-                    for (int w = 0; w < NSEL; ++w) {
-                        const int nn = SL::in_chunk(w, c8);
-                        if (nn > 0) NG[w] = (nn >= 4) ? 0u : (NG[w] << (8 * nn));
-                    }
-                }
-            }
-            // ---- new state: quantized minima, selector bytes, argmin bit ----
-            uint32_t nbit = 0;
-#pragma unroll
-            for (int w = 0; w < NSEL; ++w) {
-                NG[w] &= SL::bmask(w);                 // bit 0 of each byte: V->C sign negative
-                nbit += __popc(NG[w]);
-            }
-            // message sign = V->C sign XOR (count of positives odd): applied to P as a byte
-            // swap inside each half; for PEW (P holds magnitudes) to the selector bytes
-            if constexpr (UCN) syn = (syn >> 15) & 1u;
-            const bool podd = ((uint32_t)deg + nbit) & 1u;
-            const uint32_t code = c1 & 255u;
-            const uint32_t onebit = 1u << (code & 31u);
-            const uint32_t wsel = code >> 5;
-            const uint32_t pm = (PEW && podd) ? 0xFFFFFFFFu : 0u;
-#pragma unroll
-            for (int w = 0; w < NSEL; ++w)
-                SEL[gi][w] = (NG[w] ^ (pm & SL::bmask(w))) | ((wsel == (uint32_t)w) ? onebit : 0u);
-            const int m1 = min((int)(c1 >> 8), qmax);
-            if constexpr (PEW) {
-                const uint32_t m2 = (deg < 2) ? 255u : (uint32_t)min((int)(c2 >> 8), qmax);
-                UC[gi] = (int)syn;
-                P[gi] = gval[gi] ? ((uint32_t)m1 * 0x0101u | (m2 * 0x0101u) << 16) : 0u;
-            } else {
-                uint32_t p;
-                if constexpr (LUT) {
-                    // [+m, -m] byte pairs of Q(relu(m*w)) for this iteration and proto row
-                    const int ib = (deg < 2) ? qmax + 1 : min((int)(c2 >> 8), qmax);
-                    const int row = (int)((ri >> 24) & 0xFFu);
-                    const uint16_t* qt = QT + (t & 1) * a.qslice + ((UCN && syn) ? a.qucn : 0) +
-                                         row * (qmax + 2);
-                    p = (uint32_t)qt[m1] | ((uint32_t)qt[ib] << 16);
-                } else {
-                    const int m2 = (deg < 2) ? F5_BIG_U : min((int)(c2 >> 8), qmax);
-                    const float w = (UCN && syn) ? wu : wa;
-                    const int mA = q_mag5(m1, w, step, inv, qmax);
-                    const int mB = q_mag5(m2, w, step, inv, qmax);
-                    const uint32_t pa = ((uint32_t)mA & 0xFFu) | (((uint32_t)(-mA) & 0xFFu) << 8);
-                    const uint32_t pb = ((uint32_t)mB & 0xFFu) | (((uint32_t)(-mB) & 0xFFu) << 8);
-                    p = pa | (pb << 16);
-                }
-                p = __builtin_amdgcn_perm(p, p, podd ? 0x02030001u : 0x03020100u);
-                P[gi] = gval[gi] ? p : 0u;    // duplicate stand-in check: no messages
-            }
-        }
-        if (t == 0) F5_STAMP(5);
-        // ======== check nodes: pass 2 (scatter C->V into S) =================================
-#pragma unroll
-        for (int gi = 0; gi < MAXG; ++gi) {
-            const int grp = wave + gi * NWV;
-            if (grp >= a.ngroups) break;
-            if (a.ablate & 2) continue;
-            const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
-            const int r0 = (int)(ri & 0xFFFFu);
-            const int deg = (int)((ri >> 16) & 0xFFu);
-            // whole 8-edge chunks, padding slots adding into the lane's dummy word (exact 6- and
-            // 7-edge chunks measured 2.5% slower on wman (CW 16) and 4% slower on 5G BG2 (CW 8));
-            // CW 4 (5G BG1, degrees 3..19, a third of the slots would be padding): exact chunks
-            auto chunk2 = [&](const int c8, auto ne) __attribute__((always_inline)) {
-                constexpr int NE = decltype(ne)::value;
-                const uint32_t R0 = perm_word(gi, c8 / 4);
-                const uint32_t R1 = (NE > 4) ? perm_word(gi, c8 / 4 + 1) : 0u;
-#pragma unroll
-                for (int j = 0; j < NE; ++j) {
-                    const int k = c8 + j;
-                    if (k < MAXDEG) {
-                        const uint32_t pk = gad[gi][k >> 1];
-                        const uint32_t addr = (k & 1) ? hi16(pk) : lo16(pk);
-                        const int c = msg(gi, k, j < 4 ? R0 : R1, at, au, r0);
-                        __atomic_fetch_add(reinterpret_cast<LdsU32*>(addr), (uint32_t)c, __ATOMIC_RELAXED);
-                    }
-                }
-            };
-            using N8 = std::integral_constant<int, 8>;
-#pragma unroll
-            for (int c8 = 0; c8 < MAXDEG; c8 += 8) {
-                const int n = deg - c8;
-                if (CW > 4 || n >= 8) { if (n > 0) chunk2(c8, N8{}); }
-                else if (n == 7) chunk2(c8, std::integral_constant<int, 7>{});
-                else if (n == 6) chunk2(c8, std::integral_constant<int, 6>{});
-                else if (n == 5) chunk2(c8, std::integral_constant<int, 5>{});
-                else if (n == 4) chunk2(c8, std::integral_constant<int, 4>{});
-                else if (n == 3) chunk2(c8, std::integral_constant<int, 3>{});
-                else if (n == 2) chunk2(c8, std::integral_constant<int, 2>{});
-                else if (n == 1) chunk2(c8, std::integral_constant<int, 1>{});
-            }
-        }
-        if (bcopy) BETA[((t + 1) & 1) * a.N + tid] = bload;
-        __syncthreads();
-        if (t == 0) F5_STAMP(6);
-        // ======== variable nodes ===========================================================
-        const bool last = (t == a.T - 1);
-        if constexpr (LUT) {
-            if (!last && tid < (a.qslice >> 1))
-                reinterpret_cast<uint32_t*>(QT + ((t + 1) & 1) * a.qslice)[tid] = qnext;
-        }
-        const float* bnext = BETA + (size_t)((t + 1) & 1) * a.N;     // unused when last
-        uint32_t any_hd = 0, any_pos = 0, nbits = 0;
-        const float qmf = (float)qmax;
-        const int sb = -(int)F5_SBIAS;
-        if (tid < F5_NDUMMY) W[total + tid] = F5_DUMMY_W;    // pass-2 adds of padding edges
-        if constexpr (!OUT) {
-            // counters only.  A wave owns the contiguous 64-entry chunks [c_beg, c_end); with
-            // SLOTS | z a chunk lies in one proto column, so beta is wave-uniform.  Only the
-            // hard-decision sign matters here, and clipping never changes a sign.
-            int amax = INT_MIN;                       // max APP over the target entries (last)
-            uint32_t aor = 0;                         // OR of F5_APPH-biased APPs (bit 23)
-            const int c_beg = wave * a.cpw;
-            const int c_end = min(c_beg + a.cpw, a.nfull);
-            const bool zuni = (z % SLOTS) == 0;
-            const uint32_t cvalid = (cw < nvalid) ? 1u : 0u;
-            const int tb = a.target_bits;
-            // Tv clamp bounds as the low 16 bits of Tv + F5_APP0 (= 16384 + Tv)
-            const uint32_t tlo = (uint32_t)(F5_APP0 - 2 * qmax) & 0xFFFFu;
-            const uint32_t thi = (uint32_t)(F5_APP0 + 2 * qmax) & 0xFFFFu;
-            // one loop body per (last iteration, whole word is target) pair; 4 chunks per trip
-            // with the reads issued first.  Reads past c_end stay inside LDS and are unused.
-            auto vn_loop = [&](auto lastc, auto fullc, auto zunic) __attribute__((always_inline)) {
-                constexpr bool LAST = decltype(lastc)::value;
-                constexpr bool FULLT = decltype(fullc)::value;
-                constexpr bool ZUNI = decltype(zunic)::value;
-                const uint32_t* Wr = W + c_beg * 64 + lane;
-                const float* Cr = CH + c_beg * 64 + lane;
-                for (int c = c_beg; c < c_end; c += 4, Wr += 256, Cr += 256) {
-                    uint32_t wv[4];
-                    float chv[4], bv[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        wv[j] = Wr[j * 64];
-                        chv[j] = Cr[j * 64];
-                        if (!LAST) {
-                            if (ZUNI) {
-                                const uint32_t col = __umulhi((uint32_t)((c + j) * SLOTS), a.zmagic);
-                                bv[j] = bnext[__builtin_amdgcn_readfirstlane(col)];
-                            } else {
-                                const uint32_t v = (uint32_t)((c + j) * 64 + lane) >> LOGCW;
-                                bv[j] = bnext[__umulhi(v, a.zmagic)];
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        if (j == 0 || c + j < c_end) {
-                            // Q(y) for y already scaled to grid units: clamp to +-qmax, then
-                            // add 1.5*2^23 so the float add rounds half to even (as rintf) and
-                            // the integer sits in the low mantissa bits: bits - F5_MAGIC_BITS
-                            const int s = (int)(wv[j] & 0x7FFFu);                     // S + bias
-                            const float yc = __builtin_amdgcn_fmed3f(chv[j] * inv, -qmf, qmf);
-                            const int qc = __float_as_int(yc + F5_MAGIC_A);
-                            // APP + F5_APPH: bit 23 set iff APP >= 0
-                            const int appb = qc + s;
-                            if (LAST) {
-                                int appt = appb;
-                                if (!FULLT) {
-                                    const int v = ((c + j) * 64 + lane) >> LOGCW;
-                                    appt = (v < tb) ? appb : INT_MIN;
-                                }
-                                amax = max(amax, appt);
-                                nbits += (uint32_t)(appt >= F5_APPH) & cvalid;
-                            } else {
-                                if (FULLT) {
-                                    aor |= (uint32_t)appb;
-                                } else {
-                                    const int v = ((c + j) * 64 + lane) >> LOGCW;
-                                    aor |= (v < tb) ? (uint32_t)appb : 0u;
-                                }
-                                const float yb = __builtin_amdgcn_fmed3f(chv[j] * bv[j], -qmf, qmf);
-                                // Tv + biases, Tv kept within +-2 qmax (pass 1's 8-bit range;
-                                // min(|Tv - m|, qmax) and the sign of Tv - m are unchanged)
-                                // (16-bit clamp: only the low half of Tv + F5_APP0 reaches W)
-                                const uint32_t tb2 = clamp_i16((uint32_t)(__float_as_int(yb + F5_MAGIC) + s),
-                                                               tlo, thi);
-                                // W = (Tv << 16) | S bias, Tv = tb2 - F5_MAGIC_BITS - S bias
-                                uint32_t wn = tb2 * 65536u + F5_WBIAS;
-                                if (UCN) wn |= ((uint32_t)appb >> 8) & 0x8000u;
-                                const_cast<uint32_t*>(Wr)[j * 64] = wn;
-                            }
-                        }
-                    }
-                }
-            };
-            using T_ = std::true_type;
-            using F_ = std::false_type;
-            if (!(a.ablate & 4)) {
-                const bool fullt = tb >= nv;
-                if (last) {                       // no W update: beta unused
-                    if (fullt) vn_loop(T_{}, T_{}, T_{}); else vn_loop(T_{}, F_{}, T_{});
-                } else if (zuni) {
-                    if (fullt) vn_loop(F_{}, T_{}, T_{}); else vn_loop(F_{}, F_{}, T_{});
-                } else {
-                    if (fullt) vn_loop(F_{}, T_{}, F_{}); else vn_loop(F_{}, F_{}, F_{});
-                }
-            }
-            // the partial last chunk (n_vars*CW not a multiple of 64), per-lane checks
-            if (a.nfull * 64 < total && wave == (a.nfull / max(a.cpw, 1)) % NWV && !(a.ablate & 4)) {
-                const int e = a.nfull * 64 + lane;
-                if (e < total) {
-                    const uint32_t v = (uint32_t)e >> LOGCW;
-                    const int s = (int)(W[e] & 0x7FFFu);
-                    const float ch = CH[e];
-                    const int app = q_scaled5(ch * inv, qmf) + s + sb;
-                    const int appt = ((int)v < a.target_bits) ? app : INT_MIN;
-                    amax = max(amax, appt == INT_MIN ? INT_MIN : appt + F5_APPH);
-                    aor |= (appt == INT_MIN) ? 0u : (uint32_t)(appt + F5_APPH);
-                    if (!last) {
-                        const int tn = min(max(q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], qmf) + s + sb,
-                                               -2 * qmax), 2 * qmax);
-                        W[e] = ((uint32_t)tn << 16) | (((uint32_t)~app >> 16) & 0x8000u) | F5_SBIAS;
-                    } else {
-                        nbits += (uint32_t)(appt >= 0 && appt != INT_MIN) & (uint32_t)cvalid;
-                    }
-                }
-            }
-            any_hd = last ? (amax >= F5_APPH) : ((aor >> 23) & 1u);
-            any_pos = amax > F5_APPH;
-        } else {
-        for (int r = 0; r < ((a.ablate & 4) ? 0 : a.nent); ++r) {
-            const int e = tid + r * NT;
-            if (e < total) {
-                const uint32_t v = (uint32_t)e >> LOGCW;
-                const uint32_t wv = W[e];
-                const int S = (int)(wv & 0x7FFFu) + sb;
-                const float ch = CH[e];
-                int app = q_units5(ch, inv, qmax) + S;                   // Q(xa) + sum C2V
-                app = min(max(app, -a.clip_u), a.clip_u);                // clip +-clip_LLR
-                if (!last) {
-                    const int tn = min(max(q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], (float)qmax) + S,
-                                           -2 * qmax), 2 * qmax);
-                    W[e] = ((uint32_t)tn << 16) | ((uint32_t)(app >= 0) << 15) | F5_SBIAS;
-                }
-                if ((int)v < a.target_bits) {
-                    any_hd |= (uint32_t)(app >= 0);
-                    if (last) { any_pos |= (uint32_t)(app > 0); nbits += (uint32_t)(app >= 0); }
-                    if (a.app_out && cw < nvalid)
-                        a.app_out[((size_t)t * a.B + b0 + cw) * a.target_bits + v] = (float)app * step;
-                }
-                if (a.hd_out && app >= 0 && cw < nvalid) {
-                    const int64_t b = b0 + cw;
-                    const int64_t tile = b / TILE;
-                    const int bl = (int)(b - tile * TILE);
-                    const size_t idx = ((((size_t)(t + 1) * a.ntiles + tile) * nv + v) * 4) + (bl & 3);
-                    atomicOr(reinterpret_cast<unsigned long long*>(a.hd_out + idx), 1ull << (bl >> 2));
-                }
-            }
-        }
-        if (last) nbits = (cw < nvalid) ? nbits : 0u;
-        }
-        unsigned long long bw = __ballot(any_hd);
-        unsigned long long m = 0;
-#pragma unroll
-        for (int s2 = 0; s2 < SLOTS; ++s2) m |= (bw >> (s2 * CW)) & cwmask;
-        if (lane == 0 && m) atomicOr(&RED[0], m);
-        if (last) {
-            bw = __ballot(any_pos);
-            m = 0;
-#pragma unroll
-            for (int s2 = 0; s2 < SLOTS; ++s2) m |= (bw >> (s2 * CW)) & cwmask;
-            if (lane == 0 && m) atomicOr(&RED[2], m);
-            uint32_t nb = nbits;
-            for (int off = 32; off > 0; off >>= 1) nb += __shfl_xor(nb, off);
-            if (lane == 0 && nb) atomicAdd(&RED[3], (unsigned long long)nb);
-        }
-        __syncthreads();
-    }
-    F5_STAMP(30);
-    if (a.stamps && tid == 0) {
-        uint32_t hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        a.stamps[(size_t)blockIdx.x * 32 + 31] = ((unsigned long long)xcc << 32) | hw;
-    }
-    if (tid == 0) {
-        const unsigned long long wl = RED[0] & valid_cw;
-        const unsigned long long all = RED[1] & RED[0] & valid_cw;
-        const unsigned long long ap = RED[2] & valid_cw;
-        if (a.counters) {
-            const unsigned long long c0 = RED[3];
-            const unsigned long long c1 = __popcll(wl);
-            const unsigned long long c2 = __popcll(all);
-            const unsigned long long c3 = 2ull * __popcll(ap) + __popcll(wl & ~ap);
-            unsigned long long* cc = reinterpret_cast<unsigned long long*>(a.counters);
-            if (c0) atomicAdd(cc + 0, c0);
-            if (c1) atomicAdd(cc + 1, c1);
-            if (c2) atomicAdd(cc + 2, c2);
-            if (c3) atomicAdd(cc + 3, c3);
-        }
-        RED[5] = all;
-        RED[6] = wl;
-    }
-    if (a.flags) {
-        __syncthreads();
-        if (tid < nvalid)
-            a.flags[b0 + tid] = (uint8_t)(((RED[5] >> tid) & 1) | (((RED[6] >> tid) & 1) << 1));
-    }
-}
+namespace f5 {
 
 // Per-decode tables shared by every workgroup:
 //   betas[t][n] = beta[t][n] / step  (a power of two: fl32(ch*beta)/step == fl32(ch*(beta/step)))
@@ -847,24 +103,6 @@ __global__ void k_f5_gad(const int32_t* __restrict__ row_ptr, const int32_t* __r
     }
 }
 
-// ---- shapes ------------------------------------------------------------------------------
-struct Shape5 {
-    int cw, maxg, maxdeg;
-    bool autosel;  // considered by plan5 (else only via LDPC_F5_SHAPE=<index>)
-    bool bal;      // deal groups to waves by row degree (k_f5_gad); LDPC_F5_BALANCE=0/1 overrides
-};
-constexpr Shape5 kShapes5[] = {
-    {16, 3, 16, true, false},    // wman-like (z=24, deg 14-15)
-    {16, 3, 24, true, false},    // 802.11n-like (deg 22)
-    {8, 5, 16, true, false},     // 5G BG2-like (z=64, deg <= 10)
-    {64, 3, 8, true, false},     // z=1 sparse (MacKay)
-    {64, 2, 32, true, false},    // z=1 dense rows (BCH)
-    {4, 3, 12, true, false},     // 5G BG2-like at two workgroups per CU (z=64: 16 slots, 4 codewords)
-    {8, 2, 24, true, false},     // 802.11n-like at three workgroups per CU
-    {4, 4, 20, true, false},     // 5G BG1-like (n = 2304 variables, deg 3-19, z = 72), one WG per CU
-    // measured and dropped: {8, 2, 16} at 8 waves/SIMD (64 VGPRs) ran 28.3 ms vs 21.3 ms for
-    // {16, 3, 16} on wman -- twice the per-workgroup fixed cost per codeword
-};
 
 size_t f5_lds(int nv, int cw, int T, int N) {
     (void)T;
@@ -891,6 +129,11 @@ Plan5 plan5(const DevGraph& g, int T) {
         const int ngroups = g.M * hstep;
         const int nw = (ngroups + sh.maxg - 1) / sh.maxg;
         if (nw > 16 || nw < 1) continue;
+        if (sh.hg > 0 && sh.hg < sh.maxg) {      // rows too heavy for a light slot must fit the heavy ones
+            int heavy = 0;
+            for (int i = 0; i < g.M; ++i) heavy += (g.h_row_ptr[i + 1] - g.h_row_ptr[i] > sh.ldeg);
+            if (heavy * hstep > sh.hg * nw) continue;
+        }
         if (g.N > 64 * nw) continue;                                    // beta slice copy
         const size_t lds = f5_lds(g.n_vars, sh.cw, T, g.N);
         if (lds > F5_LDS_MAX) continue;
@@ -900,7 +143,7 @@ Plan5 plan5(const DevGraph& g, int T) {
         // on the same SIMD: measured, a 14-wave group at 7 waves/SIMD runs alone).  VALU issue
         // saturates around 6 waves per SIMD, so waves beyond 24 per CU earn nothing.
         const int wg_lds = (int)(F5_LDS_MAX / lds);
-        const int wpe = std::max(f5_wpe(sh.cw, sh.maxg, sh.maxdeg), 4);
+        const int wpe = std::max(f5_wpe(sh.cw, sh.maxg, sh.maxdeg, sh.hg > 0 ? sh.hg : sh.maxg), 4);
         const int wg_waves = wpe / ((nw + 3) / 4);
         const int wgs = std::max(1, std::min(wg_lds, wg_waves));
         const double eff = (double)g.max_cdeg / (double)(((g.max_cdeg + 7) / 8) * 8);
@@ -918,43 +161,6 @@ Plan5 plan5(const DevGraph& g, int T) {
     return best;
 }
 
-template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW, bool OUT, bool LUT>
-int launch5o(const F5Args& a, int nblocks, int nw, size_t lds, const float* alpha,
-             const float* alpha_ucn, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused5<CW, MAXG, MAXDEG, UCN, PEW, OUT, LUT>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)F5_LDS_MAX);
-        attr = true;
-    }
-    hipLaunchKernelGGL((k_fused5<CW, MAXG, MAXDEG, UCN, PEW, OUT, LUT>), dim3(nblocks), dim3(64 * nw), lds, s,
-                       a, alpha, alpha_ucn);
-    return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
-}
-
-// the weight table is used when every row shares one weight and there is no UCN weight set
-template <int CW, int MAXG, int MAXDEG, bool UCN, bool PEW>
-int launch5k(const F5Args& a, int nblocks, int nw, size_t lds, bool lut, const float* alpha,
-             const float* alpha_ucn, hipStream_t s) {
-    constexpr bool CANLUT = !PEW;
-    const bool out = a.app_out || a.hd_out;
-    if (CANLUT && lut)
-        return out ? launch5o<CW, MAXG, MAXDEG, UCN, PEW, true, CANLUT>(a, nblocks, nw, lds, alpha, alpha_ucn, s)
-                   : launch5o<CW, MAXG, MAXDEG, UCN, PEW, false, CANLUT>(a, nblocks, nw, lds, alpha, alpha_ucn, s);
-    return out ? launch5o<CW, MAXG, MAXDEG, UCN, PEW, true, false>(a, nblocks, nw, lds, alpha, alpha_ucn, s)
-               : launch5o<CW, MAXG, MAXDEG, UCN, PEW, false, false>(a, nblocks, nw, lds, alpha, alpha_ucn, s);
-}
-
-template <int CW, int MAXG, int MAXDEG>
-int launch5s(const F5Args& a, int nblocks, int nw, size_t lds, bool lut, const float* alpha,
-             const float* alpha_ucn, bool pew, hipStream_t s) {
-    if (alpha_ucn)
-        return pew ? launch5k<CW, MAXG, MAXDEG, true, true>(a, nblocks, nw, lds, lut, alpha, alpha_ucn, s)
-                   : launch5k<CW, MAXG, MAXDEG, true, false>(a, nblocks, nw, lds, lut, alpha, alpha_ucn, s);
-    return pew ? launch5k<CW, MAXG, MAXDEG, false, true>(a, nblocks, nw, lds, lut, alpha, nullptr, s)
-               : launch5k<CW, MAXG, MAXDEG, false, false>(a, nblocks, nw, lds, lut, alpha, nullptr, s);
-}
-
 // LDPC_DIAG_STAMPS=<file>: raw per-workgroup marks of one launch, [nblocks][32] u64 (100 MHz
 // s_memrealtime: 0 start, 1 after the LLR/CH prologue, 2 after the edge-address setup, 5 after
 // iteration 0's pass 1, 6 after its pass-2 barrier, 8 + t start of iteration t, 30 end; slot 31
@@ -970,7 +176,9 @@ void report_stamps(const unsigned long long* d, int nblocks, hipStream_t s, cons
     }
 }
 
-}  // namespace
+}  // namespace f5
+
+using namespace f5;
 
 bool fused5_supported(const DevGraph& g, int T) { return plan5(g, T).shape >= 0; }
 
@@ -1062,7 +270,8 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
                            1.0f / step, qslice, betas, lut ? qtab : nullptr);
         const int lcw = f5_logcw(sh.cw);
         const char* be = getenv("LDPC_F5_BALANCE");
-        const bool bal = be ? atoi(be) != 0 : sh.bal;
+        const bool hetero = sh.hg > 0 && sh.hg < sh.maxg;
+        const bool bal = hetero || (be ? atoi(be) != 0 : sh.bal);
         hipLaunchKernelGGL(k_f5_gad, dim3((unsigned)((p.ngroups * 64 + 255) / 256)), dim3(256), 0, s,
                            g.row_ptr, g.pe_col, g.pe_shift, g.M, p.ngroups, p.hstep, g.z, lcw,
                            sh.maxdeg, npk, g.n_vars * sh.cw, p.nw, bal ? 1 : 0, gad, grow);
@@ -1082,14 +291,15 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
         return LDPC_ERR_OOM;
     int rc;
     switch (p.shape) {
-        case 0: rc = launch5s<16, 3, 16>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
-        case 1: rc = launch5s<16, 3, 24>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
-        case 2: rc = launch5s<8, 5, 16>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
-        case 3: rc = launch5s<64, 3, 8>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
-        case 4: rc = launch5s<64, 2, 32>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
-        case 5: rc = launch5s<4, 3, 12>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
-        case 6: rc = launch5s<8, 2, 24>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
-        case 7: rc = launch5s<4, 4, 20>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 0: rc = f5_launch<0>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 1: rc = f5_launch<1>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 2: rc = f5_launch<2>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 3: rc = f5_launch<3>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 4: rc = f5_launch<4>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 5: rc = f5_launch<5>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 6: rc = f5_launch<6>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 7: rc = f5_launch<7>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 8: rc = f5_launch<8>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
         default: rc = LDPC_ERR_UNSUPPORTED;
     }
     if (diag) {

@@ -39,6 +39,7 @@ struct DevGraph {
     const int32_t* pe_shift;   // [E]  P[i,j] mod z
     const int32_t* col_ptr;    // [N+1]
     const int32_t* col_pe;     // [E]  proto edges of each column, ascending row
+    const int32_t* h_row_ptr;  // [M+1] host copy of row_ptr (kernel planning)
 };
 
 // Per-decode buffers and scalars.
