@@ -138,12 +138,12 @@ Plan5 plan5(const DevGraph& g, int T) {
         const size_t lds = f5_lds(g.n_vars, sh.cw, T, g.N);
         if (lds > F5_LDS_MAX) continue;
         if (((size_t)g.n_vars * sh.cw + F5_NDUMMY) * 4 > 65536) continue;    // 16-bit addresses
-        // resident workgroups per CU: LDS and the shape's VGPR budget (f5_wpe waves per SIMD;
+        // resident workgroups per CU: LDS and the shape's VGPR budget (Shape5::wpe waves per SIMD;
         // a workgroup puts ceil(nw/4) waves on its busiest SIMD and the next workgroup starts
         // on the same SIMD: measured, a 14-wave group at 7 waves/SIMD runs alone).  VALU issue
         // saturates around 6 waves per SIMD, so waves beyond 24 per CU earn nothing.
         const int wg_lds = (int)(F5_LDS_MAX / lds);
-        const int wpe = std::max(f5_wpe(sh.cw, sh.maxg, sh.maxdeg, sh.hg > 0 ? sh.hg : sh.maxg), 4);
+        const int wpe = std::max(sh.wpe, 4);
         const int wg_waves = wpe / ((nw + 3) / 4);
         const int wgs = std::max(1, std::min(wg_lds, wg_waves));
         const double eff = (double)g.max_cdeg / (double)(((g.max_cdeg + 7) / 8) * 8);
@@ -300,6 +300,7 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
         case 6: rc = f5_launch<6>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
         case 7: rc = f5_launch<7>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
         case 8: rc = f5_launch<8>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
+        case 9: rc = f5_launch<9>(a, nblocks, p.nw, p.lds, lut, b.alpha, au, per_edge_w, s); break;
         default: rc = LDPC_ERR_UNSUPPORTED;
     }
     if (diag) {

@@ -194,12 +194,6 @@ struct Sel {
         if (a.stamps && tid == 0) a.stamps[(size_t)blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
-// occupancy target (waves per SIMD) of a shape: the VGPR budget that lets the planned number of
-// workgroups share a CU (plan5 assumes the same figure)
-constexpr int f5_wpe(int cw, int maxg, int maxdeg, int hg) {
-    return (cw == 16 && maxdeg == 16) ? 6 : (cw == 4 && hg < maxg) ? 4 : (cw == 4 && maxg == 4) ? 4
-         : (cw == 4) ? 7 : (cw == 8 && maxg == 2) ? 6 : 1;
-}
 // per-slot degree bound: a wave's first HG group slots take rows of degree <= MAXDEG, the
 // others rows of degree <= LDEG (shapes for graphs whose rows differ widely in degree: the
 // state of a light slot needs fewer registers).  HG == MAXG: one bound for every slot.
@@ -211,8 +205,10 @@ struct GDeg {
 };
 constexpr int f5_logcw(int cw) { return cw == 64 ? 6 : cw == 32 ? 5 : cw == 16 ? 4 : cw == 8 ? 3 : 2; }
 
-template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, bool UCN, bool PEW, bool OUT, bool LUT>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(f5_wpe(CW, MAXG, MAXDEG, HG))))
+// WPE: the shape's occupancy target (waves per SIMD): the VGPR budget that lets the planned
+// number of workgroups share a CU (Shape5::wpe; plan5 assumes the same figure)
+template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, int WPE, bool UCN, bool PEW, bool OUT, bool LUT>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ alpha_ucn) {
     using SL = Sel<MAXDEG>;                 // selector layout of every slot (light ones use a prefix)
     using GD = GDeg<MAXDEG, HG, LDEG>;
@@ -776,60 +772,63 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
 // ---- shapes ------------------------------------------------------------------------------
 struct Shape5 {
     int cw, maxg, maxdeg;
+    int wpe;       // occupancy target, waves per SIMD (1: no VGPR cap).  VALU issue saturates near 6
     bool autosel;  // considered by plan5 (else only via LDPC_F5_SHAPE=<index>)
     bool bal;      // deal groups to waves by row degree (k_f5_gad); LDPC_F5_BALANCE=0/1 overrides
     int hg = 0, ldeg = 0;   // hg < maxg: slots gi >= hg take rows of degree <= ldeg (GDeg; the
                             // degree-ranked dealing puts the heaviest groups in slots gi < hg)
 };
 constexpr Shape5 kShapes5[] = {
-    {16, 3, 16, true, false},    // wman-like (z=24, deg 14-15)
-    {16, 3, 24, true, false},    // 802.11n-like (deg 22)
-    {8, 5, 16, true, false},     // 5G BG2-like (z=64, deg <= 10)
-    {64, 3, 8, true, false},     // z=1 sparse (MacKay)
-    {64, 2, 32, true, false},    // z=1 dense rows (BCH)
-    {4, 3, 12, true, false},     // 5G BG2-like at two workgroups per CU (z=64: 16 slots, 4 codewords)
-    {8, 2, 24, true, false},     // 802.11n-like at three workgroups per CU
-    {4, 4, 20, true, false},     // 5G BG1-like (n = 2304 variables, deg 3-19, z = 72), one WG per CU
-    {4, 7, 20, true, true, 3, 10},   // 5G BG1-like, 3 heavy + 4 light slots, 8 waves: two WGs per CU
+    {16, 3, 16, 6, true, false},    // wman-like (z=24, deg 14-15)
+    {16, 3, 24, 1, true, false},    // 802.11n-like (deg 22)
+    {8, 5, 16, 1, true, false},     // 5G BG2-like (z=64, deg <= 10)
+    {64, 3, 8, 1, true, false},     // z=1 sparse (MacKay)
+    {64, 2, 32, 1, true, false},    // z=1 dense rows (BCH)
+    {4, 3, 12, 7, true, false},     // 5G BG2-like at two workgroups per CU (z=64: 16 slots, 4 codewords)
+    {8, 2, 24, 6, true, false},     // 802.11n-like at three workgroups per CU
+    {4, 4, 20, 4, true, false},     // 5G BG1-like (n = 2304 variables, deg 3-19, z = 72), one WG per CU
+    {4, 7, 20, 4, true, true, 3, 10},   // 5G BG1-like, 3 heavy + 4 light slots, 8 waves: two WGs per CU
+    {4, 5, 10, 6, true, true, 2, 6},    // 5G BG2-like (deg 8-10 / 4-6), 8 waves: three WGs per CU
     // measured and dropped: {8, 2, 16} at 8 waves/SIMD (64 VGPRs) ran 28.3 ms vs 21.3 ms for
-    // {16, 3, 16} on wman -- twice the per-workgroup fixed cost per codeword
+    // {16, 3, 16} on wman -- twice the per-workgroup fixed cost per codeword; {4, 5, 20, 2/10} at
+    // 10 waves and 80 VGPRs spilled ~50 registers
 };
 
-template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, bool UCN, bool PEW, bool OUT, bool LUT>
+template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, int WPE, bool UCN, bool PEW, bool OUT, bool LUT>
 int launch5o(const F5Args& a, int nblocks, int nw, size_t lds, const float* alpha,
              const float* alpha_ucn, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused5<CW, MAXG, MAXDEG, HG, LDEG, UCN, PEW, OUT, LUT>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused5<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)F5_LDS_MAX);
         attr = true;
     }
-    hipLaunchKernelGGL((k_fused5<CW, MAXG, MAXDEG, HG, LDEG, UCN, PEW, OUT, LUT>), dim3(nblocks), dim3(64 * nw), lds, s,
+    hipLaunchKernelGGL((k_fused5<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>), dim3(nblocks), dim3(64 * nw), lds, s,
                        a, alpha, alpha_ucn);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 
 // the weight table is used when every row shares one weight and there is no UCN weight set
-template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, bool UCN, bool PEW>
+template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, int WPE, bool UCN, bool PEW>
 int launch5k(const F5Args& a, int nblocks, int nw, size_t lds, bool lut, const float* alpha,
              const float* alpha_ucn, hipStream_t s) {
     constexpr bool CANLUT = !PEW;
     const bool out = a.app_out || a.hd_out;
     if (CANLUT && lut)
-        return out ? launch5o<CW, MAXG, MAXDEG, HG, LDEG, UCN, PEW, true, CANLUT>(a, nblocks, nw, lds, alpha, alpha_ucn, s)
-                   : launch5o<CW, MAXG, MAXDEG, HG, LDEG, UCN, PEW, false, CANLUT>(a, nblocks, nw, lds, alpha, alpha_ucn, s);
-    return out ? launch5o<CW, MAXG, MAXDEG, HG, LDEG, UCN, PEW, true, false>(a, nblocks, nw, lds, alpha, alpha_ucn, s)
-               : launch5o<CW, MAXG, MAXDEG, HG, LDEG, UCN, PEW, false, false>(a, nblocks, nw, lds, alpha, alpha_ucn, s);
+        return out ? launch5o<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, true, CANLUT>(a, nblocks, nw, lds, alpha, alpha_ucn, s)
+                   : launch5o<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, false, CANLUT>(a, nblocks, nw, lds, alpha, alpha_ucn, s);
+    return out ? launch5o<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, true, false>(a, nblocks, nw, lds, alpha, alpha_ucn, s)
+               : launch5o<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, false, false>(a, nblocks, nw, lds, alpha, alpha_ucn, s);
 }
 
-template <int CW, int MAXG, int MAXDEG, int HG = MAXG, int LDEG = MAXDEG>
+template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, int WPE>
 int launch5s(const F5Args& a, int nblocks, int nw, size_t lds, bool lut, const float* alpha,
              const float* alpha_ucn, bool pew, hipStream_t s) {
     if (alpha_ucn)
-        return pew ? launch5k<CW, MAXG, MAXDEG, HG, LDEG, true, true>(a, nblocks, nw, lds, lut, alpha, alpha_ucn, s)
-                   : launch5k<CW, MAXG, MAXDEG, HG, LDEG, true, false>(a, nblocks, nw, lds, lut, alpha, alpha_ucn, s);
-    return pew ? launch5k<CW, MAXG, MAXDEG, HG, LDEG, false, true>(a, nblocks, nw, lds, lut, alpha, nullptr, s)
-               : launch5k<CW, MAXG, MAXDEG, HG, LDEG, false, false>(a, nblocks, nw, lds, lut, alpha, nullptr, s);
+        return pew ? launch5k<CW, MAXG, MAXDEG, HG, LDEG, WPE, true, true>(a, nblocks, nw, lds, lut, alpha, alpha_ucn, s)
+                   : launch5k<CW, MAXG, MAXDEG, HG, LDEG, WPE, true, false>(a, nblocks, nw, lds, lut, alpha, alpha_ucn, s);
+    return pew ? launch5k<CW, MAXG, MAXDEG, HG, LDEG, WPE, false, true>(a, nblocks, nw, lds, lut, alpha, nullptr, s)
+               : launch5k<CW, MAXG, MAXDEG, HG, LDEG, WPE, false, false>(a, nblocks, nw, lds, lut, alpha, nullptr, s);
 }
 
 // the launcher of shape S (kShapes5[S]); defined in the translation unit built from

@@ -16,7 +16,7 @@ int f5_launch(const F5Args& a, int nblocks, int nw, size_t lds, bool lut, const 
     constexpr Shape5 sh = kShapes5[S];
     constexpr int hg = sh.hg > 0 ? sh.hg : sh.maxg;
     constexpr int ldeg = sh.hg > 0 ? sh.ldeg : sh.maxdeg;
-    return launch5s<sh.cw, sh.maxg, sh.maxdeg, hg, ldeg>(a, nblocks, nw, lds, lut, alpha, alpha_ucn,
+    return launch5s<sh.cw, sh.maxg, sh.maxdeg, hg, ldeg, sh.wpe>(a, nblocks, nw, lds, lut, alpha, alpha_ucn,
                                                           pew, s);
 }
 
