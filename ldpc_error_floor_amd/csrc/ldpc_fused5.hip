@@ -13,17 +13,15 @@ namespace ldpc {
 
 namespace f5 {
 
-// Per-decode tables shared by every workgroup:
-//   betas[t][n] = beta[t][n] / step  (a power of two: fl32(ch*beta)/step == fl32(ch*(beta/step)))
+// Per-decode weight table shared by every workgroup (beta needs none: the kernel keeps ch / step
+// and reads beta as given, fl32(ch*beta)/step == fl32((ch/step)*beta)):
 //   qtab[t][tab][row][m] = [+q, -q] bytes, q = Q(relu(|o| * w)), |o| = m grid units
 //                     (m = qmax+1 stands for "no other edge", the 10000 value), w = alpha_t,row
 //                     (tab 0) or alpha_ucn_t,row (tab 1, UCN only); qslice halfwords per t
 __global__ void k_f5_tables(const float* __restrict__ alpha, const float* __restrict__ alpha_ucn,
-                            const float* __restrict__ beta, const int32_t* __restrict__ row_ptr,
-                            int T, int Mp, int E, int N, int qmax, float step, float inv,
-                            int qslice, float* betas, uint16_t* qtab) {
+                            const int32_t* __restrict__ row_ptr, int T, int Mp, int E, int qmax,
+                            float step, float inv, int qslice, uint16_t* qtab) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f < T * N) betas[f] = beta[f] * inv;
     const int nq = qmax + 2;
     if (qtab && f < T * qslice) {
         const int tt = f / qslice, rem = f - tt * qslice;
@@ -243,9 +241,9 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     a.zmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.z - 1) / (uint64_t)g.z);
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // timing only
     // shared tables: one small launch per decode instead of per-workgroup dependent loads
-    const size_t nbeta = (size_t)b.T * g.N, nqt = (size_t)b.T * qslice;
+    const size_t nqt = (size_t)b.T * qslice;
     const int npk = (sh.maxdeg + 1) / 2;
-    const size_t off_qt = (nbeta * 4 + 255) & ~(size_t)255;
+    const size_t off_qt = 0;
     const size_t off_gad = (off_qt + nqt * 2 + 255) & ~(size_t)255;
     const size_t off_grow = off_gad + (size_t)p.ngroups * npk * 64 * 4;
     const size_t tbytes = off_grow + (size_t)p.ngroups * 16;
@@ -259,15 +257,14 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
         }
         ws.tables_bytes = tbytes;
     }
-    float* betas = reinterpret_cast<float*>(ws.tables);
     uint16_t* qtab = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(ws.tables) + off_qt);
     uint32_t* gad = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws.tables) + off_gad);
     uint4* grow = reinterpret_cast<uint4*>(reinterpret_cast<char*>(ws.tables) + off_grow);
     {
-        const size_t nthr = std::max(nbeta, lut ? nqt : (size_t)0);
-        hipLaunchKernelGGL(k_f5_tables, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s,
-                           b.alpha, b.alpha_ucn, b.beta, g.row_ptr, b.T, g.M, g.E, g.N, qmax, step,
-                           1.0f / step, qslice, betas, lut ? qtab : nullptr);
+        if (lut)
+            hipLaunchKernelGGL(k_f5_tables, dim3((unsigned)((nqt + 255) / 256)), dim3(256), 0, s,
+                               b.alpha, b.alpha_ucn, g.row_ptr, b.T, g.M, g.E, qmax, step,
+                               1.0f / step, qslice, qtab);
         const int lcw = f5_logcw(sh.cw);
         const char* be = getenv("LDPC_F5_BALANCE");
         const bool hetero = sh.hg > 0 && sh.hg < sh.maxg;
@@ -277,7 +274,7 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
                            sh.maxdeg, npk, g.n_vars * sh.cw, p.nw, bal ? 1 : 0, gad, grow);
         if (hipGetLastError() != hipSuccess) return LDPC_ERR_HIP;
     }
-    a.betas = betas;
+    a.betas = b.beta;      // [T][N] as given (the kernel keeps ch / step)
     a.qtab = qtab;
     a.qslice = qslice;
     a.qucn = qucn;

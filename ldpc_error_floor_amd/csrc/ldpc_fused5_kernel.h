@@ -79,7 +79,7 @@ struct F5Args {
     int hstep, ngroups, nent;
     int nfull, cpw;    // VN: full 64-entry chunks, chunks per wave
     int Mp;            // proto rows
-    const float* betas;        // [T][N] beta / step (setup kernel)
+    const float* betas;        // [T][N] beta (the kernel keeps ch / step)
     const uint16_t* qtab;      // [T][qslice] weight tables (setup kernel), LUT builds only
     int qslice;                // halfwords per iteration: [alpha | alpha_ucn][Mp][qmax+2], even
     int qucn;                  // halfword offset of the alpha_ucn table inside a slice
@@ -221,7 +221,9 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     const int total = nv * CW;
     uint32_t* W = reinterpret_cast<uint32_t*>(smem);                              // [nv*CW + CW]
     float* CH = reinterpret_cast<float*>(smem + ((size_t)total + F5_NDUMMY) * 4); // [nv*CW]
-    float* BETA = CH + total;                     // [2][N]: beta_t / step in slot t & 1
+    // CH holds ch / step (exact: step is a power of two), so Q(ch) is a clamp and rounding of
+    // CH, and Q(fl32(ch * beta)) in grid units is that of fl32(CH * beta)
+    float* BETA = CH + total;                     // [2][N]: beta_t in slot t & 1
     unsigned long long* RED = reinterpret_cast<unsigned long long*>(
         smem + ((((size_t)total + F5_NDUMMY) * 4 + (size_t)total * 4 + (size_t)2 * a.N * 4 + 15) & ~(size_t)15));
     uint16_t* QT = reinterpret_cast<uint16_t*>(RED + 8);                          // [2][qslice]
@@ -277,7 +279,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 reinterpret_cast<uint32_t*>(QT)[f] = reinterpret_cast<const uint32_t*>(a.qtab)[f];
         }
         __syncthreads();
-        for (int e = tid; e < total; e += NT) CH[e] = scr[(e & (CW - 1)) * rl + (e >> LOGCW)];
+        for (int e = tid; e < total; e += NT) CH[e] = scr[(e & (CW - 1)) * rl + (e >> LOGCW)] * inv;
         __syncthreads();
         for (int e = tid; e < total; e += NT) {
             const uint32_t v = (uint32_t)e >> LOGCW;
@@ -620,7 +622,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                             // add 1.5*2^23 so the float add rounds half to even (as rintf) and
                             // the integer sits in the low mantissa bits: bits - F5_MAGIC_BITS
                             const int s = (int)(wv[j] & 0x7FFFu);                     // S + bias
-                            const float yc = __builtin_amdgcn_fmed3f(chv[j] * inv, -qmf, qmf);
+                            const float yc = __builtin_amdgcn_fmed3f(chv[j], -qmf, qmf);
                             const int qc = __float_as_int(yc + F5_MAGIC_A);
                             // APP + F5_APPH: bit 23 set iff APP >= 0
                             const int appb = qc + s;
@@ -673,7 +675,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     const uint32_t v = (uint32_t)e >> LOGCW;
                     const int s = (int)(W[e] & 0x7FFFu);
                     const float ch = CH[e];
-                    const int app = q_scaled5(ch * inv, qmf) + s + sb;
+                    const int app = q_scaled5(ch, qmf) + s + sb;
                     const int appt = ((int)v < a.target_bits) ? app : INT_MIN;
                     amax = max(amax, appt == INT_MIN ? INT_MIN : appt + F5_APPH);
                     aor |= (appt == INT_MIN) ? 0u : (uint32_t)(appt + F5_APPH);
@@ -696,7 +698,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 const uint32_t wv = W[e];
                 const int S = (int)(wv & 0x7FFFu) + sb;
                 const float ch = CH[e];
-                int app = q_units5(ch, inv, qmax) + S;                   // Q(xa) + sum C2V
+                int app = q_scaled5(ch, (float)qmax) + S;                // Q(xa) + sum C2V
                 app = min(max(app, -a.clip_u), a.clip_u);                // clip +-clip_LLR
                 if (!last) {
                     const int tn = min(max(q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], (float)qmax) + S,
@@ -791,7 +793,8 @@ constexpr Shape5 kShapes5[] = {
     {4, 5, 10, 6, true, true, 2, 6},    // 5G BG2-like (deg 8-10 / 4-6), 8 waves: three WGs per CU
     // measured and dropped: {8, 2, 16} at 8 waves/SIMD (64 VGPRs) ran 28.3 ms vs 21.3 ms for
     // {16, 3, 16} on wman -- twice the per-workgroup fixed cost per codeword; {4, 5, 20, 2/10} at
-    // 10 waves and 80 VGPRs spilled ~50 registers
+    // 10 waves and 80 VGPRs spilled ~50 registers; {8, 3, 16} (wman, 6 waves, four WGs per CU)
+    // 23.1 ms vs 18.7 ms; {4, 2, 24} (802.11n, 4 waves, seven WGs per CU) within 0.3% of {8, 2, 24}
 };
 
 template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, int WPE, bool UCN, bool PEW, bool OUT, bool LUT>
