@@ -40,7 +40,8 @@ __global__ void k_f5_tables(const float* __restrict__ alpha, const float* __rest
 // Edge addresses per (check group, lane): lane = slot * CW + cw serves circulant row
 // h = hg * SLOTS + slot of proto row i (grp = i * hstep + hg); edge k of that row reads
 // W[(pe_col * z + (h + shift) mod z) * CW + cw], packed as byte offsets two per word.  Lanes
-// with h >= z (last group of a row) mirror slot 0's row and are masked out of the results.
+// with h >= z (last group of a row) point every edge at the lane's own dummy word (no two
+// lanes' pass-2 atomics on one LDS word) and are masked out of the results.
 //
 // Table position s is what wave s % nw runs as its group s / nw.  bal = 0: position s is group
 // s.  bal = 1 (graphs with very unequal row degrees): groups are ranked by row degree, heaviest
@@ -78,14 +79,13 @@ __global__ void k_f5_gad(const int32_t* __restrict__ row_ptr, const int32_t* __r
     const int i = rg / hstep, hg = rg - i * hstep;
     const int r0 = row_ptr[i], deg = row_ptr[i + 1] - r0;
     const int h = hg * slots + slot;
-    const int hl = (h < z) ? h : hg * slots;
     for (int p = 0; p < npk; ++p) {
         uint32_t word = 0;
         for (int j = 0; j < 2; ++j) {
             const int k = 2 * p + j;
             uint32_t byte = (uint32_t)(total + lane) * 4u;            // dummy word of this lane
-            if (k < deg && k < maxdeg) {
-                int hs = hl + pe_shift[r0 + k];
+            if (h < z && k < deg && k < maxdeg) {
+                int hs = h + pe_shift[r0 + k];
                 hs = (hs >= z) ? hs - z : hs;
                 byte = (uint32_t)(((pe_col[r0 + k] * z + hs) << logcw) + cw) * 4u;
             }

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 K=${K:-fused}; B=${B:-262144}; TAG=${TAG:-p}
 OUT=gpurun_out/prof_${TAG}_${K}
 mkdir -p $OUT
-ARGS="--kernel $K --batch $B --reps 3"
+ARGS="--kernel $K --batch $B --reps 3 --config ${CFG:-C2}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 tools/prof_decode.py $ARGS > $OUT/trace.log 2>&1 || { tail $OUT/trace.log; exit 1; }
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM" \
