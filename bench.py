@@ -35,6 +35,9 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD (32 lanes
+# per cycle, MI355X_MICROARCH.md "Wave scheduling") at 2.4 GHz, in wave-instructions per second
+VALU_PEAK_WINST = 256 * 4 * 2.4e9 / 2
 DATA = os.path.join(ROOT, "ldpc_error_floor_amd", "data")
 
 # SURVEY.md §8 d workloads.  C2 is BASELINE.json's configs[1] (the driver's line).
@@ -213,6 +216,7 @@ def main():
     bytes_cw = survey_bytes_per_cw(g.E, g.N, z, T, ucn=cfg["sharing"][1] > 0)
     achieved = bytes_cw * B / (primary["kernel_ms"] / 1e3) / 1e9
     traffic = None
+    valu = None
     safe = "".join(ch if (ch.isalnum() or ch in "_.-") else "_" for ch in primary["name"])
     tf = os.path.join(ROOT, "profiles", f"traffic_{safe}.json")
     if os.path.exists(tf):
@@ -221,6 +225,16 @@ def main():
                 tj = json.load(f)
             if int(tj.get("batch", -1)) == B:
                 traffic = tj.get("hbm_bytes_per_launch")
+                if tj.get("valu_insts_per_launch"):
+                    rate = tj["valu_insts_per_launch"] / (primary["kernel_ms"] / 1e3)
+                    valu = {"achieved": round(rate, 1), "peak": VALU_PEAK_WINST,
+                            "unit": "wave-instructions/s", "frac": round(rate / VALU_PEAK_WINST, 4),
+                            "insts_per_launch": tj["valu_insts_per_launch"],
+                            "wait_any_frac": tj.get("wait_any_frac"), "source": tj.get("source"),
+                            "note": "the fused kernel's real bound: SQ_INSTS_VALU (PMC, "
+                                    "profiles/) over this run's kernel time, against one wave64 "
+                                    "VALU issue per 2 cycles per SIMD; VOP3/SDWA forms issue "
+                                    "at about half that rate (DESIGN.md 3.2)"}
         except (OSError, ValueError):
             traffic = None
     c = primary["counters"]
@@ -256,6 +270,7 @@ def main():
                      "note": "achieved = SURVEY 8d two-kernel fp32 bytes/codeword x B / decode "
                              "time (HIP events); for the fused kernel this is an effective "
                              "figure (its real HBM traffic is design_bytes_per_cw)"},
+        "valu_issue": valu,
         "fer_at_snr": {"frames": n_frames, "fer_last": c[1] / n_frames,
                        "ber_last": c[0] / (n_frames * g.N * z)},
     }

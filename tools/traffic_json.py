@@ -94,6 +94,9 @@ def main():
           "fetch_bytes": round(fetch), "write_bytes": round(write),
           "bytes_per_codeword": round((fetch + write) / a.batch, 1),
           "avg_launch_ns": round(avg_ns), "source": os.path.relpath(a.out, ROOT),
+          "valu_insts_per_launch": round(pm["SQ_INSTS_VALU"]) if "SQ_INSTS_VALU" in pm else None,
+          "wait_any_frac": (round(pm["SQ_WAIT_ANY"] / pm["SQ_WAVE_CYCLES"], 4)
+                            if "SQ_WAIT_ANY" in pm and pm.get("SQ_WAVE_CYCLES") else None),
           "method": "2 x FETCH_SIZE + WRITE_SIZE (KiB), separate --pmc passes, gfx950 "
                     "FETCH_SIZE half-count correction (MI355X_MICROARCH.md, HBM)"}
     path = os.path.join(ROOT, "profiles", f"traffic_{sn}.json")
