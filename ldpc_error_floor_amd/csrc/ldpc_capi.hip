@@ -256,6 +256,17 @@ int ldpc_graph_create(const int32_t* proto, int32_t M, int32_t N, int32_t z, int
     host.insert(host.end(), g->pe_shift.begin(), g->pe_shift.end());
     host.insert(host.end(), g->col_ptr.begin(), g->col_ptr.end());
     host.insert(host.end(), g->col_pe.begin(), g->col_pe.end());
+    // | pad to 16 B | vn_edge: per edge in column order, {C->V row base r0*z + (pe - r0), row
+    // degree, shift, 0} (the VN kernel's one scalar load per edge)
+    while (host.size() % 4) host.push_back(0);
+    const size_t off_vn = host.size();
+    for (int e = 0; e < g->E; ++e) {
+        const int pe = g->col_pe[e], i = g->pe_row[pe], r0 = g->row_ptr[i];
+        host.push_back(r0 * z + (pe - r0));
+        host.push_back(g->row_ptr[i + 1] - r0);
+        host.push_back(g->pe_shift[pe]);
+        host.push_back(0);
+    }
     {
         DeviceGuard dg(device);
         if (dev_alloc(&g->d_tables, host.size()) != LDPC_OK) { delete g; return LDPC_ERR_OOM; }
@@ -276,6 +287,7 @@ int ldpc_graph_create(const int32_t* proto, int32_t M, int32_t N, int32_t z, int
     d.pe_shift = p; p += g->E;
     d.col_ptr = p; p += N + 1;
     d.col_pe = p;
+    d.vn_edge = reinterpret_cast<const int4*>(g->d_tables + off_vn);
     d.h_row_ptr = g->row_ptr.data();
     *out = g;
     return LDPC_OK;

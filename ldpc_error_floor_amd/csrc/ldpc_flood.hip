@@ -264,16 +264,24 @@ __global__ void __launch_bounds__(256) k_vn_update(DevGraph g, Bufs p, int t) {
         const int j = v / g.z;
         const int gg = v - j * g.z;
         float4 S = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int e = g.col_ptr[j]; e < g.col_ptr[j + 1]; ++e) {
-            const int pe = g.col_pe[e];
-            const int i = g.pe_row[pe];
-            const int r0 = g.row_ptr[i];
-            const int deg = g.row_ptr[i + 1] - r0;
-            int h = gg - g.pe_shift[pe];
-            if (h < 0) h += g.z;
-            const size_t row = (size_t)r0 * g.z + (size_t)h * deg + (pe - r0);
-            const float4 cv = ld4(Ct + row * TILE);
-            S.x += cv.x; S.y += cv.y; S.z += cv.z; S.w += cv.w;
+        // the column's edges four at a time: one scalar table load per edge and all four
+        // message rows in flight before the (in-order, as before) sum
+        const int e0 = g.col_ptr[j], e1 = g.col_ptr[j + 1];
+        for (int e = e0; e < e1; e += 4) {
+            float4 cv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (e + u < e1) {
+                    const int4 ve = g.vn_edge[e + u];
+                    int h = gg - ve.z;
+                    if (h < 0) h += g.z;
+                    cv[u] = ld4(Ct + ((size_t)ve.x + (size_t)h * ve.y) * TILE);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (e + u < e1) { S.x += cv[u].x; S.y += cv[u].y; S.z += cv[u].z; S.w += cv[u].w; }
+            }
         }
         const size_t vrow = ((size_t)tile * g.n_vars + v) * TILE + 4 * lane;
         const float4 ch = ld4(p.ch + vrow);
