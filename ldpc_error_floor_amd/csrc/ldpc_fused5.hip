@@ -15,14 +15,15 @@ namespace f5 {
 
 // Per-decode weight table shared by every workgroup (beta needs none: the kernel keeps ch / step
 // and reads beta as given, fl32(ch*beta)/step == fl32((ch/step)*beta)):
-//   qtab[t][tab][row][m] = [+q, -q] bytes, q = Q(relu(|o| * w)), |o| = m grid units
-//                     (m = qmax+1 stands for "no other edge", the 10000 value), w = alpha_t,row
+//   qtab[t][tab][row][m] = [+q, -q] bytes, q = Q(relu(|o| * w)), |o| = min(m, qmax) grid units
+//                     for m <= 3 qmax (the kernel indexes by the unclamped |Tv - m|), m = 3 qmax
+//                     + 1 stands for "no other edge" (the 10000 value), w = alpha_t,row
 //                     (tab 0) or alpha_ucn_t,row (tab 1, UCN only); qslice halfwords per t
 __global__ void k_f5_tables(const float* __restrict__ alpha, const float* __restrict__ alpha_ucn,
                             const int32_t* __restrict__ row_ptr, int T, int Mp, int E, int qmax,
                             float step, float inv, int qslice, uint16_t* qtab) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    const int nq = qmax + 2;
+    const int nq = 3 * qmax + 2;               // |o| = 0 .. 3 qmax (min(|o|, qmax) used), none
     if (qtab && f < T * qslice) {
         const int tt = f / qslice, rem = f - tt * qslice;
         const int tab = rem / (Mp * nq), r2 = rem - tab * (Mp * nq);
@@ -30,7 +31,7 @@ __global__ void k_f5_tables(const float* __restrict__ alpha, const float* __rest
         uint16_t v = 0;
         if (tab == 0 || (tab == 1 && alpha_ucn)) {
             const float w = (tab ? alpha_ucn : alpha)[(size_t)tt * E + row_ptr[row]];
-            const int q = q_mag5(m > qmax ? F5_BIG_U : m, w, step, inv, qmax);
+            const int q = q_mag5(m == nq - 1 ? F5_BIG_U : min(m, qmax), w, step, inv, qmax);
             v = (uint16_t)(((uint32_t)q & 0xFFu) | (((uint32_t)(-q) & 0xFFu) << 8));
         }
         qtab[f] = v;
@@ -197,7 +198,8 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     const Shape5& sh = kShapes5[p.shape];
     // weight tables (uniform row weights): only if they cost no workgroup slot per CU
     // per-iteration slices of the weight tables, double-buffered in LDS
-    const int qucn = g.M * (qmax + 2);
+    const int qrow = 3 * qmax + 2;
+    const int qucn = g.M * qrow;
     const int qslice = ((b.alpha_ucn ? 2 : 1) * qucn + 1) & ~1;
     bool lut = !per_edge_w && g.M < 256 && (qslice >> 1) <= 64 * p.nw &&
                getenv("LDPC_F5_NOLUT") == nullptr;
@@ -278,6 +280,7 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     a.qtab = qtab;
     a.qslice = qslice;
     a.qucn = qucn;
+    a.qrow = qrow;
     a.gad = gad;
     a.grow = grow;
     const int nblocks = (int)((b.B + sh.cw - 1) / sh.cw);

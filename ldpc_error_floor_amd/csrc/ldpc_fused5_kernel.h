@@ -81,7 +81,8 @@ struct F5Args {
     int Mp;            // proto rows
     const float* betas;        // [T][N] beta (the kernel keeps ch / step)
     const uint16_t* qtab;      // [T][qslice] weight tables (setup kernel), LUT builds only
-    int qslice;                // halfwords per iteration: [alpha | alpha_ucn][Mp][qmax+2], even
+    int qslice;                // halfwords per iteration: [alpha | alpha_ucn][Mp][qrow], even
+    int qrow;                  // halfwords per table row: 3 qmax + 2
     int qucn;                  // halfword offset of the alpha_ucn table inside a slice
     const uint32_t* gad;       // [ngroups][NPK][64] packed edge byte addresses (k_f5_gad)
     const uint4* grow;         // [ngroups] {r0 | deg << 16 | row << 24, lane-valid mask lo, hi, 0}
@@ -475,24 +476,28 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 }
             }
             // ---- new state: quantized minima, selector bytes, argmin bit ----
-            uint32_t nbit = 0;
+            uint32_t px = 0;                           // parity of the negative V->C signs
 #pragma unroll
             for (int w = 0; w < NSEL; ++w) {
                 NG[w] &= SL::bmask(w);                 // bit 0 of each byte: V->C sign negative
-                nbit += __popc(NG[w]);
+                px ^= NG[w];
             }
             // message sign = V->C sign XOR (count of positives odd): applied to P as a byte
             // swap inside each half; for PEW (P holds magnitudes) to the selector bytes
             if constexpr (UCN) syn = (syn >> 15) & 1u;
-            const bool podd = ((uint32_t)deg + nbit) & 1u;
+            const bool podd = ((uint32_t)__popc(px) + (uint32_t)deg) & 1u;
+            // argmin bit: the edge code is 8 * b + 1 for selector byte b (word b / 4), so one
+            // 64-bit shift places it inside the word pair b / 8
             const uint32_t code = c1 & 255u;
-            const uint32_t onebit = 1u << (code & 31u);
-            const uint32_t wsel = code >> 5;
+            const uint64_t onepair = 1ull << (code & 63u);
+            const uint32_t pairsel = code >> 6;
             const uint32_t pm = (PEW && podd) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
             for (int w = 0; w < NSEL; ++w)
-                if (w < GD::nsel(gi))
-                    SEL[gi][w] = (NG[w] ^ (pm & SL::bmask(w))) | ((wsel == (uint32_t)w) ? onebit : 0u);
+                if (w < GD::nsel(gi)) {
+                    const uint32_t ob = (w & 1) ? (uint32_t)(onepair >> 32) : (uint32_t)onepair;
+                    SEL[gi][w] = (NG[w] ^ (pm & SL::bmask(w))) | ((pairsel == (uint32_t)(w >> 1)) ? ob : 0u);
+                }
             const int m1 = min((int)(c1 >> 8), qmax);
             if constexpr (PEW) {
                 const uint32_t m2 = (deg < 2) ? 255u : (uint32_t)min((int)(c2 >> 8), qmax);
@@ -501,12 +506,20 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             } else {
                 uint32_t p;
                 if constexpr (LUT) {
-                    // [+m, -m] byte pairs of Q(relu(m*w)) for this iteration and proto row
-                    const int ib = (deg < 2) ? qmax + 1 : min((int)(c2 >> 8), qmax);
+                    // [+m, -m] byte pairs of Q(relu(m*w)) for this iteration and proto row,
+                    // indexed by the unclamped |V->C| (the table repeats Q(qmax) up to 3 qmax,
+                    // |Tv - m|'s bound); entry nq - 1 stands for "no other edge"
                     const int row = (int)((ri >> 24) & 0xFFu);
-                    const uint16_t* qt = QT + (t & 1) * a.qslice + ((UCN && syn) ? a.qucn : 0) +
-                                         row * (qmax + 2);
-                    p = (uint32_t)qt[m1] | ((uint32_t)qt[ib] << 16);
+                    const unsigned char* qt = reinterpret_cast<const unsigned char*>(
+                        QT + (t & 1) * a.qslice + ((UCN && syn) ? a.qucn : 0) + row * a.qrow);
+                    // byte offsets 2 |d| = key >> 7 (the code byte stays below 128 up to 16 edges)
+                    const uint32_t o1 = (MAXDEG <= 16) ? (c1 >> 7) : ((c1 >> 7) & ~1u);
+                    const uint32_t o2 = (deg < 2) ? 2u * (uint32_t)(a.qrow - 1)
+                                                  : ((MAXDEG <= 16) ? (c2 >> 7) : ((c2 >> 7) & 0x1FEu));
+                    const uint32_t qa = *reinterpret_cast<const uint16_t*>(qt + o1);
+                    const uint32_t qb = *reinterpret_cast<const uint16_t*>(qt + o2);
+                    // [+mA, -mA, +mB, -mB], halves swapped when the count of positives is odd
+                    p = __builtin_amdgcn_perm(qb, qa, podd ? 0x04050001u : 0x05040100u);
                 } else {
                     const int m2 = (deg < 2) ? F5_BIG_U : min((int)(c2 >> 8), qmax);
                     const float w = (UCN && syn) ? wu : wa;
@@ -515,8 +528,8 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     const uint32_t pa = ((uint32_t)mA & 0xFFu) | (((uint32_t)(-mA) & 0xFFu) << 8);
                     const uint32_t pb = ((uint32_t)mB & 0xFFu) | (((uint32_t)(-mB) & 0xFFu) << 8);
                     p = pa | (pb << 16);
+                    p = __builtin_amdgcn_perm(p, p, podd ? 0x02030001u : 0x03020100u);
                 }
-                p = __builtin_amdgcn_perm(p, p, podd ? 0x02030001u : 0x03020100u);
                 P[gi] = gval[gi] ? p : 0u;    // duplicate stand-in check: no messages
             }
         }
