@@ -20,6 +20,8 @@ struct ldpc_graph {
     DevGraph dev{};
     int T_w = 0;
     int per_edge_w = 0;        // CN weights differ inside a proto row (sharing 1/4)
+    std::vector<int32_t> row_merge;   // [M] DevGraph::h_row_merge
+    int32_t* d_row_merge = nullptr;
     float* d_alpha = nullptr;
     float* d_alpha_ucn = nullptr;
     float* d_beta = nullptr;
@@ -300,6 +302,7 @@ int ldpc_graph_destroy(ldpc_graph* g) {
     dev_free(g->d_alpha);
     dev_free(g->d_alpha_ucn);
     dev_free(g->d_beta);
+    dev_free(g->d_row_merge);
     delete g;
     return LDPC_OK;
 }
@@ -342,6 +345,28 @@ int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* 
                     break;
                 }
             }
+    // rows that may share check groups in the fused kernel: equal degree, uniform weights
+    // inside the row (no per-edge weights) and the previous row's CN / UCN weights at every t
+    g->row_merge.assign(g->M, 0);
+    for (int i = 1; i < g->M && !g->per_edge_w; ++i) {
+        bool same = g->row_ptr[i + 1] - g->row_ptr[i] == g->row_ptr[i] - g->row_ptr[i - 1];
+        for (int t = 0; t < T && same; ++t) {
+            const size_t a0 = (size_t)t * g->E + g->row_ptr[i - 1], a1 = (size_t)t * g->E + g->row_ptr[i];
+            same = alpha[a1] == alpha[a0] && (!alpha_ucn || alpha_ucn[a1] == alpha_ucn[a0]);
+        }
+        g->row_merge[i] = same ? 1 : 0;
+    }
+    g->dev.h_row_merge = nullptr;
+    g->dev.row_merge = nullptr;
+    if (!g->d_row_merge) {
+        const int st2 = dev_alloc(&g->d_row_merge, (size_t)g->M);
+        if (st2 != LDPC_OK) return st2;
+    }
+    if (hipMemcpy(g->d_row_merge, g->row_merge.data(), (size_t)g->M * sizeof(int32_t),
+                  hipMemcpyHostToDevice) != hipSuccess)
+        return LDPC_ERR_HIP;
+    g->dev.h_row_merge = g->row_merge.data();
+    g->dev.row_merge = g->d_row_merge;
     return LDPC_OK;
 }
 

@@ -38,54 +38,99 @@ __global__ void k_f5_tables(const float* __restrict__ alpha, const float* __rest
     }
 }
 
-// Edge addresses per (check group, lane): lane = slot * CW + cw serves circulant row
-// h = hg * SLOTS + slot of proto row i (grp = i * hstep + hg); edge k of that row reads
-// W[(pe_col * z + (h + shift) mod z) * CW + cw], packed as byte offsets two per word.  Lanes
-// with h >= z (last group of a row) point every edge at the lane's own dummy word (no two
-// lanes' pass-2 atomics on one LDS word) and are masked out of the results.
-//
-// Table position s is what wave s % nw runs as its group s / nw.  bal = 0: position s is group
-// s.  bal = 1 (graphs with very unequal row degrees): groups are ranked by row degree, heaviest
-// first, and dealt to the waves in snake order (round r left to right when r is even, right to
-// left when odd), so every wave's edge count is within one row's degree of the others'.
-__device__ int f5_group_of(int s, const int32_t* __restrict__ row_ptr, int M, int hstep,
-                           int ngroups, int nw, int bal) {
+// Check groups.  A run is a maximal range of consecutive proto rows that may share a group:
+// row i continues row i-1's run when merge[i] != 0 (equal degree and, every iteration, equal
+// CN / UCN weights: ldpc_weights_set).  A run's checks, row-major (z per row), are cut into
+// groups of SLOTS consecutive checks, so only a run's last group idles lanes (one row per run:
+// the last group of every row).  Groups are numbered run by run ("canonical" order).
+__host__ __device__ inline int f5_run_groups(int nrows, int z, int slots) {
+    return (nrows * z + slots - 1) / slots;
+}
+// f(first_row, nrows, degree) for every run, in row order; stops when f returns true
+template <class F>
+__host__ __device__ inline void f5_for_runs(const int32_t* row_ptr, const int32_t* merge, int M, F f) {
+    for (int i = 0; i < M;) {
+        int j = i + 1;
+        while (j < M && merge && merge[j]) ++j;
+        if (f(i, j - i, row_ptr[i + 1] - row_ptr[i])) return;
+        i = j;
+    }
+}
+inline int f5_ngroups(const int32_t* row_ptr, const int32_t* merge, int M, int z, int slots) {
+    int n = 0;
+    f5_for_runs(row_ptr, merge, M, [&](int, int nr, int) { n += f5_run_groups(nr, z, slots); return false; });
+    return n;
+}
+
+// Table position s is what wave s % nw runs as its group s / nw.  bal = 0: position s is
+// canonical group s.  bal = 1 (graphs with very unequal row degrees): groups are ranked by
+// degree, heaviest first (ties in row order), and dealt to the waves in snake order (round r
+// left to right when r is even, right to left when odd), so every wave's edge count is within
+// one row's degree of the others'.
+__device__ int f5_group_of(int s, const int32_t* __restrict__ row_ptr, const int32_t* merge, int M,
+                           int z, int slots, int ngroups, int nw, int bal) {
     if (!bal) return s;
     const int r = s / nw, w = s - r * nw;
     const int nr = min(nw, ngroups - r * nw);               // groups dealt in round r
     const int rank = r * nw + ((r & 1) ? nr - 1 - w : w);
-    // rank of group (i, hg) = hstep * #rows heavier than i (ties: lower row first) + hg
-    for (int i = 0; i < M; ++i) {
-        const int di = row_ptr[i + 1] - row_ptr[i];
-        int before = 0;
-        for (int i2 = 0; i2 < M; ++i2) {
-            const int d2 = row_ptr[i2 + 1] - row_ptr[i2];
-            before += (d2 > di || (d2 == di && i2 < i));
+    int canon = 0, res = s;
+    f5_for_runs(row_ptr, merge, M, [&](int i0, int n, int d) {
+        const int ng = f5_run_groups(n, z, slots);
+        int before = 0;                                     // groups ranked ahead of this run's
+        f5_for_runs(row_ptr, merge, M, [&](int j0, int m, int d2) {
+            if (d2 > d || (d2 == d && j0 < i0)) before += f5_run_groups(m, z, slots);
+            return false;
+        });
+        if (rank >= before && rank < before + ng) {
+            res = canon + (rank - before);
+            return true;
         }
-        if (rank >= before * hstep && rank < (before + 1) * hstep) return i * hstep + (rank - before * hstep);
-    }
-    return s;
+        canon += ng;
+        return false;
+    });
+    return res;
 }
 
+// Edge addresses per (table position, lane): lane = slot * CW + cw serves check c = off * SLOTS
+// + slot of its group's run (off: the group's index inside the run), i.e. circulant row h = c
+// mod z of proto row i = first + c / z; edge k of that row reads W[(pe_col * z + (h + shift) mod
+// z) * CW + cw], packed as byte offsets two per word.  Lanes past the run's last check point
+// every edge at the lane's own dummy word (no two lanes' pass-2 atomics on one LDS word) and are
+// masked out of the results.  grow: the run's first row (its weights stand for the run's),
+// degree and the lane-valid mask.
 __global__ void k_f5_gad(const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ pe_col,
-                         const int32_t* __restrict__ pe_shift, int M, int ngroups, int hstep, int z,
-                         int logcw, int maxdeg, int npk, int total, int nw, int bal, uint32_t* gad,
-                         uint4* grow) {
+                         const int32_t* __restrict__ pe_shift, const int32_t* __restrict__ merge,
+                         int M, int ngroups, int z, int logcw, int maxdeg, int npk, int total,
+                         int nw, int bal, uint32_t* gad, uint4* grow) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= ngroups * 64) return;
     const int grp = f >> 6, lane = f & 63;
     const int cwn = 1 << logcw, slots = 64 >> logcw;
     const int slot = lane >> logcw, cw = lane & (cwn - 1);
-    const int rg = f5_group_of(grp, row_ptr, M, hstep, ngroups, nw, bal);
-    const int i = rg / hstep, hg = rg - i * hstep;
-    const int r0 = row_ptr[i], deg = row_ptr[i + 1] - r0;
-    const int h = hg * slots + slot;
+    const int rg = f5_group_of(grp, row_ptr, merge, M, z, slots, ngroups, nw, bal);
+    int first = 0, nrows = 1, off = rg;
+    f5_for_runs(row_ptr, merge, M, [&](int i0, int n, int) {
+        const int ng = f5_run_groups(n, z, slots);
+        if (off < ng) {
+            first = i0;
+            nrows = n;
+            return true;
+        }
+        off -= ng;
+        return false;
+    });
+    const int deg = row_ptr[first + 1] - row_ptr[first];
+    const int c = off * slots + slot;
+    const bool valid = c < nrows * z;
+    const int i = first + (valid ? c / z : 0);
+    const int h = valid ? c - (c / z) * z : 0;
+    const int r0 = row_ptr[i];
     for (int p = 0; p < npk; ++p) {
         uint32_t word = 0;
         for (int j = 0; j < 2; ++j) {
             const int k = 2 * p + j;
             uint32_t byte = (uint32_t)(total + lane) * 4u;            // dummy word of this lane
-            if (h < z && k < deg && k < maxdeg) {
+            if (valid && k < deg && k < maxdeg) {
                 int hs = h + pe_shift[r0 + k];
                 hs = (hs >= z) ? hs - z : hs;
                 byte = (uint32_t)(((pe_col[r0 + k] * z + hs) << logcw) + cw) * 4u;
@@ -97,8 +142,9 @@ __global__ void k_f5_gad(const int32_t* __restrict__ row_ptr, const int32_t* __r
     if (lane == 0) {
         uint32_t lo = 0, hi = 0;
         for (int l = 0; l < 64; ++l)
-            if (hg * slots + (l >> logcw) < z) (l < 32 ? lo : hi) |= 1u << (l & 31);
-        grow[grp] = make_uint4((uint32_t)r0 | ((uint32_t)deg << 16) | ((uint32_t)i << 24), lo, hi, 0u);
+            if (off * slots + (l >> logcw) < nrows * z) (l < 32 ? lo : hi) |= 1u << (l & 31);
+        grow[grp] = make_uint4((uint32_t)row_ptr[first] | ((uint32_t)deg << 16) | ((uint32_t)first << 24),
+                               lo, hi, 0u);
     }
 }
 
@@ -109,7 +155,8 @@ size_t f5_lds(int nv, int cw, int T, int N) {
 }
 
 struct Plan5 {
-    int shape = -1, nw = 0, hstep = 0, ngroups = 0;
+    int shape = -1, nw = 0, ngroups = 0;
+    const int32_t* merge = nullptr;      // device row-merge flags used (null: one row per run)
     size_t lds = 0;
 };
 
@@ -118,20 +165,28 @@ Plan5 plan5(const DevGraph& g, int T) {
     double best_score = 0;
     const char* force = getenv("LDPC_F5_SHAPE");
     const int forced = force ? atoi(force) : -1;
+    const char* me = getenv("LDPC_F5_MERGE");            // 0: one proto row per run (A/B runs)
+    const bool use_merge = g.h_row_merge && g.row_merge && !(me && atoi(me) == 0);
+    const int32_t* hm = use_merge ? g.h_row_merge : nullptr;
     for (int si = 0; si < (int)(sizeof(kShapes5) / sizeof(kShapes5[0])); ++si) {
         const Shape5& sh = kShapes5[si];
         if (forced >= 0 ? si != forced : !sh.autosel) continue;
         if ((g.z == 1) != (sh.cw == 64)) continue;
         if (g.max_cdeg > sh.maxdeg) continue;
         const int slots = 64 / sh.cw;
-        const int hstep = (g.z + slots - 1) / slots;
-        const int ngroups = g.M * hstep;
-        const int nw = (ngroups + sh.maxg - 1) / sh.maxg;
-        if (nw > 16 || nw < 1) continue;
-        if (sh.hg > 0 && sh.hg < sh.maxg) {      // rows too heavy for a light slot must fit the heavy ones
+        const int ngroups = f5_ngroups(g.h_row_ptr, hm, g.M, g.z, slots);
+        // waves: enough for MAXG groups each, rounded up to a multiple of 4 (a workgroup's
+        // busiest SIMD holds ceil(nw / 4) waves either way; the extra waves share the VN phase)
+        const int nw0 = (ngroups + sh.maxg - 1) / sh.maxg;
+        const int nw = std::min(16, (nw0 + 3) & ~3);
+        if (nw * sh.maxg < ngroups || nw < 1) continue;
+        if (sh.hg > 0 && sh.hg < sh.maxg) {      // groups too heavy for a light slot must fit the heavy ones
             int heavy = 0;
-            for (int i = 0; i < g.M; ++i) heavy += (g.h_row_ptr[i + 1] - g.h_row_ptr[i] > sh.ldeg);
-            if (heavy * hstep > sh.hg * nw) continue;
+            f5_for_runs(g.h_row_ptr, hm, g.M, [&](int, int n, int d) {
+                heavy += (d > sh.ldeg) ? f5_run_groups(n, g.z, slots) : 0;
+                return false;
+            });
+            if (heavy > sh.hg * nw) continue;
         }
         if (g.N > 64 * nw) continue;                                    // beta slice copy
         const size_t lds = f5_lds(g.n_vars, sh.cw, T, g.N);
@@ -146,13 +201,13 @@ Plan5 plan5(const DevGraph& g, int T) {
         const int wg_waves = wpe / ((nw + 3) / 4);
         const int wgs = std::max(1, std::min(wg_lds, wg_waves));
         const double eff = (double)g.max_cdeg / (double)(((g.max_cdeg + 7) / 8) * 8);
-        const double util = (double)g.z / (double)(hstep * slots);    // lanes on real checks
-        const double score = (double)std::min(wgs * nw, 24) * eff * util + 1e-3 * sh.cw;
+        const double util = (double)(g.M * g.z) / (double)(ngroups * slots);    // lanes on real checks
+        const double score = (double)std::min(wgs * nw0, 24) * eff * util + 1e-3 * sh.cw;
         if (score > best_score) {
             best_score = score;
             best.shape = si;
             best.nw = nw;
-            best.hstep = hstep;
+            best.merge = use_merge ? g.row_merge : nullptr;
             best.ngroups = ngroups;
             best.lds = lds;
         }
@@ -230,7 +285,6 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     a.N = g.N;
     a.E = g.E;
     a.z = g.z;
-    a.hstep = p.hstep;
     a.ngroups = p.ngroups;
     a.nent = (g.n_vars * sh.cw + 64 * p.nw - 1) / (64 * p.nw);
     a.nfull = g.n_vars * sh.cw / 64;
@@ -272,7 +326,7 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
         const bool hetero = sh.hg > 0 && sh.hg < sh.maxg;
         const bool bal = hetero || (be ? atoi(be) != 0 : sh.bal);
         hipLaunchKernelGGL(k_f5_gad, dim3((unsigned)((p.ngroups * 64 + 255) / 256)), dim3(256), 0, s,
-                           g.row_ptr, g.pe_col, g.pe_shift, g.M, p.ngroups, p.hstep, g.z, lcw,
+                           g.row_ptr, g.pe_col, g.pe_shift, p.merge, g.M, p.ngroups, g.z, lcw,
                            sh.maxdeg, npk, g.n_vars * sh.cw, p.nw, bal ? 1 : 0, gad, grow);
         if (hipGetLastError() != hipSuccess) return LDPC_ERR_HIP;
     }

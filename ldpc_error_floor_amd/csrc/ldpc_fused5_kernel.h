@@ -76,7 +76,7 @@ struct F5Args {
     int ntiles, T, target_bits, clip_u, qmax;
     float inv, step;
     int n_vars, N, E, z;
-    int hstep, ngroups, nent;
+    int ngroups, nent;
     int nfull, cpw;    // VN: full 64-entry chunks, chunks per wave
     int Mp;            // proto rows
     const float* betas;        // [T][N] beta (the kernel keeps ch / step)

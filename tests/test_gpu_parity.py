@@ -153,12 +153,15 @@ def test_fused5_every_shape_bit_exact(shape, cuda_device, monkeypatch):
     assert ran, f"no fixture fits fused5 shape {F5_SHAPES[shape]}"
 
 
+@pytest.mark.parametrize("merge", ["0", "1"])
 @pytest.mark.parametrize("balance", ["0", "1"])
-def test_fused5_group_dealing_bit_exact(balance, cuda_device, monkeypatch):
-    """k_f5_gad's two group-to-wave mappings (identity, degree-ranked snake) on every exact
-    QMS fixture with the automatically chosen shape."""
+def test_fused5_group_dealing_bit_exact(balance, merge, cuda_device, monkeypatch):
+    """k_f5_gad's group construction (one proto row per run, or runs of equal-degree,
+    equal-weight rows sharing groups) and its two group-to-wave mappings (identity,
+    degree-ranked snake) on every exact QMS fixture with the automatically chosen shape."""
     from ldpc_error_floor_amd.decoder import NMSDecoder
     monkeypatch.setenv("LDPC_F5_BALANCE", balance)
+    monkeypatch.setenv("LDPC_F5_MERGE", merge)
     ran = 0
     for name in DECODER_CASES:
         c = load_case(name)
