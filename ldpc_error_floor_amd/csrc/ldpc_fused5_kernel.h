@@ -9,20 +9,21 @@
 // compressed min-sum state is held and decoded, which sets the VALU count per edge:
 //
 //  * P   — one VGPR holding the check's four possible output messages as signed bytes
-//          [+mA, -mA, +mB, -mB] (mA: min over all edges, mB: second minimum, both already
+//          [-mA, +mA, -mB, +mB] (mA: min over all edges, mB: second minimum, both already
 //          weighted and quantized, in grid units);
-//  * SEL — one selector byte per edge, four edges per VGPR: byte = 2*is_argmin + negative,
+//  * SEL — one selector byte per edge, four edges per VGPR: byte = 2*is_argmin + (v2c >= 0),
 //          the index of the edge's message inside P.  v_perm_b32(P, P, SEL[w]) yields four
 //          edges' messages, and pass 1 subtracts a message straight from its byte with an
 //          SDWA sign-extended source: a quarter op per edge to decode (v3: 5 ops).
 //  * pass 1 folds V->C magnitudes with one v_min + one v_med3 per edge (running first/second
-//    minimum of key = |v2c| << 8 | edge code), and the V->C signs with one v_alignbit per
-//    edge, which appends the top byte of v2c (8 copies of its sign) to a SEL-shaped word;
+//    minimum of key = |v2c| << 8 | edge code, |v2c| from the offset-binary difference with one
+//    v_sad_u16), and the V->C signs with one v_alignbit per edge, which appends the top byte of
+//    the difference (8 copies of "v2c >= 0") to a SEL-shaped word;
 //    the quantizer clamp moves after the minimum (clamp is monotonic);
-//  * W[v][cw] = Tv (bits 31..16, signed) | hd (bit 15) | S + 2^14 (bits 14..0): pass 1 reads Tv
-//    with an SDWA sign-extended word select, pass 2 adds the message without a shift;
-//  * an edge slot past a check's degree points at a per-codeword dummy word whose Tv is
-//    +16383: its |v2c| never wins a minimum, its sign is positive, its hd bit is 0, and pass 2
+//  * W[v][cw] = Tv + 128 (bits 31..16) | hd (bit 15) | S + 2^14 (bits 14..0): pass 1 reads Tv
+//    with an SDWA word select, pass 2 adds the message without a shift;
+//  * an edge slot past a check's degree points at a per-lane dummy word whose Tv is -96: its
+//    |v2c| never wins a minimum, its sign is negative (not counted), its hd bit is 0, and pass 2
 //    adds into it harmlessly (the VN phase resets it), so partial chunks need no masks.
 //
 // Per-edge weights (sharing types with one weight per edge) keep raw minima in P (16 bit
@@ -44,17 +45,21 @@ namespace f5 {
 constexpr int F5_BIG_U = 1023;               // "no other edge": value 10000 (Main_Functions.py:248)
 constexpr size_t F5_LDS_MAX = 160 * 1024;
 constexpr uint32_t F5_SBIAS = 16384;         // S field bias (bits 14..0)
-// padding edges read this word: Tv = 96 gives a V->C value in [65, 127] for any message
-// (|m| <= 31), positive, never below qmax and inside the 8-bit range pass 1 works in
-constexpr uint32_t F5_DUMMY_W = (96u << 16) | F5_SBIAS;
+// W's Tv field holds Tv + F5_TVB: pass 1's byte subtract then yields V->C + 128 in offset
+// binary, whose distance from 128 (one v_sad_u16) is |V->C| and whose top bit is "V->C >= 0"
+constexpr int F5_TVB = 128;
+// padding edges read this word: Tv = -96 gives a V->C value in [-127, -65] for any message
+// (|m| <= 31): negative (absent from the count of positive signs), never below qmax and inside
+// the 8-bit range pass 1 works in
+constexpr uint32_t F5_DUMMY_W = ((uint32_t)(F5_TVB - 96) << 16) | F5_SBIAS;
 // one dummy word per lane (after W): padding slots of different lanes never add into the same
 // LDS word, so their pass-2 atomics do not serialise
 constexpr int F5_NDUMMY = 64;
 constexpr float F5_MAGIC = 12582912.0f;                 // 1.5 * 2^23
 constexpr int F5_MAGIC_BITS = 0x4B400000;              // bit pattern of F5_MAGIC
 constexpr int F5_APP0 = F5_MAGIC_BITS + (int)F5_SBIAS;  // APP == 0 in the VN's biased domain
-// (Tv + F5_APP0) * 2^16 + F5_WBIAS == (Tv << 16) | F5_SBIAS  (mod 2^32)
-constexpr uint32_t F5_WBIAS = F5_SBIAS - (uint32_t)F5_APP0 * 65536u;
+// (Tv + F5_APP0) * 2^16 + F5_WBIAS == ((Tv + F5_TVB) << 16) | F5_SBIAS  (mod 2^32)
+constexpr uint32_t F5_WBIAS = F5_SBIAS + (uint32_t)F5_TVB * 65536u - (uint32_t)F5_APP0 * 65536u;
 // APP path magic: 1.5 * 2^23 + 2^22 - S bias, same binade, so Q(y) + APP bits land at
 // F5_APPH + APP with F5_APPH = 0x4B800000: APP >= 0 exactly when bit 23 is set (an OR over
 // entries then answers "any hard decision 1")
@@ -111,11 +116,6 @@ __device__ __forceinline__ int q_mag5(int m, float w, float step, float inv, int
 // 16-bit VOP2 forms: full issue rate on gfx950 where the 32-bit min / max / shift-left and
 // every SDWA / VOP3 form take twice the cycles (tools/valu_table.hip); the high half of the
 // result is zeroed.
-__device__ __forceinline__ uint32_t max_i16(uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_max_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
 __device__ __forceinline__ uint32_t min_u16(uint32_t a, uint32_t b) {
     uint32_t r;
     asm("v_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -134,22 +134,23 @@ __device__ __forceinline__ uint32_t hi16(uint32_t x) {
     asm("v_lshrrev_b32 %0, 16, %1" : "=v"(r) : "v"(x));
     return r;
 }
-// (Tv - m) * 256 sign-extended: Tv = signed high half of the W word, m = signed byte POS of r.
-// Exact while |Tv - m| <= 127 (Tv is kept within +-2 qmax, |m| <= qmax <= 31).
+// d256 = (Tv + 128 - m mod 256) << 8, bits 31..16 zero: V->C in offset binary in byte 1, whose
+// bit 7 (bit 15) is "Tv - m >= 0"; the high half of the W word holds Tv + F5_TVB, m = signed
+// byte POS of r.  Exact while |Tv - m| <= 127 (Tv is kept within +-2 qmax, |m| <= qmax <= 31).
 template <int POS>
 __device__ __forceinline__ uint32_t sub_d256(uint32_t w, uint32_t r) {
     uint32_t d;
     if constexpr (POS == 0)
-        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_0"
+        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:BYTE_0"
             : "=v"(d) : "v"(w), "v"(r));
     else if constexpr (POS == 1)
-        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_1"
+        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:BYTE_1"
             : "=v"(d) : "v"(w), "v"(r));
     else if constexpr (POS == 2)
-        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_2"
+        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:BYTE_2"
             : "=v"(d) : "v"(w), "v"(r));
     else
-        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_3"
+        asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:BYTE_1 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:BYTE_3"
             : "=v"(d) : "v"(w), "v"(r));
     return d;
 }
@@ -161,6 +162,16 @@ __device__ __forceinline__ uint32_t clamp_i16(uint32_t a, uint32_t lo, uint32_t 
     asm("v_min_i16 %0, %1, %2" : "=v"(r) : "s"(hi), "v"(r));
     return r;
 }
+// key = |V->C| << 8 | code = |d256 - 0x8000| + code.  (v_sad_u16 sums the absolute differences
+// of BOTH 16-bit halves, tools/probe/sad_probe.hip: d256's high half is zero, and so is ksad's.)
+__device__ __forceinline__ uint32_t key_sad(uint32_t d256, uint32_t ksad, uint32_t code) {
+    return __builtin_amdgcn_sad_u16(d256, ksad, code);
+}
+// NG << 8 | byte 1 of d: appends an edge's offset-binary V->C byte to a selector-shaped word
+__device__ __forceinline__ uint32_t append_b1(uint32_t ng, uint32_t d) {
+    return __builtin_amdgcn_perm(ng, d, 0x06050401u);
+}
+
 __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t r;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -168,7 +179,7 @@ __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // ---- SEL layout: edge k -> byte of word k/4, counted from the last inserted edge ------------
-// A selector byte is 2*is_argmin + negative: the index of the edge's message inside P, so
+// A selector byte is 2*is_argmin + (V->C >= 0): the index of the edge's message inside P, so
 // v_perm_b32(P, P, SEL[w]) yields the messages of four edges at once.
 template <int MAXDEG>
 struct Sel {
@@ -285,7 +296,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         for (int e = tid; e < total; e += NT) {
             const uint32_t v = (uint32_t)e >> LOGCW;
             const int t0 = q_scaled5(CH[e] * BETA[__umulhi(v, a.zmagic)], (float)qmax);  // lw_0
-            W[e] = ((uint32_t)t0 << 16) | ((uint32_t)(t0 >= 0) << 15) | F5_SBIAS;     // hd_{-1}
+            W[e] = ((uint32_t)(t0 + F5_TVB) << 16) | ((uint32_t)(t0 >= 0) << 15) | F5_SBIAS;   // hd_{-1}
         }
         if (tid < F5_NDUMMY) W[total + tid] = F5_DUMMY_W;
     }
@@ -316,6 +327,9 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     __syncthreads();
 
     F5_STAMP(2);
+    // v_sad_u16's second operand (VOP3 takes no literal; one opaque VGPR, not rematerialised)
+    uint32_t ksad;
+    asm volatile("v_mov_b32 %0, 0x8000" : "=v"(ksad));
     // check state: P (messages / raw minima), SEL (per-edge fields), ucn (syndrome, PEW only)
     uint32_t P[MAXG], SEL[MAXG][NSEL];
     int UC[MAXG];
@@ -435,15 +449,15 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     if (k < GD::deg(gi)) {
                         const uint32_t d256 = dd[j];
                         // key = |d| << 8 | code, all in the low 16 bits
-                        const uint32_t key = max_i16(d256, 0u - d256) | SL::code(k);
-                        // append the byte of sign copies of d to the edge's selector word
-                        NG[k / 4] = __builtin_amdgcn_alignbit(NG[k / 4], d256, 24);
+                        const uint32_t key = key_sad(d256, ksad, SL::code(k));
+                        // append the offset-binary V->C byte (bit 7: d >= 0) to the selector word
+                        NG[k / 4] = append_b1(NG[k / 4], d256);
                         const uint32_t o1 = c1;
                         c1 = min_u16(o1, key);
                         c2 = med3u(o1, c2, key);
                     }
                 }
-                // absent slots of the chunk enter as positive (zero) sign bytes
+                // absent slots of the chunk enter as zero bytes (not counted as positive)
 #pragma unroll
                 for (int w = 0; w < NSEL; ++w) {
                     int n = 0;
@@ -467,7 +481,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 else if (CW <= 8 && n == 1) chunk1(c8, std::integral_constant<int, 1>{});
                 else if (n > 0) chunk1(c8, std::integral_constant<int, 8>{});
                 else {
-                    // chunk skipped (deg <= c8): its edges enter as positive (zero) sign fields
+                    // chunk skipped (deg <= c8): its edges enter as zero bytes
 #pragma unroll
                     for (int w = 0; w < NSEL; ++w) {
                         const int nn = SL::in_chunk(w, c8);
@@ -476,22 +490,23 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 }
             }
             // ---- new state: quantized minima, selector bytes, argmin bit ----
-            uint32_t px = 0;                           // parity of the negative V->C signs
+            uint32_t px = 0;                           // parity of the V->C >= 0 flags
 #pragma unroll
             for (int w = 0; w < NSEL; ++w) {
-                NG[w] &= SL::bmask(w);                 // bit 0 of each byte: V->C sign negative
+                NG[w] = (NG[w] >> 7) & SL::bmask(w);   // bit 0 of each byte: V->C >= 0
                 px ^= NG[w];
             }
             // message sign = V->C sign XOR (count of positives odd): applied to P as a byte
-            // swap inside each half; for PEW (P holds magnitudes) to the selector bytes
+            // swap inside each half; for PEW (P holds magnitudes) to the selector bytes, whose
+            // bit 0 then means "negative message" (V->C >= 0 XOR count even)
             if constexpr (UCN) syn = (syn >> 15) & 1u;
-            const bool podd = ((uint32_t)__popc(px) + (uint32_t)deg) & 1u;
+            const bool podd = (uint32_t)__popc(px) & 1u;
             // argmin bit: the edge code is 8 * b + 1 for selector byte b (word b / 4), so one
             // 64-bit shift places it inside the word pair b / 8
             const uint32_t code = c1 & 255u;
             const uint64_t onepair = 1ull << (code & 63u);
             const uint32_t pairsel = code >> 6;
-            const uint32_t pm = (PEW && podd) ? 0xFFFFFFFFu : 0u;
+            const uint32_t pm = (PEW && !podd) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
             for (int w = 0; w < NSEL; ++w)
                 if (w < GD::nsel(gi)) {
@@ -518,8 +533,9 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                                                   : ((MAXDEG <= 16) ? (c2 >> 7) : ((c2 >> 7) & 0x1FEu));
                     const uint32_t qa = *reinterpret_cast<const uint16_t*>(qt + o1);
                     const uint32_t qb = *reinterpret_cast<const uint16_t*>(qt + o2);
-                    // [+mA, -mA, +mB, -mB], halves swapped when the count of positives is odd
-                    p = __builtin_amdgcn_perm(qb, qa, podd ? 0x04050001u : 0x05040100u);
+                    // [-mA, +mA, -mB, +mB] (index 2 is_argmin + (V->C >= 0)), halves swapped
+                    // when the count of positives is odd
+                    p = __builtin_amdgcn_perm(qb, qa, podd ? 0x05040100u : 0x04050001u);
                 } else {
                     const int m2 = (deg < 2) ? F5_BIG_U : min((int)(c2 >> 8), qmax);
                     const float w = (UCN && syn) ? wu : wa;
@@ -528,7 +544,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     const uint32_t pa = ((uint32_t)mA & 0xFFu) | (((uint32_t)(-mA) & 0xFFu) << 8);
                     const uint32_t pb = ((uint32_t)mB & 0xFFu) | (((uint32_t)(-mB) & 0xFFu) << 8);
                     p = pa | (pb << 16);
-                    p = __builtin_amdgcn_perm(p, p, podd ? 0x02030001u : 0x03020100u);
+                    p = __builtin_amdgcn_perm(p, p, podd ? 0x03020100u : 0x02030001u);
                 }
                 P[gi] = gval[gi] ? p : 0u;    // duplicate stand-in check: no messages
             }
@@ -695,7 +711,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     if (!last) {
                         const int tn = min(max(q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], qmf) + s + sb,
                                                -2 * qmax), 2 * qmax);
-                        W[e] = ((uint32_t)tn << 16) | (((uint32_t)~app >> 16) & 0x8000u) | F5_SBIAS;
+                        W[e] = ((uint32_t)(tn + F5_TVB) << 16) | (((uint32_t)~app >> 16) & 0x8000u) | F5_SBIAS;
                     } else {
                         nbits += (uint32_t)(appt >= 0 && appt != INT_MIN) & (uint32_t)cvalid;
                     }
@@ -716,7 +732,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 if (!last) {
                     const int tn = min(max(q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], (float)qmax) + S,
                                            -2 * qmax), 2 * qmax);
-                    W[e] = ((uint32_t)tn << 16) | ((uint32_t)(app >= 0) << 15) | F5_SBIAS;
+                    W[e] = ((uint32_t)(tn + F5_TVB) << 16) | ((uint32_t)(app >= 0) << 15) | F5_SBIAS;
                 }
                 if ((int)v < a.target_bits) {
                     any_hd |= (uint32_t)(app >= 0);

@@ -109,6 +109,14 @@ __global__ void __launch_bounds__(256) k_mix(uint32_t* out, uint32_t seed, unsig
         else if (MIX == 83) asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(8)" : "+v"(a[j]) : "v"(b[j] * 4u + (threadIdx.x & 63u) * 64u));
         else if (MIX == 84) asm volatile("ds_read_u16_d16_hi %0, %1\n s_waitcnt lgkmcnt(8)" : "+v"(a[j]) : "v"(b[j] * 4u + (threadIdx.x & 63u) * 64u));
         else if (MIX == 85) asm volatile("ds_add_u32 %1, %0\n s_waitcnt lgkmcnt(8)" : "+v"(a[j]) : "v"(b[j] * 4u + (threadIdx.x & 63u) * 64u));
+        else if (MIX == 86) asm volatile("v_sad_u16 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+        else if (MIX == 87) asm volatile("v_med3_u16 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+        else if (MIX == 88) asm volatile("v_sad_u8 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+        else if (MIX == 89) asm volatile("v_sad_u16 %0, %0, %1, 17" : "+v"(a[j]) : "v"(b[j]));
+        else if (MIX == 90) asm volatile("v_max3_u32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+        else if (MIX == 91) asm volatile("v_med3_i16 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+        else if (MIX == 92) asm volatile("v_sub_u32_sdwa %0, sext(%0), sext(%1) dst_sel:BYTE_1 dst_unused:UNUSED_SEXT src0_sel:WORD_1 src1_sel:BYTE_2" : "+v"(a[j]) : "v"(b[j]));
+        else if (MIX == 93) asm volatile("v_msad_u8 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -228,6 +236,14 @@ int main() {
     run<83>("ds_read_b32", ncu, d);
     run<84>("ds_read_u16_d16_hi", ncu, d);
     run<85>("ds_add_u32", ncu, d);
+    run<86>("v_sad_u16", ncu, d);
+    run<87>("v_med3_u16", ncu, d);
+    run<88>("v_sad_u8", ncu, d);
+    run<89>("v_sad_u16 inl", ncu, d);
+    run<90>("v_max3_u32", ncu, d);
+    run<91>("v_med3_i16", ncu, d);
+    run<92>("v_sub_u32_sdwa byte", ncu, d);
+    run<93>("v_msad_u8", ncu, d);
     hipFree(d);
     return 0;
 }
