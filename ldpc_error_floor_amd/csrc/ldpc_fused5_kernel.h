@@ -14,11 +14,12 @@
 //  * SEL — one selector byte per edge, four edges per VGPR: byte = 2*is_argmin + (v2c >= 0),
 //          the index of the edge's message inside P.  v_perm_b32(P, P, SEL[w]) yields four
 //          edges' messages, and pass 1 subtracts a message straight from its byte with an
-//          SDWA sign-extended source: a quarter op per edge to decode (v3: 5 ops).
+//          SDWA sign-extended source: a quarter op per edge to decode (v3: 5 ops);
+//  * pass 2 (scatter) of a group runs right after its state update (F5_P2_MODE).
 //  * pass 1 folds V->C magnitudes with one v_min + one v_med3 per edge (running first/second
 //    minimum of key = |v2c| << 8 | edge code, |v2c| from the offset-binary difference with one
-//    v_sad_u16), and the V->C signs with one v_alignbit per edge, which appends the top byte of
-//    the difference (8 copies of "v2c >= 0") to a SEL-shaped word;
+//    v_sad_u16), and the V->C signs with one v_perm per edge, which appends the offset-binary
+//    byte (bit 7: "v2c >= 0") to a SEL-shaped word;
 //    the quantizer clamp moves after the minimum (clamp is monotonic);
 //  * W[v][cw] = Tv + 128 (bits 31..16) | hd (bit 15) | S + 2^14 (bits 14..0): pass 1 reads Tv
 //    with an SDWA word select, pass 2 adds the message without a shift;
@@ -42,6 +43,12 @@ namespace ldpc {
 
 namespace f5 {
 
+// pass-2 placement: 0 = every group's pass 1 + state, then every group's scatter; 1 = each
+// group's scatter right after its state update (pass-1 reads of Tv are unaffected by the
+// scatter's adds into the biased S field, so the order is free)
+#ifndef F5_P2_MODE
+#define F5_P2_MODE 1
+#endif
 constexpr int F5_BIG_U = 1023;               // "no other edge": value 10000 (Main_Functions.py:248)
 constexpr size_t F5_LDS_MAX = 160 * 1024;
 constexpr uint32_t F5_SBIAS = 16384;         // S field bias (bits 14..0)
@@ -380,6 +387,46 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         if (bcopy) bload = a.betas[(size_t)(t + 1) * a.N + tid];
         const float* atp = alpha + (size_t)(t > 0 ? t - 1 : 0) * a.E;
         const float* aup = UCN ? alpha_ucn + (size_t)(t > 0 ? t - 1 : 0) * a.E : nullptr;
+        // ======== check nodes: pass 2 (scatter C->V into S), one group ======================
+        auto pass2g = [&](const int gi) __attribute__((always_inline)) {
+            const int grp = wave + gi * NWV;
+            if (grp >= a.ngroups) return;
+            if (a.ablate & 2) return;
+            const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
+            const int r0 = (int)(ri & 0xFFFFu);
+            const int deg = (int)((ri >> 16) & 0xFFu);
+            // whole 8-edge chunks, padding slots adding into the lane's dummy word (exact 6- and
+            // 7-edge chunks measured 2.5% slower on wman (CW 16) and 4% slower on 5G BG2 (CW 8));
+            // CW 4 (5G BG1, degrees 3..19, a third of the slots would be padding): exact chunks
+            auto chunk2 = [&](const int c8, auto ne) __attribute__((always_inline)) {
+                constexpr int NE = decltype(ne)::value;
+                const uint32_t R0 = perm_word(gi, c8 / 4);
+                const uint32_t R1 = (NE > 4) ? perm_word(gi, c8 / 4 + 1) : 0u;
+#pragma unroll
+                for (int j = 0; j < NE; ++j) {
+                    const int k = c8 + j;
+                    if (k < GD::deg(gi)) {
+                        const uint32_t pk = gad[gi][k >> 1];
+                        const uint32_t addr = (k & 1) ? hi16(pk) : lo16(pk);
+                        const int c = msg(gi, k, j < 4 ? R0 : R1, at, au, r0);
+                        __atomic_fetch_add(reinterpret_cast<LdsU32*>(addr), (uint32_t)c, __ATOMIC_RELAXED);
+                    }
+                }
+            };
+            using N8 = std::integral_constant<int, 8>;
+#pragma unroll
+            for (int c8 = 0; c8 < GD::deg(gi); c8 += 8) {
+                const int n = deg - c8;
+                if (CW > 4 || n >= 8) { if (n > 0) chunk2(c8, N8{}); }
+                else if (n == 7) chunk2(c8, std::integral_constant<int, 7>{});
+                else if (n == 6) chunk2(c8, std::integral_constant<int, 6>{});
+                else if (n == 5) chunk2(c8, std::integral_constant<int, 5>{});
+                else if (n == 4) chunk2(c8, std::integral_constant<int, 4>{});
+                else if (n == 3) chunk2(c8, std::integral_constant<int, 3>{});
+                else if (n == 2) chunk2(c8, std::integral_constant<int, 2>{});
+                else if (n == 1) chunk2(c8, std::integral_constant<int, 1>{});
+            }
+        };
         // ======== check nodes: pass 1 (read Tv, fold minima and signs) + new state ==========
 #pragma unroll
         for (int gi = 0; gi < MAXG; ++gi) {
@@ -548,48 +595,12 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 }
                 P[gi] = gval[gi] ? p : 0u;    // duplicate stand-in check: no messages
             }
+            if constexpr (F5_P2_MODE == 1) pass2g(gi);     // this group's scatter right away
         }
         if (t == 0) F5_STAMP(5);
-        // ======== check nodes: pass 2 (scatter C->V into S) =================================
+        if constexpr (F5_P2_MODE == 0) {
 #pragma unroll
-        for (int gi = 0; gi < MAXG; ++gi) {
-            const int grp = wave + gi * NWV;
-            if (grp >= a.ngroups) break;
-            if (a.ablate & 2) continue;
-            const uint32_t ri = __builtin_amdgcn_readfirstlane(grow[gi]);
-            const int r0 = (int)(ri & 0xFFFFu);
-            const int deg = (int)((ri >> 16) & 0xFFu);
-            // whole 8-edge chunks, padding slots adding into the lane's dummy word (exact 6- and
-            // 7-edge chunks measured 2.5% slower on wman (CW 16) and 4% slower on 5G BG2 (CW 8));
-            // CW 4 (5G BG1, degrees 3..19, a third of the slots would be padding): exact chunks
-            auto chunk2 = [&](const int c8, auto ne) __attribute__((always_inline)) {
-                constexpr int NE = decltype(ne)::value;
-                const uint32_t R0 = perm_word(gi, c8 / 4);
-                const uint32_t R1 = (NE > 4) ? perm_word(gi, c8 / 4 + 1) : 0u;
-#pragma unroll
-                for (int j = 0; j < NE; ++j) {
-                    const int k = c8 + j;
-                    if (k < GD::deg(gi)) {
-                        const uint32_t pk = gad[gi][k >> 1];
-                        const uint32_t addr = (k & 1) ? hi16(pk) : lo16(pk);
-                        const int c = msg(gi, k, j < 4 ? R0 : R1, at, au, r0);
-                        __atomic_fetch_add(reinterpret_cast<LdsU32*>(addr), (uint32_t)c, __ATOMIC_RELAXED);
-                    }
-                }
-            };
-            using N8 = std::integral_constant<int, 8>;
-#pragma unroll
-            for (int c8 = 0; c8 < GD::deg(gi); c8 += 8) {
-                const int n = deg - c8;
-                if (CW > 4 || n >= 8) { if (n > 0) chunk2(c8, N8{}); }
-                else if (n == 7) chunk2(c8, std::integral_constant<int, 7>{});
-                else if (n == 6) chunk2(c8, std::integral_constant<int, 6>{});
-                else if (n == 5) chunk2(c8, std::integral_constant<int, 5>{});
-                else if (n == 4) chunk2(c8, std::integral_constant<int, 4>{});
-                else if (n == 3) chunk2(c8, std::integral_constant<int, 3>{});
-                else if (n == 2) chunk2(c8, std::integral_constant<int, 2>{});
-                else if (n == 1) chunk2(c8, std::integral_constant<int, 1>{});
-            }
+            for (int gi = 0; gi < MAXG; ++gi) pass2g(gi);
         }
         if (bcopy) BETA[((t + 1) & 1) * a.N + tid] = bload;
         __syncthreads();
