@@ -309,15 +309,13 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     }
 
     F5_STAMP(1);
-    // ---- per-group edge addresses (bytes, 16-bit packed), row info, lane validity ----------
+    // ---- per-group edge addresses (bytes, 16-bit packed) and row info ----------------------
     // (built once per decode by k_f5_gad; one coalesced load per packed word)
     uint32_t gad[MAXG][NPK];
     uint32_t grow[MAXG];
-    bool gval[MAXG];
 #pragma unroll
     for (int gi = 0; gi < MAXG; ++gi) {
         grow[gi] = 0;
-        gval[gi] = false;
 #pragma unroll
         for (int p = 0; p < NPK; ++p) gad[gi][p] = 0;
         const int grp = wave + gi * NWV;
@@ -326,9 +324,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
 #pragma unroll
             for (int p = 0; p < NPK; ++p)
                 if (p < GD::npk(gi)) gad[gi][p] = gt[p * 64];
-            const uint4 r = a.grow[grp];
-            grow[gi] = r.x;
-            gval[gi] = (((lane < 32) ? r.y : r.z) >> (lane & 31)) & 1u;
+            grow[gi] = __builtin_amdgcn_readfirstlane(a.grow[grp].x);   // wave-uniform: an SGPR
         }
     }
     __syncthreads();
@@ -564,7 +560,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             if constexpr (PEW) {
                 const uint32_t m2 = (deg < 2) ? 255u : (uint32_t)min((int)(c2 >> 8), qmax);
                 UC[gi] = (int)syn;
-                P[gi] = gval[gi] ? ((uint32_t)m1 * 0x0101u | (m2 * 0x0101u) << 16) : 0u;
+                P[gi] = (uint32_t)m1 * 0x0101u | (m2 * 0x0101u) << 16;
             } else {
                 uint32_t p;
                 if constexpr (LUT) {
@@ -593,7 +589,9 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     p = pa | (pb << 16);
                     p = __builtin_amdgcn_perm(p, p, podd ? 0x03020100u : 0x02030001u);
                 }
-                P[gi] = gval[gi] ? p : 0u;    // duplicate stand-in check: no messages
+                // (a lane past its run's last check has every edge on its own dummy word, so
+                // its messages land there: no validity mask needed)
+                P[gi] = p;
             }
             if constexpr (F5_P2_MODE == 1) pass2g(gi);     // this group's scatter right away
         }
