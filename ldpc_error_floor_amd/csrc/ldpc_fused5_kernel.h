@@ -825,7 +825,7 @@ constexpr Shape5 kShapes5[] = {
     {64, 3, 8, 1, true, false},     // z=1 sparse (MacKay)
     {64, 2, 32, 1, true, false},    // z=1 dense rows (BCH)
     {4, 3, 12, 7, true, false},     // 5G BG2-like at two workgroups per CU (z=64: 16 slots, 4 codewords)
-    {8, 2, 24, 6, true, false},     // 802.11n-like at three workgroups per CU
+    {8, 2, 22, 6, true, false},     // 802.11n-like (deg <= 22: no all-padding address word) at three WGs per CU
     {4, 4, 20, 4, true, false},     // 5G BG1-like (n = 2304 variables, deg 3-19, z = 72), one WG per CU
     {4, 7, 20, 4, true, true, 3, 10},   // 5G BG1-like, 3 heavy + 4 light slots, 8 waves: two WGs per CU
     {4, 5, 10, 6, true, true, 2, 6},    // 5G BG2-like (deg 8-10 / 4-6), 8 waves: three WGs per CU

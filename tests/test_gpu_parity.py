@@ -125,7 +125,7 @@ def test_file_level_decoder_matches_reference(cuda_device):
 # every fused v5 shape (kShapes5 in ldpc_fused5.hip), forced with LDPC_F5_SHAPE, on every exact
 # QMS fixture it fits: APP export build and counters-only build, bit-exact
 F5_SHAPES = {0: "cw16,g3,d16", 1: "cw16,g3,d24", 2: "cw8,g5,d16", 3: "cw64,g3,d8",
-             4: "cw64,g2,d32", 5: "cw4,g3,d12", 6: "cw8,g2,d24", 7: "cw4,g4,d20", 8: "cw4,g7,d20", 9: "cw4,g5,d10"}
+             4: "cw64,g2,d32", 5: "cw4,g3,d12", 6: "cw8,g2,d22", 7: "cw4,g4,d20", 8: "cw4,g7,d20", 9: "cw4,g5,d10"}
 
 
 @pytest.mark.parametrize("shape", sorted(F5_SHAPES))
