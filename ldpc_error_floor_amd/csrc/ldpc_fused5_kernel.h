@@ -71,6 +71,10 @@ constexpr uint32_t F5_WBIAS = F5_SBIAS + (uint32_t)F5_TVB * 65536u - (uint32_t)F
 // F5_APPH + APP with F5_APPH = 0x4B800000: APP >= 0 exactly when bit 23 is set (an OR over
 // entries then answers "any hard decision 1")
 constexpr float F5_MAGIC_A = 16760832.0f;
+// counters-only VN without UCN: bits 0x4B7F4000, so the low 16 bits of its Q(y) bits plus the W
+// word's low half (S + 2^14) are APP + 0x8000, whose bit 15 is [APP >= 0]
+constexpr float F5_MAGIC_H = 16728064.0f;
+static_assert(16728064 == 8388608 + 0x7F4000, "F5_MAGIC_H bits 0x4B7F4000");
 constexpr int F5_APPH = 0x4B800000;
 static_assert(12582912 + 4194304 - (int)F5_SBIAS == 16760832, "APP magic");
 
@@ -303,7 +307,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         for (int e = tid; e < total; e += NT) {
             const uint32_t v = (uint32_t)e >> LOGCW;
             const int t0 = q_scaled5(CH[e] * BETA[__umulhi(v, a.zmagic)], (float)qmax);  // lw_0
-            W[e] = ((uint32_t)(t0 + F5_TVB) << 16) | ((uint32_t)(t0 >= 0) << 15) | F5_SBIAS;   // hd_{-1}
+            W[e] = ((uint32_t)(t0 + F5_TVB) << 16) | ((uint32_t)(UCN && t0 >= 0) << 15) | F5_SBIAS;   // hd_{-1}
         }
         if (tid < F5_NDUMMY) W[total + tid] = F5_DUMMY_W;
     }
@@ -611,6 +615,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         }
         const float* bnext = BETA + (size_t)((t + 1) & 1) * a.N;     // unused when last
         uint32_t any_hd = 0, any_pos = 0, nbits = 0;
+        constexpr int F5_HDB = UCN ? 23 : 15;     // bit of aor that says "some APP >= 0"
         const float qmf = (float)qmax;
         const int sb = -(int)F5_SBIAS;
         if (tid < F5_NDUMMY) W[total + tid] = F5_DUMMY_W;    // pass-2 adds of padding edges
@@ -659,6 +664,25 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                             // Q(y) for y already scaled to grid units: clamp to +-qmax, then
                             // add 1.5*2^23 so the float add rounds half to even (as rintf) and
                             // the integer sits in the low mantissa bits: bits - F5_MAGIC_BITS
+                            if (!LAST && !UCN) {
+                                // W's low half is exactly S + bias here (no hd bit without UCN)
+                                // and only low halves matter: add the whole word, no mask.
+                                // Low 16 bits of qh + W = APP + 0x8000: bit 15 = [APP >= 0]
+                                const uint32_t wraw = wv[j];
+                                const float yc = __builtin_amdgcn_fmed3f(chv[j], -qmf, qmf);
+                                const uint32_t apph = (uint32_t)__float_as_int(yc + F5_MAGIC_H) + wraw;
+                                if (FULLT) {
+                                    aor |= apph;
+                                } else {
+                                    const int v = ((c + j) * 64 + lane) >> LOGCW;
+                                    aor |= (v < tb) ? apph : 0u;
+                                }
+                                const float yb = __builtin_amdgcn_fmed3f(chv[j] * bv[j], -qmf, qmf);
+                                const uint32_t tb2 = clamp_i16((uint32_t)__float_as_int(yb + F5_MAGIC) + wraw,
+                                                               tlo, thi);
+                                const_cast<uint32_t*>(Wr)[j * 64] = tb2 * 65536u + F5_WBIAS;
+                                continue;
+                            }
                             const int s = (int)(wv[j] & 0x7FFFu);                     // S + bias
                             const float yc = __builtin_amdgcn_fmed3f(chv[j], -qmf, qmf);
                             const int qc = __float_as_int(yc + F5_MAGIC_A);
@@ -716,7 +740,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     const int app = q_scaled5(ch, qmf) + s + sb;
                     const int appt = ((int)v < a.target_bits) ? app : INT_MIN;
                     amax = max(amax, appt == INT_MIN ? INT_MIN : appt + F5_APPH);
-                    aor |= (appt == INT_MIN) ? 0u : (uint32_t)(appt + F5_APPH);
+                    aor |= (appt != INT_MIN && appt >= 0) ? (1u << F5_HDB) : 0u;
                     if (!last) {
                         const int tn = min(max(q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], qmf) + s + sb,
                                                -2 * qmax), 2 * qmax);
@@ -726,7 +750,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     }
                 }
             }
-            any_hd = last ? (amax >= F5_APPH) : ((aor >> 23) & 1u);
+            any_hd = last ? (amax >= F5_APPH) : ((aor >> F5_HDB) & 1u);
             any_pos = amax > F5_APPH;
         } else {
         for (int r = 0; r < ((a.ablate & 4) ? 0 : a.nent); ++r) {
