@@ -21,7 +21,7 @@
 //    v_sad_u16), and the V->C signs with one v_perm per edge, which appends the offset-binary
 //    byte (bit 7: "v2c >= 0") to a SEL-shaped word;
 //    the quantizer clamp moves after the minimum (clamp is monotonic);
-//  * W[v][cw] = Tv + 128 (bits 31..16) | hd (bit 15) | S + 2^14 (bits 14..0): pass 1 reads Tv
+//  * W[v][cw] = hd (bit 31) | Tv + 128 (bits 30..16) | S + 2^14 (bits 15..0): pass 1 reads Tv
 //    with an SDWA word select, pass 2 adds the message without a shift;
 //  * an edge slot past a check's degree points at a per-lane dummy word whose Tv is -96: its
 //    |v2c| never wins a minimum, its sign is negative (not counted), its hd bit is 0, and pass 2
@@ -307,7 +307,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         for (int e = tid; e < total; e += NT) {
             const uint32_t v = (uint32_t)e >> LOGCW;
             const int t0 = q_scaled5(CH[e] * BETA[__umulhi(v, a.zmagic)], (float)qmax);  // lw_0
-            W[e] = ((uint32_t)(t0 + F5_TVB) << 16) | ((uint32_t)(UCN && t0 >= 0) << 15) | F5_SBIAS;   // hd_{-1}
+            W[e] = ((uint32_t)(t0 + F5_TVB) << 16) | ((uint32_t)(UCN && t0 >= 0) << 31) | F5_SBIAS;   // hd_{-1}
         }
         if (tid < F5_NDUMMY) W[total + tid] = F5_DUMMY_W;
     }
@@ -440,7 +440,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             uint32_t NG[NSEL];
 #pragma unroll
             for (int w = 0; w < NSEL; ++w) NG[w] = 0;
-            uint32_t syn = 0;     // UCN: XOR of the edges' W words (bit 15: previous hard decisions)
+            uint32_t syn = 0;     // UCN: XOR of the edges' W words (bit 31: previous hard decisions)
             // this row's weights as scalar loads issued ahead of the chunks (a per-lane choice
             // between two global addresses would be a vector load waited on in the state update)
             float wa = 0.f, wu = 0.f;
@@ -546,7 +546,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             // message sign = V->C sign XOR (count of positives odd): applied to P as a byte
             // swap inside each half; for PEW (P holds magnitudes) to the selector bytes, whose
             // bit 0 then means "negative message" (V->C >= 0 XOR count even)
-            if constexpr (UCN) syn = (syn >> 15) & 1u;
+            if constexpr (UCN) syn = syn >> 31;
             const bool podd = (uint32_t)__popc(px) & 1u;
             // argmin bit: the edge code is 8 * b + 1 for selector byte b (word b / 4), so one
             // 64-bit shift places it inside the word pair b / 8
@@ -615,7 +615,6 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         }
         const float* bnext = BETA + (size_t)((t + 1) & 1) * a.N;     // unused when last
         uint32_t any_hd = 0, any_pos = 0, nbits = 0;
-        constexpr int F5_HDB = UCN ? 23 : 15;     // bit of aor that says "some APP >= 0"
         const float qmf = (float)qmax;
         const int sb = -(int)F5_SBIAS;
         if (tid < F5_NDUMMY) W[total + tid] = F5_DUMMY_W;    // pass-2 adds of padding edges
@@ -664,9 +663,9 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                             // Q(y) for y already scaled to grid units: clamp to +-qmax, then
                             // add 1.5*2^23 so the float add rounds half to even (as rintf) and
                             // the integer sits in the low mantissa bits: bits - F5_MAGIC_BITS
-                            if (!LAST && !UCN) {
-                                // W's low half is exactly S + bias here (no hd bit without UCN)
-                                // and only low halves matter: add the whole word, no mask.
+                            if (!LAST) {
+                                // W's low half is exactly S + bias (the hd bit is bit 31) and only
+                                // low halves matter: add the whole word, no mask.
                                 // Low 16 bits of qh + W = APP + 0x8000: bit 15 = [APP >= 0]
                                 const uint32_t wraw = wv[j];
                                 const float yc = __builtin_amdgcn_fmed3f(chv[j], -qmf, qmf);
@@ -680,40 +679,24 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                                 const float yb = __builtin_amdgcn_fmed3f(chv[j] * bv[j], -qmf, qmf);
                                 const uint32_t tb2 = clamp_i16((uint32_t)__float_as_int(yb + F5_MAGIC) + wraw,
                                                                tlo, thi);
-                                const_cast<uint32_t*>(Wr)[j * 64] = tb2 * 65536u + F5_WBIAS;
+                                uint32_t wn = tb2 * 65536u + F5_WBIAS;
+                                if (UCN) wn |= (apph << 16) & 0x80000000u;       // hd for the syndrome
+                                const_cast<uint32_t*>(Wr)[j * 64] = wn;
                                 continue;
                             }
+                            // last iteration: counters only (no W update)
                             const int s = (int)(wv[j] & 0x7FFFu);                     // S + bias
                             const float yc = __builtin_amdgcn_fmed3f(chv[j], -qmf, qmf);
                             const int qc = __float_as_int(yc + F5_MAGIC_A);
                             // APP + F5_APPH: bit 23 set iff APP >= 0
                             const int appb = qc + s;
-                            if (LAST) {
-                                int appt = appb;
-                                if (!FULLT) {
-                                    const int v = ((c + j) * 64 + lane) >> LOGCW;
-                                    appt = (v < tb) ? appb : INT_MIN;
-                                }
-                                amax = max(amax, appt);
-                                nbits += (uint32_t)(appt >= F5_APPH) & cvalid;
-                            } else {
-                                if (FULLT) {
-                                    aor |= (uint32_t)appb;
-                                } else {
-                                    const int v = ((c + j) * 64 + lane) >> LOGCW;
-                                    aor |= (v < tb) ? (uint32_t)appb : 0u;
-                                }
-                                const float yb = __builtin_amdgcn_fmed3f(chv[j] * bv[j], -qmf, qmf);
-                                // Tv + biases, Tv kept within +-2 qmax (pass 1's 8-bit range;
-                                // min(|Tv - m|, qmax) and the sign of Tv - m are unchanged)
-                                // (16-bit clamp: only the low half of Tv + F5_APP0 reaches W)
-                                const uint32_t tb2 = clamp_i16((uint32_t)(__float_as_int(yb + F5_MAGIC) + s),
-                                                               tlo, thi);
-                                // W = (Tv << 16) | S bias, Tv = tb2 - F5_MAGIC_BITS - S bias
-                                uint32_t wn = tb2 * 65536u + F5_WBIAS;
-                                if (UCN) wn |= ((uint32_t)appb >> 8) & 0x8000u;
-                                const_cast<uint32_t*>(Wr)[j * 64] = wn;
+                            int appt = appb;
+                            if (!FULLT) {
+                                const int v = ((c + j) * 64 + lane) >> LOGCW;
+                                appt = (v < tb) ? appb : INT_MIN;
                             }
+                            amax = max(amax, appt);
+                            nbits += (uint32_t)(appt >= F5_APPH) & cvalid;
                         }
                     }
                 }
@@ -740,17 +723,17 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                     const int app = q_scaled5(ch, qmf) + s + sb;
                     const int appt = ((int)v < a.target_bits) ? app : INT_MIN;
                     amax = max(amax, appt == INT_MIN ? INT_MIN : appt + F5_APPH);
-                    aor |= (appt != INT_MIN && appt >= 0) ? (1u << F5_HDB) : 0u;
+                    aor |= (appt != INT_MIN && appt >= 0) ? 0x8000u : 0u;
                     if (!last) {
                         const int tn = min(max(q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], qmf) + s + sb,
                                                -2 * qmax), 2 * qmax);
-                        W[e] = ((uint32_t)(tn + F5_TVB) << 16) | (((uint32_t)~app >> 16) & 0x8000u) | F5_SBIAS;
+                        W[e] = ((uint32_t)(tn + F5_TVB) << 16) | ((uint32_t)~app & 0x80000000u) | F5_SBIAS;
                     } else {
                         nbits += (uint32_t)(appt >= 0 && appt != INT_MIN) & (uint32_t)cvalid;
                     }
                 }
             }
-            any_hd = last ? (amax >= F5_APPH) : ((aor >> F5_HDB) & 1u);
+            any_hd = last ? (amax >= F5_APPH) : ((aor >> 15) & 1u);     // bit 15: some APP >= 0
             any_pos = amax > F5_APPH;
         } else {
         for (int r = 0; r < ((a.ablate & 4) ? 0 : a.nent); ++r) {
@@ -765,7 +748,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 if (!last) {
                     const int tn = min(max(q_scaled5(ch * bnext[__umulhi(v, a.zmagic)], (float)qmax) + S,
                                            -2 * qmax), 2 * qmax);
-                    W[e] = ((uint32_t)(tn + F5_TVB) << 16) | ((uint32_t)(app >= 0) << 15) | F5_SBIAS;
+                    W[e] = ((uint32_t)(tn + F5_TVB) << 16) | ((uint32_t)(app >= 0) << 31) | F5_SBIAS;
                 }
                 if ((int)v < a.target_bits) {
                     any_hd |= (uint32_t)(app >= 0);
