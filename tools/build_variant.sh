@@ -12,6 +12,12 @@ PATCH=${1:-}; [ $# -gt 0 ] && shift
 B=ldpc_error_floor_amd/_build
 W=$(mktemp -d /tmp/ldpc_variant.XXXX)
 cp -r ldpc_error_floor_amd/csrc "$W/csrc"
+# only the fused v5 units are rebuilt; a patch touching any other source (a shared header such as
+# ldpc_internal.h changes struct layouts) would link mismatched objects: refuse it
+if [ -n "$PATCH" ] && grep -E '^\+\+\+ ' "$PATCH" | grep -vqE 'ldpc_fused5(_kernel\.h|\.hip|_shape\.hip)$'; then
+  echo "build_variant: $PATCH touches files other than ldpc_fused5*; build the full tree instead" >&2
+  rm -rf "$W"; exit 2
+fi
 if [ -n "$PATCH" ]; then (cd "$W/csrc" && patch -s -p3 < "$OLDPWD/$PATCH"); fi
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -I$W/csrc -mllvm -pragma-unroll-threshold=500000 $*"
 NS=$(python3 -c "import sys; sys.path.insert(0, 'ldpc_error_floor_amd'); import build; print(build._f5_shape_count())")
