@@ -4,18 +4,27 @@
 One "step" = one decode of a resident batch (default B = 2^20 codewords per GPU, the
 BASELINE.json configs[1] workload) with FER/BER counters accumulated on the device.  The
 AWGN LLRs (3.5 dB, QMS q=5) are generated on the GPU before the timed region.
-``python bench.py --gpus N --steps K --warmup W``; N > 1 is launched by torch.distributed.run
-(one rank per GPU, weak scaling: every rank decodes its own B codewords).
+``python bench.py --gpus N --steps K --warmup W``: one rank per GPU, weak scaling (every rank
+decodes its own B codewords, a disjoint slice of the global Philox stream).  Under
+torch.distributed.run (WORLD_SIZE set) each process is one rank; run directly with N > 1, this
+script starts the N ranks itself as fresh child processes (it never touches the GPU before
+that) and exits with the first failing rank's status.
 
 ``--config C3|C4|C5`` runs the SURVEY §8 d companion workloads instead (802.11n, 5G BG2,
 5G BG1); the default C2 line is the one the driver records.
 
 Prints ONE JSON line (rank 0).  Besides the driver's fields it carries:
-  roofline      dominant kernel vs HBM: achieved = SURVEY §8 d bytes/codeword x B / kernel
-                time (HIP events on the decode stream); traffic = PMC HBM bytes per launch
-                when profiles/traffic_<kernel>.json exists (see tools/profile.sh), else null
+  roofline      the dominant kernel against the resource that binds it.  flood (state in HBM):
+                bound "hbm", achieved = SURVEY §8 d bytes/codeword x B / kernel time (HIP
+                events on the decode stream).  fused (state in LDS/VGPRs, VALU-issue bound):
+                bound "valu", achieved = SQ_INSTS_VALU per launch (PMC of this build,
+                profiles/traffic_<kernel>.json) / kernel time against one wave64 VALU issue
+                per 2 cycles per SIMD; hbm_frac = measured PMC traffic / time / 8 TB/s and
+                effective_frac = the §8 d figure / 8 TB/s ride along.  traffic = PMC HBM
+                bytes per launch (null without a profile of this kernel at this batch).
   cpu_baseline  the dense TF-graph-equivalent numpy restatement of the reference decoder
-                (oracle/nms_dense.py) on the C1 sample (B=120, T=20, 3.5 dB), rank 0, N=1
+                (oracle/nms_dense.py) on the C1 sample (B=120, T=20, 3.5 dB), rank 0, N=1,
+                every host core this process may run on
   e2e_with_rng  K steps that each draw a fresh AWGN batch inside the timed region
                 (ldpc_decode_awgn: generated in the decoder's prologue; SURVEY §8 d
                 "separately time end-to-end with GPU RNG and counters")
@@ -26,6 +35,8 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -88,7 +99,7 @@ def cpu_baseline(proto, g, W, cp, B=120, T=20, snr=3.5):
     from threadpoolctl import threadpool_limits
     from ldpc_error_floor_amd.channel import create_mix_epoch
     from oracle import nms_dense, nms_oracle
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores = len(os.sched_getaffinity(0))          # SURVEY §8 d: all host cores
     sigma = float(cp.sigma(snr))
     wr, nr = np.random.RandomState(2044), np.random.RandomState(1076)
     X, _ = create_mix_epoch([sigma], wr, nr, B, g.N, g.N - g.M, 24, [], True, 2, 0, 0, 0, 0, 5, 20.0)
@@ -109,6 +120,8 @@ def cpu_baseline(proto, g, W, cp, B=120, T=20, snr=3.5):
     except OSError:
         pass
     return {"value": round(B / dt, 3), "unit": "codewords/s", "cores": cores, "kind": "port",
+            "threads": f"BLAS pool limited to {cores} (threadpoolctl; numpy elementwise ops run "
+                       f"single-threaded)",
             "sample": f"C1: wman QMS q5 T={T}, B={B} host-channel codewords at {snr} dB (seeds "
                       f"2044/1076), dense TF-graph-equivalent numpy (oracle/nms_dense.py), "
                       f"{dt:.1f} s",
@@ -116,9 +129,47 @@ def cpu_baseline(proto, g, W, cp, B=120, T=20, snr=3.5):
             "sparse_oracle_cw_s": round(8 * B / dt_sparse, 1)}
 
 
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n):
+    """Start ranks 0..n-1 of this command as fresh child processes (one per GPU; RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT as torch.distributed.run would set them) and wait.
+    The parent never initialises HIP and never execs.  Rank 0 prints the JSON line (the
+    children share this stdout).  Returns 0, or the status of the first rank that failed (the
+    others are then terminated)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"bench.py: rank {procs.index(p)} exited with status {rc}; stopping the "
+                      f"other ranks", file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return status
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU per step")
@@ -130,25 +181,51 @@ def main():
     ap.add_argument("--all-kernels", action="store_true",
                     help="also time the non-default kernel and report it under 'kernels'")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
     # one rank per GPU over RCCL; LDPC_BENCH_BACKEND=gloo rehearses the multi-rank code path
-    # with several ranks on the same GPU (the driver's runs use the default)
+    # with several ranks on the same GPU (collectives then go through host copies)
     backend = os.environ.get("LDPC_BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
     gpu = local if backend == "nccl" else local % max(ndev, 1)
-    if world > 1:
-        torch.cuda.set_device(gpu)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group(backend)
+    if backend == "nccl" and world > 1 and gpu >= ndev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {ndev} GPUs visible")
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+
+    def allreduce(t, op):
+        """In-place all-reduce of a device tensor (host round trip for gloo)."""
+        if world == 1:
+            return t
+        if backend == "nccl":
+            dist.all_reduce(t, op=op)
+            return t
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+        return t
+
+    def barrier():
+        if world > 1:
+            if backend == "nccl":
+                dist.barrier(device_ids=[gpu])
+            else:
+                dist.barrier()
 
     from ldpc_error_floor_amd.decoder import NMSDecoder
     cfg = CONFIGS[args.config]
@@ -169,11 +246,11 @@ def main():
         for _ in range(args.warmup):
             dec.decode(llr, T=T, app=False, counters=counters)
         torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
+        counters.zero_()
+        barrier()
+        torch.cuda.synchronize(dev)
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
-        counters.zero_()
         t0 = time.perf_counter()
         ev0.record(stream)
         for i in range(args.steps):
@@ -185,14 +262,10 @@ def main():
         ev1.record(stream)
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
-        if world > 1:
-            dist.barrier()
-        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        cnt = counters.clone()
-        if world > 1:
-            dist.all_reduce(cnt)
+        barrier()
+        elapsed = allreduce(torch.tensor([t1 - t0], dtype=torch.float64, device=dev),
+                            dist.ReduceOp.MAX if world > 1 else None)
+        cnt = allreduce(counters.clone(), dist.ReduceOp.SUM if world > 1 else None)
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
         return dict(name=name, elapsed=float(elapsed.item()), kernel_ms=kernel_ms,
                     counters=cnt.cpu().tolist(), design_bytes=dec.kernel_info(T)[0])
@@ -213,30 +286,40 @@ def main():
 
     t = primary["elapsed"]
     value = world * B * args.steps / t
+    kernel_s = primary["kernel_ms"] / 1e3
     bytes_cw = survey_bytes_per_cw(g.E, g.N, z, T, ucn=cfg["sharing"][1] > 0)
-    achieved = bytes_cw * B / (primary["kernel_ms"] / 1e3) / 1e9
-    traffic = None
-    valu = None
-    safe = "".join(ch if (ch.isalnum() or ch in "_.-") else "_" for ch in primary["name"])
-    tf = os.path.join(ROOT, "profiles", f"traffic_{safe}.json")
-    if os.path.exists(tf):
-        try:
-            with open(tf) as f:
-                tj = json.load(f)
-            if int(tj.get("batch", -1)) == B:
-                traffic = tj.get("hbm_bytes_per_launch")
-                if tj.get("valu_insts_per_launch"):
-                    rate = tj["valu_insts_per_launch"] / (primary["kernel_ms"] / 1e3)
-                    valu = {"achieved": round(rate, 1), "peak": VALU_PEAK_WINST,
-                            "unit": "wave-instructions/s", "frac": round(rate / VALU_PEAK_WINST, 4),
-                            "insts_per_launch": tj["valu_insts_per_launch"],
-                            "wait_any_frac": tj.get("wait_any_frac"), "source": tj.get("source"),
-                            "note": "the fused kernel's real bound: SQ_INSTS_VALU (PMC, "
-                                    "profiles/) over this run's kernel time, against one wave64 "
-                                    "VALU issue per 2 cycles per SIMD; VOP3/SDWA forms issue "
-                                    "at about half that rate (DESIGN.md 3.2)"}
-        except (OSError, ValueError):
-            traffic = None
+    effective = bytes_cw * B / kernel_s / 1e9            # GB/s, SURVEY §8 d two-kernel bytes
+    prof = load_profile(primary["name"], B)
+    traffic = prof.get("hbm_bytes_per_launch") if prof else None
+    fused = primary["name"] != "flood"
+    if fused:
+        vi = prof.get("valu_insts_per_launch") if prof else None
+        rate = vi / kernel_s if vi else None
+        roofline = {"bound": "valu",
+                    "achieved": round(rate, 1) if rate else None, "peak": VALU_PEAK_WINST,
+                    "unit": "wave-instructions/s",
+                    "frac": round(rate / VALU_PEAK_WINST, 4) if rate else None,
+                    "traffic": traffic,
+                    "hbm_frac": (round(traffic / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
+                                 if traffic else None),
+                    "effective_frac": round(effective / HBM_PEAK_GBS, 4),
+                    "valu_insts_per_launch": vi,
+                    "wait_any_frac": prof.get("wait_any_frac") if prof else None,
+                    "profile": prof.get("source") if prof else None}
+        roofline["note"] = ("fused: all T iterations per codeword block in LDS/VGPRs; the only "
+                            "HBM traffic is the LLR read, so VALU issue binds. achieved = PMC "
+                            "SQ_INSTS_VALU per launch (this build, profile above) / this run's "
+                            "kernel time (HIP events); peak = one wave64 VALU instruction per 2 "
+                            "cycles per SIMD at 2.4 GHz (VOP3/SDWA forms take ~4, DESIGN.md 3.2). "
+                            "effective_frac = SURVEY 8d two-kernel bytes/codeword x B / time / "
+                            "8 TB/s (a design-comparison figure, not a bandwidth).")
+    else:
+        roofline = {"bound": "hbm", "achieved": round(effective, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(effective / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "note": "achieved = SURVEY 8d bytes/codeword x B / kernel time (HIP events)"}
+    roofline.update({"kernel": primary["name"], "kernel_ms": round(primary["kernel_ms"], 3),
+                     "algorithmic_bytes_per_cw": bytes_cw,
+                     "design_bytes_per_cw": int(primary["design_bytes"])})
     c = primary["counters"]
     n_frames = world * B * args.steps
     wdesc = (f"trained weights ({os.path.basename(cfg['weights'])})" if "weights" in cfg
@@ -261,18 +344,11 @@ def main():
                                f"{wdesc}{pdesc}, B={B} codewords/GPU/step @ {snr} dB",
                    "batch_per_gpu": B, "iterations": T, "kernel": primary["name"],
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
-                     "kernel": primary["name"], "kernel_ms": round(primary["kernel_ms"], 3),
-                     "algorithmic_bytes_per_cw": bytes_cw,
-                     "design_bytes_per_cw": int(primary["design_bytes"]),
-                     "note": "achieved = SURVEY 8d two-kernel fp32 bytes/codeword x B / decode "
-                             "time (HIP events); for the fused kernel this is an effective "
-                             "figure (its real HBM traffic is design_bytes_per_cw)"},
-        "valu_issue": valu,
+        "roofline": roofline,
         "fer_at_snr": {"frames": n_frames, "fer_last": c[1] / n_frames,
                        "ber_last": c[0] / (n_frames * g.N * z)},
+        "counters": {"bit_err_last": c[0], "frame_err_last": c[1], "frame_err_all": c[2],
+                     "loss2": c[3], "seed": 1076, "rank_offsets": [r * B for r in range(world)]},
     }
     out["e2e_with_rng"] = {"codewords_per_s": round(world * B * args.steps / e2e["elapsed"], 1),
                            "ms_per_step": round(1e3 * e2e["elapsed"] / args.steps, 3)}
@@ -284,6 +360,18 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def load_profile(name, batch):
+    """profiles/traffic_<kernel>.json (tools/traffic_json.py) when it was taken at this batch."""
+    safe = "".join(ch if (ch.isalnum() or ch in "_.-") else "_" for ch in name)
+    path = os.path.join(ROOT, "profiles", f"traffic_{safe}.json")
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return tj if int(tj.get("batch", -1)) == batch else None
 
 
 if __name__ == "__main__":

@@ -23,9 +23,8 @@ INCLUDE = os.path.join(ROOT, "include")
 BUILD = os.path.join(PKG, "_build")
 ARCH = os.environ.get("LDPC_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["ldpc_capi.hip", "ldpc_flood.hip", "ldpc_fused.hip", "ldpc_fused3.hip",
-               "ldpc_fused4.hip", "ldpc_fused5.hip", "ldpc_channel.hip",
-               "ldpc_collect.hip"]
+HIP_SOURCES = ["ldpc_capi.hip", "ldpc_flood.hip", "ldpc_fused.hip", "ldpc_fused5.hip",
+               "ldpc_channel.hip", "ldpc_collect.hip"]
 HEADERS = ["ldpc_internal.h", "ldpc_fused.h", "ldpc_fused5_kernel.h", "ldpc_awgn.h"]
 # ldpc_fused5_shape.hip is compiled once per kShapes5 entry (-DF5_SHAPE=i), in parallel
 F5_SHAPE_SRC = "ldpc_fused5_shape.hip"

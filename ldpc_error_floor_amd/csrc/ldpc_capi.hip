@@ -448,9 +448,9 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
     if (mode < 0) return LDPC_ERR_ARG;
     const bool ucn = g->d_alpha_ucn != nullptr;
     int kern = p->kernel;
-    if (kern == LDPC_KERNEL_AUTO)
-        kern = fused_supported(g->dev, mode, p->T) ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
-    if (kern == LDPC_KERNEL_FUSED && !fused_supported(g->dev, mode, p->T)) return LDPC_ERR_UNSUPPORTED;
+    const bool fok = fused_supported(g->dev, mode, p->T, p->clip_llr);
+    if (kern == LDPC_KERNEL_AUTO) kern = fok ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
+    if (kern == LDPC_KERNEL_FUSED && !fok) return LDPC_ERR_UNSUPPORTED;
     if (kern != LDPC_KERNEL_FLOOD && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_ARG;
     const int64_t nv = (int64_t)g->N * g->z, ne = (int64_t)g->E * g->z;
     int64_t bytes = 0;
@@ -467,7 +467,7 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
         nm = "flood";
     } else {
         bytes = fused_bytes_per_cw(g->dev, p->T);
-        nm = fused_kernel_name(g->dev, mode, p->T, g->per_edge_w != 0);
+        nm = fused_kernel_name(g->dev, mode, p->T, p->clip_llr);
     }
     if (bytes_per_cw) *bytes_per_cw = bytes;
     if (name && name_len > 0) {
@@ -494,11 +494,10 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     const bool ucn = g->d_alpha_ucn != nullptr;
 
     int kern = p->kernel;
-    if (kern == LDPC_KERNEL_AUTO)
-        kern = fused_supported(g->dev, mode, p->T) ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
+    const bool fok = fused_supported(g->dev, mode, p->T, p->clip_llr);
+    if (kern == LDPC_KERNEL_AUTO) kern = fok ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
     if (kern != LDPC_KERNEL_FLOOD && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_ARG;
-    if (kern == LDPC_KERNEL_FUSED && !fused_supported(g->dev, mode, p->T))
-        return LDPC_ERR_UNSUPPORTED;
+    if (kern == LDPC_KERNEL_FUSED && !fok) return LDPC_ERR_UNSUPPORTED;
     if (gen && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_UNSUPPORTED;   // caller falls back
 
     const int ntiles = (int)((B + TILE - 1) / TILE);

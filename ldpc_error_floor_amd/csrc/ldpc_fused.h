@@ -11,26 +11,15 @@ struct FusedWorkspace {
     size_t tables_bytes = 0;
 };
 
-bool fused_supported(const DevGraph& g, int mode, int T);
+// fused v5 serves this request (QMS q in {5,-5,4,3}, clip_llr on the grid, a shape fits)
+bool fused_supported(const DevGraph& g, int mode, int T, float clip_llr);
 int64_t fused_bytes_per_cw(const DevGraph& g, int T);
 int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
                  bool ucn, bool want_bits, int ntiles_max, int T_max, int per_edge_w,
                  int64_t* counters, uint8_t* flags, hipStream_t s);
 void fused_bits_view(const FusedWorkspace& ws, Bufs& b);
-const char* fused_kernel_name(const DevGraph& g, int mode, int T, bool per_edge_w);
+const char* fused_kernel_name(const DevGraph& g, int mode, int T, float clip_llr);
 
-// v4 (ldpc_fused4.hip): two codewords per lane (packed 16-bit), preferred when it fits
-bool fused4_supported(const DevGraph& g, int T, int qmax, bool per_edge_w);
-const char* fused4_shape_name(const DevGraph& g, int T);
-int fused4_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, float step,
-                  int clip_u, uint64_t* hd_out, int64_t* counters, uint8_t* flags, hipStream_t s);
-
-// v3 (ldpc_fused3.hip): shape-specialised variant, preferred when a shape fits
-bool fused3_supported(const DevGraph& g, int T);
-const char* fused3_shape_name(const DevGraph& g, int T);
-int fused3_decode(const DevGraph& g, const Bufs& b, const float* llr, int qmax, float step,
-                  int clip_u, bool per_edge_w, uint64_t* hd_out, int64_t* counters,
-                  uint8_t* flags, hipStream_t s);
 // v5 (ldpc_fused5.hip): byte-packed check state, default when a shape fits
 bool fused5_supported(const DevGraph& g, int T);
 const char* fused5_shape_name(const DevGraph& g, int T);

@@ -13,7 +13,9 @@
 """
 from __future__ import annotations
 
+import json
 import math
+import os
 import time
 
 import numpy as np
@@ -21,7 +23,7 @@ import numpy as np
 from .channel import append_uncor_rows, create_mix_epoch, read_uncor_llr, write_uncor_file
 from .metrics import Counters, calc_ber_fer
 
-__all__ = ["compute_results", "fer_sweep", "shard_range"]
+__all__ = ["compute_results", "fer_sweep", "shard_range", "SweepCheckpoint", "collect_uncor_inputs"]
 
 
 def compute_results(sample_num, input_llr, input_codeword, SNR_sigma, wordRandom, noiseRandom,
@@ -72,15 +74,63 @@ def shard_range(total: int, rank: int, world: int):
     return begin, begin + per + (1 if rank < rem else 0)
 
 
+CKPT_VERSION = 1
+
+
+class SweepCheckpoint:
+    """One rank's sweep state as a small JSON file, replaced atomically (write + rename).
+
+    ``key`` holds everything that fixes the codeword stream and its partition (seed, sigmas,
+    total codewords, batch, T, puncture/shorten, rank/world); a resume against a different key
+    is refused.  ``si`` / ``pos`` = the SNR index and global codeword index to decode next,
+    ``counters`` = this rank's (not yet all-reduced) int64 counter block, ``uncor_bytes`` = the
+    length of the uncorrected-word file at that point (truncated back to it on resume, so rows
+    written after the checkpoint are not duplicated)."""
+
+    def __init__(self, path):
+        self.path = path
+
+    def load(self):
+        if not os.path.exists(self.path):
+            return None
+        with open(self.path) as f:
+            st = json.load(f)
+        if st.get("version") != CKPT_VERSION:
+            raise ValueError(f"{self.path}: checkpoint version {st.get('version')} != {CKPT_VERSION}")
+        return st
+
+    def save(self, key, si, pos, counters, uncor_bytes=None, done=False):
+        st = {"version": CKPT_VERSION, "key": key, "si": int(si), "pos": int(pos),
+              "counters": [[int(v) for v in row] for row in counters],
+              "uncor_bytes": uncor_bytes, "done": bool(done), "time": time.time()}
+        tmp = self.path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(st, f)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, self.path)
+
+
 def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T=None,
-              punct=(0, 0), short=(0, 0), kernel=None, group=None, progress=None,
-              uncor_path=None):
+              punct=None, short=None, kernel=None, group=None, progress=None,
+              uncor_path=None, checkpoint=None, checkpoint_every: int = 64,
+              resume: bool = False):
     """Decode ``n_codewords`` per SNR point (split across ranks) with GPU LLRs and device
     counters.  Returns a list of ``Counters`` (global totals on every rank).
 
+    ``punct`` / ``short``: 1-based inclusive ranges of the channel (``create_mix_epoch``,
+    ``Print_Functions.py:29-72``); ``None`` uses the decoder's own (``Decoder(..., punct,
+    short)`` / ``build_session``).  SNR point ``si`` uses the Philox stream ``seed + 7919 si``
+    indexed by the global codeword number, so any partition of the codewords (ranks, batches,
+    a resume) decodes the same words.
+
     ``uncor_path``: append the frames wrong at every iteration to this file in the
     ``Uncor.txt`` format (``sampling_type == 2``, ``Print_Functions.py:155-156``), collected on
-    the GPU; with several ranks each rank writes ``<uncor_path>.rank<r>``."""
+    the GPU; with several ranks each rank writes ``<uncor_path>.rank<r>``.
+
+    ``checkpoint``: path of this sweep's checkpoint (``<path>.rank<r>`` with several ranks),
+    written every ``checkpoint_every`` batches and after every SNR point; ``resume=True``
+    continues from it (a missing file starts from the beginning)."""
     import torch
     import torch.distributed as dist
     dist_on = dist.is_available() and dist.is_initialized()
@@ -88,6 +138,8 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
     world = dist.get_world_size(group) if dist_on else 1
     sigmas = np.atleast_1d(np.asarray(sigmas, np.float64))
     dev = decoder.device
+    punct = tuple(getattr(decoder, "punct", (0, 0)) if punct is None else punct)
+    short = tuple(getattr(decoder, "short", (0, 0)) if short is None else short)
     counters = torch.zeros((sigmas.size, 4), dtype=torch.int64, device=dev)
     begin, end = shard_range(int(n_codewords), rank, world)
     fused_channel = uncor_path is None and hasattr(decoder, "decode_awgn")
@@ -95,8 +147,33 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
                                                  device=dev)
     flags = torch.empty(batch, dtype=torch.uint8, device=dev) if uncor_path else None
     upath = uncor_path if (uncor_path is None or world == 1) else f"{uncor_path}.rank{rank}"
+    ck = None
+    si0, pos0 = 0, begin
+    if checkpoint is not None:
+        ck = SweepCheckpoint(checkpoint if world == 1 else f"{checkpoint}.rank{rank}")
+        key = {"seed": int(seed), "sigmas": [float(x) for x in sigmas],
+               "n_codewords": int(n_codewords), "batch": int(batch),
+               "T": None if T is None else int(T), "punct": list(punct), "short": list(short),
+               "rank": rank, "world": world, "uncor": upath is not None}
+        st = ck.load() if resume else None
+        if st is not None:
+            if st["key"] != key:
+                raise ValueError(f"{ck.path}: checkpoint is for {st['key']}, this sweep is {key}")
+            si0, pos0 = st["si"], st["pos"]
+            counters.copy_(torch.tensor(st["counters"], dtype=torch.int64))
+            if upath is not None and st.get("uncor_bytes") is not None and os.path.exists(upath):
+                with open(upath, "r+b") as f:
+                    f.truncate(int(st["uncor_bytes"]))
+
+    def save(si, pos, done=False):
+        ub = (os.path.getsize(upath) if upath and os.path.exists(upath) else 0) if upath else None
+        ck.save(key, si, pos, counters.cpu().tolist(), ub, done)
+
     for si, sigma in enumerate(sigmas):
-        pos = begin
+        if si < si0:
+            continue
+        pos = pos0 if si == si0 else begin
+        nb = 0
         while pos < end:
             b = min(batch, end - pos)
             if fused_channel:
@@ -113,10 +190,59 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
                     if rows.shape[0]:
                         append_uncor_rows(rows, upath)
             pos += b
+            nb += 1
+            if ck is not None and checkpoint_every > 0 and nb % checkpoint_every == 0 and pos < end:
+                save(si, pos)
             if progress:
                 progress(si, pos - begin, end - begin)
+        if ck is not None:
+            save(si + 1, begin, done=(si + 1 == sigmas.size))
     if dist_on and world > 1:
         dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
     host = counters.cpu().numpy()
     return [Counters.from_array(host[i], int(n_codewords), decoder.n_vars)
             for i in range(sigmas.size)]
+
+
+def collect_uncor_inputs(decoder, sigma, filename, counts=(10000, 5000, 5000), out_dir="Inputs",
+                         batch: int = 1 << 16, seed: int = 1076, T=None, punct=None, short=None,
+                         max_codewords: int = 1 << 34):
+    """Regenerate the post-decoder's inputs ``<out_dir>/[Uncor]_<filename>{,_Valid,_Test}.txt``
+    (``process_data``, ``Main_Functions.py:526-576``; stripped from the reference snapshot,
+    ``.MISSING_LARGE_BLOBS:1-3``): the reference's ``sampling_type == 2`` pass —
+    ``compute_results`` -> ``calc_ber_fer``'s ``uncor_flag`` -> ``write_uncor_file``
+    (``Print_Functions.py:144-156``, ``:120-126``) — run as a GPU sweep of the base decoder.
+
+    Split k (training, _Valid, _Test) decodes the Philox stream ``seed + k`` at ``sigma`` in
+    batches and appends the frames wrong at every iteration (compacted on the GPU) in the
+    ``Uncor.txt`` row format (3 zero columns, negated LLRs, ``%.1f``) until it holds
+    ``counts[k]`` rows.  Returns {path: (rows, codewords decoded)}."""
+    import torch
+    punct = tuple(getattr(decoder, "punct", (0, 0)) if punct is None else punct)
+    short = tuple(getattr(decoder, "short", (0, 0)) if short is None else short)
+    os.makedirs(out_dir, exist_ok=True)
+    dev = decoder.device
+    llr = torch.empty((batch, decoder.n_vars), dtype=torch.float32, device=dev)
+    flags = torch.empty(batch, dtype=torch.uint8, device=dev)
+    out = {}
+    for k, (suffix, need) in enumerate(zip(("", "_Valid", "_Test"), counts)):
+        path = os.path.join(out_dir, f"[Uncor]_{filename}{suffix}.txt")
+        if os.path.exists(path):
+            os.remove(path)
+        have, pos = 0, 0
+        while have < need:
+            if pos >= max_codewords:
+                raise RuntimeError(f"{path}: only {have} uncorrected words in {pos} codewords")
+            decoder.awgn(batch, float(sigma), seed + k, offset=pos, punct=punct, short=short,
+                         out=llr)
+            decoder.decode(llr, T=T, app=False, flags=flags)
+            rows = decoder.collect_uncorrected(flags, llr)
+            if rows.shape[0]:
+                rows = rows[:need - have]
+                append_uncor_rows(rows, path)
+                have += rows.shape[0]
+            pos += batch
+        if need == 0:
+            open(path, "w").close()
+        out[path] = (have, pos)
+    return out

@@ -99,6 +99,10 @@ def build_session(cfg: NMSConfig, proto=None, weights: DecoderWeights = None, de
         weights = expand_weights(cfg.sharing, wf.blocks, T, g, cfg.fixed_iter)
     dec = NMSDecoder(proto, cfg.z_value, weights, cfg.decoding_type, cfg.q_bit,
                      cfg.target_node(g.N, g.M), cfg.clip_LLR, device=device, kernel=kernel)
+    # the channel's puncture / shorten ranges (create_mix_epoch, Print_Functions.py:29-72) become
+    # the defaults of dec.awgn / dec.decode_awgn / fer_sweep(dec, ...)
+    dec.punct = (int(cfg.punct_start), int(cfg.punct_end))
+    dec.short = (int(cfg.short_start), int(cfg.short_end))
     t_first = max(cfg.iters_max - cfg.iter_step - cfg.fixed_init, cfg.fixed_iter)
     sess = Session(dec, cfg.batch_size, T, cfg.loss_type, t_first)
     return sess, make_net_dict(T)

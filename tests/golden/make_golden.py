@@ -361,6 +361,13 @@ def main():
         decoder_case(MF, PF, "g5bg1_303_q5_snr3.0",
                      "5G_LDPC_R0.73_n_dec2304_n2112_k1536_z72_s1537_1584", 72, [3, 0, 3], 2,
                      5, 12, 8, 3.0, random_weights=(0.5, 1.2), ps=1, pe=144, ss=1537, se=1584)
+    if want("g5bg1_t50"):
+        # SURVEY 8d C5 as benchmarked: BG1 n2112, T = 50, flat [3,0,3] alpha 0.75 / beta 1 (no
+        # trained weights ship for this code), puncture 1-144, shorten 1537-1584; 2.5 dB so
+        # that some frames still fail after 50 iterations
+        decoder_case(MF, PF, "g5bg1_303_flat_t50_snr2.5",
+                     "5G_LDPC_R0.73_n_dec2304_n2112_k1536_z72_s1537_1584", 72, [3, 0, 3], 2,
+                     5, 50, 6, 2.5, flat={0: 0.75, 2: 1.0}, ps=1, pe=144, ss=1537, se=1584)
     if want("z1"):
         decoder_case(MF, PF, "mackay_333_q5_snr2.5", "MACKAY_N96_K48", 1, [3, 3, 3], 2, 5, 20,
                      16, 2.5, flat={0: 0.75, 1: 0.5, 2: 1.0})

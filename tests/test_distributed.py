@@ -94,3 +94,21 @@ def test_sweep_collects_uncorrected_frames(tmp_path):
         if uncor.sum():
             write_uncor_file(uncor, llr.numpy().reshape(b, dec.N, dec.z), dec.n_vars, str(expect))
     assert path.read_text() == expect.read_text()
+
+
+def test_bench_launcher_spawns_and_propagates_failure():
+    """bench.py --gpus 2 without a launcher starts two rank processes itself (RANK /
+    WORLD_SIZE / MASTER_* set, no exec) and exits non-zero when a rank fails — here both fail
+    for want of a GPU.  (The GPU run of the same path: tests/test_gpu_bench.py.)"""
+    import subprocess
+    import sys
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by test_gpu_bench.py")
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--no-cpu-baseline", "--batch", "256"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode != 0
+    assert "rank 0: LOCAL_RANK 0" in r.stderr and "rank 1: LOCAL_RANK 1" in r.stderr
+    assert "exited with status" in r.stderr

@@ -30,7 +30,7 @@ def test_fixture_inventory():
             "g5bg2_222_sp_snr2.0",
             "wman_303_ms_snr2.5", "wman_222_q6", "wman_222_qm5", "wman_222_q4", "wman_222_q3",
             "wifi_333_q5_snr3.0", "g5bg2_222_q5_snr2.0", "mackay_333_q5_snr2.5",
-            "polar_222_q5_snr3.0"}
+            "polar_222_q5_snr3.0", "g5bg1_303_flat_t50_snr2.5"}
     assert need <= set(DECODER_CASES)
 
 

@@ -1,0 +1,100 @@
+"""fer_sweep checkpoint / resume (per-SNR counters saved periodically for
+multi-hour 1e-9 sweeps) on CPU with the oracle-backed stand-in decoder: an interrupted sweep
+resumed from its checkpoint returns exactly the counters (and uncorrected-word file) of an
+uninterrupted one."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from test_distributed import SIGMAS, _make_decoder
+from ldpc_error_floor_amd.fer import fer_sweep
+
+N_CW, BATCH = 45, 8
+
+
+class Stop(Exception):
+    pass
+
+
+def _tuples(res):
+    return [(c.bit_err_last, c.frame_err_last, c.frame_err_all, c.loss2) for c in res]
+
+
+def _interrupt_after(n):
+    calls = {"n": 0}
+
+    def progress(si, done, total):
+        calls["n"] += 1
+        if calls["n"] == n:
+            raise Stop()
+    return progress
+
+
+@pytest.mark.parametrize("stop_at", [3, 7, 12])
+def test_resume_equals_uninterrupted(tmp_path, stop_at):
+    dec = _make_decoder()
+    full = _tuples(fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=1076))
+    ck = str(tmp_path / "sweep.ckpt")
+    with pytest.raises(Stop):
+        fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=1076, checkpoint=ck, checkpoint_every=2,
+                  progress=_interrupt_after(stop_at))
+    st = json.load(open(ck))
+    assert st["done"] is False and (st["si"], st["pos"]) != (0, 0)
+    res = fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=1076, checkpoint=ck, checkpoint_every=2,
+                    resume=True)
+    assert _tuples(res) == full
+    assert json.load(open(ck))["done"] is True
+    # resuming a finished sweep decodes nothing and returns the same totals
+    again = fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=1076, checkpoint=ck, resume=True,
+                      progress=_interrupt_after(1))
+    assert _tuples(again) == full
+
+
+def test_resume_uncorrected_file_not_duplicated(tmp_path):
+    dec = _make_decoder()
+    ref_path = str(tmp_path / "ref.txt")
+    full = _tuples(fer_sweep(dec, SIGMAS[:1], N_CW, BATCH, seed=5, uncor_path=ref_path))
+    path, ck = str(tmp_path / "Uncor.txt"), str(tmp_path / "u.ckpt")
+    with pytest.raises(Stop):
+        fer_sweep(dec, SIGMAS[:1], N_CW, BATCH, seed=5, uncor_path=path, checkpoint=ck,
+                  checkpoint_every=2, progress=_interrupt_after(5))
+    res = fer_sweep(dec, SIGMAS[:1], N_CW, BATCH, seed=5, uncor_path=path, checkpoint=ck,
+                    checkpoint_every=2, resume=True)
+    assert _tuples(res) == full and full[0][2] > 0
+    assert open(path).read() == open(ref_path).read()
+
+
+def test_resume_refuses_a_different_sweep(tmp_path):
+    dec = _make_decoder()
+    ck = str(tmp_path / "s.ckpt")
+    with pytest.raises(Stop):
+        fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=1076, checkpoint=ck, checkpoint_every=1,
+                  progress=_interrupt_after(2))
+    with pytest.raises(ValueError, match="checkpoint is for"):
+        fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=1077, checkpoint=ck, resume=True)
+    # without resume the checkpoint is overwritten from the start
+    res = fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=1077, checkpoint=ck)
+    assert json.load(open(ck))["key"]["seed"] == 1077 and len(res) == 2
+
+
+def test_collect_uncor_inputs_roundtrip(tmp_path):
+    """collect_uncor_inputs writes the three post-decoder input files in the reference's row
+    format; process_data's restatement reads them back, and every row is a frame the base
+    decoder gets wrong at every iteration."""
+    from _helpers import flags_from_app
+    from ldpc_error_floor_amd.channel import load_uncor_inputs
+    from ldpc_error_floor_amd.fer import collect_uncor_inputs
+    from oracle import nms_oracle
+    dec = _make_decoder()
+    res = collect_uncor_inputs(dec, 0.7943282, "wman_N0576_R34_z24", (5, 3, 2), str(tmp_path),
+                               batch=16, seed=9)
+    assert sorted(v[0] for v in res.values()) == [2, 3, 5]
+    tr, trc, va, vac, te, tec = load_uncor_inputs("wman_N0576_R34_z24", 5, 1, 3, 1, 2,
+                                                  inputs_dir=str(tmp_path))
+    assert tr.shape == (5, 576) and va.shape == (3, 576) and te.shape == (2, 576)
+    assert not trc.any()
+    x = -np.concatenate([tr, va, te])             # files hold negated LLRs
+    o = nms_oracle.decode(x, dec.proto, 24, dec.W.alpha, dec.W.alpha_ucn, dec.W.beta, 20, 2, 5)
+    assert np.all(flags_from_app(o["app"]) & 1)
