@@ -295,24 +295,32 @@ def main():
     if fused:
         vi = prof.get("valu_insts_per_launch") if prof else None
         rate = vi / kernel_s if vi else None
+        vb = (prof.get("valu_busy") or {}) if prof else {}
+        issue = round(rate / VALU_PEAK_WINST, 4) if rate else None
         roofline = {"bound": "valu",
                     "achieved": round(rate, 1) if rate else None, "peak": VALU_PEAK_WINST,
                     "unit": "wave-instructions/s",
-                    "frac": round(rate / VALU_PEAK_WINST, 4) if rate else None,
+                    "frac": vb.get("frac", issue),
+                    "issue_frac": issue,
                     "traffic": traffic,
                     "hbm_frac": (round(traffic / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
                                  if traffic else None),
                     "effective_frac": round(effective / HBM_PEAK_GBS, 4),
                     "valu_insts_per_launch": vi,
+                    "valu_busy": vb or None,
                     "wait_any_frac": prof.get("wait_any_frac") if prof else None,
                     "profile": prof.get("source") if prof else None}
         roofline["note"] = ("fused: all T iterations per codeword block in LDS/VGPRs; the only "
-                            "HBM traffic is the LLR read, so VALU issue binds. achieved = PMC "
-                            "SQ_INSTS_VALU per launch (this build, profile above) / this run's "
-                            "kernel time (HIP events); peak = one wave64 VALU instruction per 2 "
-                            "cycles per SIMD at 2.4 GHz (VOP3/SDWA forms take ~4, DESIGN.md 3.2). "
-                            "effective_frac = SURVEY 8d two-kernel bytes/codeword x B / time / "
-                            "8 TB/s (a design-comparison figure, not a bandwidth).")
+                            "HBM traffic is the LLR read, so the VALU pipe binds. frac = VALU "
+                            "busy: quad-cycles with a VALU issue (SQ_INSTS_VALU - "
+                            "SQ_ACTIVE_INST_VALU2) / (1024 SIMDs x GRBM_GUI_ACTIVE/8/4), PMC of "
+                            "this build (profile above). issue_frac = achieved / peak with "
+                            "achieved = SQ_INSTS_VALU per launch / this run's kernel time (HIP "
+                            "events) and peak = one wave64 VALU issue per 2 cycles per SIMD at "
+                            "2.4 GHz, which only 2-cycle VOP1/VOP2 forms reach (VOP3/SDWA take "
+                            "a whole quad-cycle, DESIGN.md 3.2). effective_frac = SURVEY 8d "
+                            "two-kernel bytes/codeword x B / time / 8 TB/s (design comparison, "
+                            "not a bandwidth).")
     else:
         roofline = {"bound": "hbm", "achieved": round(effective, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(effective / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -188,13 +188,13 @@ PYBIND11_MODULE(_ldpc_nms, m) {
         py::arg("stream") = 0);
     m.def(
         "kernel_info",
-        [](Ctx& c, int T, int decoding_type, int q_bit, int target_bits, int kernel) {
-            ldpc_decode_params p = make_params(T, decoding_type, q_bit, target_bits, 20.f, kernel);
+        [](Ctx& c, int T, int decoding_type, int q_bit, int target_bits, int kernel, float clip) {
+            ldpc_decode_params p = make_params(T, decoding_type, q_bit, target_bits, clip, kernel);
             int64_t bytes = 0;
             char name[32] = {0};
             check(ldpc_kernel_info(c.h, &p, &bytes, name, 32), "ldpc_kernel_info");
             return py::make_tuple(bytes, std::string(name));
         },
         py::arg("ctx"), py::arg("T"), py::arg("decoding_type"), py::arg("q_bit"),
-        py::arg("target_bits"), py::arg("kernel"));
+        py::arg("target_bits"), py::arg("kernel"), py::arg("clip_llr") = 20.0f);
 }

@@ -107,7 +107,7 @@ class NMSDecoder:
         T = self.T if T is None else T
         ctx = self._ensure_ctx(1, T)
         return self._ext.kernel_info(ctx, T, self.decoding_type, self.q_bit, self.target_bits,
-                                     KERNELS[kernel or self.kernel])
+                                     KERNELS[kernel or self.kernel], self.clip)
 
     def supports(self, kernel: str, T=None) -> bool:
         try:
