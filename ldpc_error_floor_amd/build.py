@@ -25,7 +25,10 @@ ARCH = os.environ.get("LDPC_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["ldpc_capi.hip", "ldpc_flood.hip", "ldpc_fused.hip", "ldpc_fused5.hip",
                "ldpc_channel.hip", "ldpc_collect.hip"]
-HEADERS = ["ldpc_internal.h", "ldpc_fused.h", "ldpc_fused5_kernel.h", "ldpc_awgn.h"]
+HEADERS = ["ldpc_internal.h", "ldpc_fused.h", "ldpc_fused5_kernel.h", "ldpc_awgn.h", "ldpc_host.h"]
+# host-only C++ (no HIP): also built with g++ -fsanitize=address,undefined by
+# tests/test_host_sanitized.py
+HOST_SOURCES = ["ldpc_host.cpp"]
 # ldpc_fused5_shape.hip is compiled once per kShapes5 entry (-DF5_SHAPE=i), in parallel
 F5_SHAPE_SRC = "ldpc_fused5_shape.hip"
 
@@ -71,6 +74,7 @@ def build(force=False, jobs=4, verbose=False):
              "-mllvm", "-pragma-unroll-threshold=500000"]
     objs, jobs_list = [], []
     units = [(src, src.replace(".hip", ".o"), []) for src in HIP_SOURCES]
+    units += [(src, src.replace(".cpp", ".o"), []) for src in HOST_SOURCES]
     units += [(F5_SHAPE_SRC, f"ldpc_fused5_s{i}.o", [f"-DF5_SHAPE={i}"])
               for i in range(_f5_shape_count())]
     for src, obj, defs in units:

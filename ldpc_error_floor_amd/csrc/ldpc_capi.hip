@@ -13,9 +13,7 @@ using namespace ldpc;
 
 struct ldpc_graph {
     int device = 0;
-    int M = 0, N = 0, z = 0, E = 0;
-    int max_cdeg = 0, max_vdeg = 0;
-    std::vector<int32_t> row_ptr, pe_row, pe_col, pe_shift, col_ptr, col_pe;
+    host::GraphTables h;       // host tables (ldpc_host.cpp), also the device image
     int32_t* d_tables = nullptr;
     DevGraph dev{};
     int T_w = 0;
@@ -182,7 +180,7 @@ int ensure_flood(ldpc_ctx* c) {
     if (c->ch) return LDPC_OK;
     const ldpc_graph* g = c->g;
     const size_t nt = (size_t)c->ntiles_max;
-    const size_t nv = (size_t)g->N * g->z, ne = (size_t)g->E * g->z;
+    const size_t nv = (size_t)g->h.N * g->h.z, ne = (size_t)g->h.E * g->h.z;
     int st = dev_alloc(&c->ch, nt * nv * TILE);
     if (st == LDPC_OK) st = dev_alloc(&c->Tv, nt * nv * TILE);
     if (st == LDPC_OK) st = dev_alloc(&c->c2v, nt * ne * TILE);
@@ -215,64 +213,16 @@ int ldpc_graph_create(const int32_t* proto, int32_t M, int32_t N, int32_t z, int
                       ldpc_graph** out) {
     if (!out) return LDPC_ERR_ARG;
     *out = nullptr;
-    if (!proto || M <= 0 || N <= 0 || z <= 0) return LDPC_ERR_ARG;
     ldpc_graph* g = new (std::nothrow) ldpc_graph();
     if (!g) return LDPC_ERR_OOM;
+    const int st = host::build_graph(proto, M, N, z, g->h);
+    if (st != LDPC_OK) { delete g; return st; }
     g->device = device;
-    g->M = M; g->N = N; g->z = z;
-    g->row_ptr.assign(M + 1, 0);
-    for (int i = 0; i < M; ++i)
-        for (int j = 0; j < N; ++j) {
-            const int32_t s = proto[(size_t)i * N + j];
-            if (s < -1) { delete g; return LDPC_ERR_ARG; }
-            if (s != -1) {
-                g->pe_row.push_back(i);
-                g->pe_col.push_back(j);
-                g->pe_shift.push_back(s % z);
-            }
-        }
-    g->E = (int)g->pe_row.size();
-    if (g->E == 0) { delete g; return LDPC_ERR_ARG; }
-    for (int e = 0; e < g->E; ++e) g->row_ptr[g->pe_row[e] + 1]++;
-    for (int i = 0; i < M; ++i) {
-        g->max_cdeg = std::max(g->max_cdeg, g->row_ptr[i + 1]);
-        g->row_ptr[i + 1] += g->row_ptr[i];
-    }
-    if (g->max_cdeg > 64) { delete g; return LDPC_ERR_UNSUPPORTED; }
-    g->col_ptr.assign(N + 1, 0);
-    for (int e = 0; e < g->E; ++e) g->col_ptr[g->pe_col[e] + 1]++;
-    for (int j = 0; j < N; ++j) {
-        g->max_vdeg = std::max(g->max_vdeg, g->col_ptr[j + 1]);
-        g->col_ptr[j + 1] += g->col_ptr[j];
-    }
-    g->col_pe.assign(g->E, 0);
-    {
-        std::vector<int32_t> fill(g->col_ptr.begin(), g->col_ptr.end() - 1);
-        for (int e = 0; e < g->E; ++e) g->col_pe[fill[g->pe_col[e]]++] = e;   // ascending row
-    }
-    // one device block: row_ptr | pe_row | pe_col | pe_shift | col_ptr | col_pe
-    std::vector<int32_t> host;
-    host.insert(host.end(), g->row_ptr.begin(), g->row_ptr.end());
-    host.insert(host.end(), g->pe_row.begin(), g->pe_row.end());
-    host.insert(host.end(), g->pe_col.begin(), g->pe_col.end());
-    host.insert(host.end(), g->pe_shift.begin(), g->pe_shift.end());
-    host.insert(host.end(), g->col_ptr.begin(), g->col_ptr.end());
-    host.insert(host.end(), g->col_pe.begin(), g->col_pe.end());
-    // | pad to 16 B | vn_edge: per edge in column order, {C->V row base r0*z + (pe - r0), row
-    // degree, shift, 0} (the VN kernel's one scalar load per edge)
-    while (host.size() % 4) host.push_back(0);
-    const size_t off_vn = host.size();
-    for (int e = 0; e < g->E; ++e) {
-        const int pe = g->col_pe[e], i = g->pe_row[pe], r0 = g->row_ptr[i];
-        host.push_back(r0 * z + (pe - r0));
-        host.push_back(g->row_ptr[i + 1] - r0);
-        host.push_back(g->pe_shift[pe]);
-        host.push_back(0);
-    }
+    const host::GraphTables& h = g->h;
     {
         DeviceGuard dg(device);
-        if (dev_alloc(&g->d_tables, host.size()) != LDPC_OK) { delete g; return LDPC_ERR_OOM; }
-        if (hipMemcpy(g->d_tables, host.data(), host.size() * sizeof(int32_t),
+        if (dev_alloc(&g->d_tables, h.device_block.size()) != LDPC_OK) { delete g; return LDPC_ERR_OOM; }
+        if (hipMemcpy(g->d_tables, h.device_block.data(), h.device_block.size() * sizeof(int32_t),
                       hipMemcpyHostToDevice) != hipSuccess) {
             dev_free(g->d_tables);
             delete g;
@@ -280,17 +230,17 @@ int ldpc_graph_create(const int32_t* proto, int32_t M, int32_t N, int32_t z, int
         }
     }
     DevGraph& d = g->dev;
-    d.M = M; d.N = N; d.z = z; d.E = g->E;
-    d.n_checks = M * z; d.n_vars = N * z; d.n_edges = g->E * z; d.max_cdeg = g->max_cdeg;
+    d.M = M; d.N = N; d.z = z; d.E = h.E;
+    d.n_checks = M * z; d.n_vars = N * z; d.n_edges = h.E * z; d.max_cdeg = h.max_cdeg;
     const int32_t* p = g->d_tables;
     d.row_ptr = p; p += M + 1;
-    d.pe_row = p; p += g->E;
-    d.pe_col = p; p += g->E;
-    d.pe_shift = p; p += g->E;
+    d.pe_row = p; p += h.E;
+    d.pe_col = p; p += h.E;
+    d.pe_shift = p; p += h.E;
     d.col_ptr = p; p += N + 1;
     d.col_pe = p;
-    d.vn_edge = reinterpret_cast<const int4*>(g->d_tables + off_vn);
-    d.h_row_ptr = g->row_ptr.data();
+    d.vn_edge = reinterpret_cast<const int4*>(g->d_tables + h.off_vn);
+    d.h_row_ptr = h.row_ptr.data();
     *out = g;
     return LDPC_OK;
 }
@@ -309,21 +259,24 @@ int ldpc_graph_destroy(ldpc_graph* g) {
 
 int ldpc_graph_query(const ldpc_graph* g, int32_t* dims) {
     if (!g || !dims) return LDPC_ERR_ARG;
-    const int32_t v[8] = {g->M, g->N, g->z, g->E, g->M * g->z, g->N * g->z, g->E * g->z,
-                          g->max_cdeg};
+    const host::GraphTables& h = g->h;
+    const int32_t v[8] = {h.M, h.N, h.z, h.E, h.M * h.z, h.N * h.z, h.E * h.z, h.max_cdeg};
     std::memcpy(dims, v, sizeof(v));
     return LDPC_OK;
 }
 
 int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* alpha_ucn,
                      const float* beta) {
-    if (!g || T <= 0 || !alpha || !beta) return LDPC_ERR_ARG;
+    if (!g) return LDPC_ERR_ARG;
+    host::WeightInfo wi;
+    const int sta = host::analyze_weights(g->h, T, alpha, alpha_ucn, beta, wi);
+    if (sta != LDPC_OK) return sta;
     DeviceGuard dg(g->device);
     dev_free(g->d_alpha);
     dev_free(g->d_alpha_ucn);
     dev_free(g->d_beta);
     g->T_w = 0;
-    const size_t ne = (size_t)T * g->E, nn = (size_t)T * g->N;
+    const size_t ne = (size_t)T * g->h.E, nn = (size_t)T * g->h.N;
     int st = dev_alloc(&g->d_alpha, ne);
     if (st == LDPC_OK && alpha_ucn) st = dev_alloc(&g->d_alpha_ucn, ne);
     if (st == LDPC_OK) st = dev_alloc(&g->d_beta, nn);
@@ -335,34 +288,15 @@ int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* 
     ok = ok && hipMemcpy(g->d_beta, beta, nn * sizeof(float), hipMemcpyHostToDevice) == hipSuccess;
     if (!ok) return LDPC_ERR_HIP;
     g->T_w = T;
-    g->per_edge_w = 0;
-    for (int t = 0; t < T && !g->per_edge_w; ++t)
-        for (int i = 0; i < g->M && !g->per_edge_w; ++i)
-            for (int e = g->row_ptr[i] + 1; e < g->row_ptr[i + 1]; ++e) {
-                const size_t a0 = (size_t)t * g->E + g->row_ptr[i], a1 = (size_t)t * g->E + e;
-                if (alpha[a1] != alpha[a0] || (alpha_ucn && alpha_ucn[a1] != alpha_ucn[a0])) {
-                    g->per_edge_w = 1;
-                    break;
-                }
-            }
-    // rows that may share check groups in the fused kernel: equal degree, uniform weights
-    // inside the row (no per-edge weights) and the previous row's CN / UCN weights at every t
-    g->row_merge.assign(g->M, 0);
-    for (int i = 1; i < g->M && !g->per_edge_w; ++i) {
-        bool same = g->row_ptr[i + 1] - g->row_ptr[i] == g->row_ptr[i] - g->row_ptr[i - 1];
-        for (int t = 0; t < T && same; ++t) {
-            const size_t a0 = (size_t)t * g->E + g->row_ptr[i - 1], a1 = (size_t)t * g->E + g->row_ptr[i];
-            same = alpha[a1] == alpha[a0] && (!alpha_ucn || alpha_ucn[a1] == alpha_ucn[a0]);
-        }
-        g->row_merge[i] = same ? 1 : 0;
-    }
+    g->per_edge_w = wi.per_edge_w;
+    g->row_merge = wi.row_merge;
     g->dev.h_row_merge = nullptr;
     g->dev.row_merge = nullptr;
     if (!g->d_row_merge) {
-        const int st2 = dev_alloc(&g->d_row_merge, (size_t)g->M);
+        const int st2 = dev_alloc(&g->d_row_merge, (size_t)g->h.M);
         if (st2 != LDPC_OK) return st2;
     }
-    if (hipMemcpy(g->d_row_merge, g->row_merge.data(), (size_t)g->M * sizeof(int32_t),
+    if (hipMemcpy(g->d_row_merge, g->row_merge.data(), (size_t)g->h.M * sizeof(int32_t),
                   hipMemcpyHostToDevice) != hipSuccess)
         return LDPC_ERR_HIP;
     g->dev.h_row_merge = g->row_merge.data();
@@ -418,7 +352,7 @@ int ldpc_decode_awgn(ldpc_ctx* c, int64_t B, const ldpc_decode_params* p,
     if (st != LDPC_ERR_UNSUPPORTED) return st;
     // this kernel reads its LLRs: generate them into the context's buffer, then decode
     ldpc_graph* g = c->g;
-    const int64_t n = c->B_max * (int64_t)g->N * g->z;
+    const int64_t n = c->B_max * (int64_t)g->h.N * g->h.z;
     if (c->llr_scratch_n < n) {
         DeviceGuard dg(g->device);
         if (c->llr_scratch) (void)hipFree(c->llr_scratch);
@@ -432,7 +366,7 @@ int ldpc_decode_awgn(ldpc_ctx* c, int64_t B, const ldpc_decode_params* p,
     }
     {
         DeviceGuard dg(g->device);
-        st = ldpc_channel_awgn(c->llr_scratch, B, g->N * g->z, ch->sigma, ch->seed, ch->offset,
+        st = ldpc_channel_awgn(c->llr_scratch, B, g->h.N * g->h.z, ch->sigma, ch->seed, ch->offset,
                                p->decoding_type, p->q_bit, ch->punct_start, ch->punct_end,
                                ch->short_start, ch->short_end, p->clip_llr, stream);
     }
@@ -452,7 +386,7 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
     if (kern == LDPC_KERNEL_AUTO) kern = fok ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
     if (kern == LDPC_KERNEL_FUSED && !fok) return LDPC_ERR_UNSUPPORTED;
     if (kern != LDPC_KERNEL_FLOOD && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_ARG;
-    const int64_t nv = (int64_t)g->N * g->z, ne = (int64_t)g->E * g->z;
+    const int64_t nv = (int64_t)g->h.N * g->h.z, ne = (int64_t)g->h.E * g->h.z;
     int64_t bytes = 0;
     const char* nm = "";
     if (kern == LDPC_KERNEL_FLOOD) {
@@ -481,12 +415,10 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
                        const ldpc_decode_outputs* o, void* stream, const AwgnParams* gen) {
     if (!c || !p || (!llr_dev && !gen)) return LDPC_ERR_ARG;
     ldpc_graph* g = c->g;
-    if (B <= 0 || B > c->B_max || p->T <= 0 || p->T > c->T_max) return LDPC_ERR_STATE;
-    if (g->T_w < p->T || !g->d_alpha || !g->d_beta) return LDPC_ERR_STATE;
-    const int mode = mode_of(p->decoding_type, p->q_bit);
-    if (mode < 0) return LDPC_ERR_ARG;
-    if (p->target_bits <= 0 || p->target_bits > g->N * g->z) return LDPC_ERR_ARG;
-    if (!(p->clip_llr > 0.f)) return LDPC_ERR_ARG;
+    if (!g->d_alpha || !g->d_beta) return LDPC_ERR_STATE;
+    int mode = -1;
+    const int chk = host::check_decode(g->h, B, c->B_max, c->T_max, g->T_w, p, &mode);
+    if (chk != LDPC_OK) return chk;
     ldpc_decode_outputs none{};
     const ldpc_decode_outputs& out = o ? *o : none;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -506,7 +438,7 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     b.B = B;
     b.ntiles = ntiles;
     b.T = p->T;
-    b.n_vars = g->N * g->z;
+    b.n_vars = g->h.N * g->h.z;
     b.target_bits = p->target_bits;
     b.clip = p->clip_llr;
     b.alpha = g->d_alpha;
@@ -553,13 +485,13 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
         if (kern == LDPC_KERNEL_FUSED) fused_bits_view(c->fused, be);
         else { be.hd = c->hd; be.hd_all = 1; }
         if (out.hard_bits) {
-            const int nw = (g->N * g->z + 31) / 32;
+            const int nw = (g->h.N * g->h.z + 31) / 32;
             const int64_t total = (int64_t)p->T * B * nw;
             hipLaunchKernelGGL(k_export_hard, dim3((unsigned)std::min<int64_t>(4096, (total + 255) / 256)),
                                dim3(256), 0, s, be, out.hard_bits, p->T, nw);
         }
         if (out.synd_bits) {
-            const int nw = (g->M * g->z + 31) / 32;
+            const int nw = (g->h.M * g->h.z + 31) / 32;
             const int64_t total = (int64_t)p->T * B * nw;
             hipLaunchKernelGGL(k_export_synd, dim3((unsigned)std::min<int64_t>(4096, (total + 255) / 256)),
                                dim3(256), 0, s, g->dev, be, out.synd_bits, p->T, nw);

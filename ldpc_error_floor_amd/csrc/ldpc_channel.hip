@@ -48,8 +48,11 @@ extern "C" int ldpc_channel_awgn(float* llr_dev, int64_t B, int32_t n_vars, doub
                                  int32_t q_bit, int32_t punct_start, int32_t punct_end,
                                  int32_t short_start, int32_t short_end, float clip_llr,
                                  void* stream) {
-    if (!llr_dev || B <= 0 || n_vars <= 0 || !(sigma > 0.0) || offset < 0) return LDPC_ERR_ARG;
-    if (decoding_type == LDPC_DEC_QMS && ldpc::mode_of(decoding_type, q_bit) < 0) return LDPC_ERR_ARG;
+    if (!llr_dev) return LDPC_ERR_ARG;
+    const int chk = ldpc::host::check_channel(B, n_vars, sigma, offset, decoding_type, q_bit,
+                                              punct_start, punct_end, short_start, short_end,
+                                              clip_llr);
+    if (chk != LDPC_OK) return chk;
     const int64_t total = B * ((n_vars + 1) / 2);
     const unsigned grid = (unsigned)std::min<int64_t>(8192, (total + 255) / 256);
     const ldpc::AwgnParams a = ldpc::make_awgn(sigma, seed, offset, decoding_type, q_bit,

@@ -183,6 +183,16 @@ __device__ __forceinline__ uint32_t append_b1(uint32_t ng, uint32_t d) {
     return __builtin_amdgcn_perm(ng, d, 0x06050401u);
 }
 
+// the lane index, recomputed where it is used (2 VALU): volatile, so the compiler can neither
+// hoist it nor keep values derived from it live across the check phase, where the register
+// budget of the shape is exhausted and such values were spilled to scratch (one scratch store
+// per wave and block: the kernel's only HBM writes besides the counters)
+__device__ __forceinline__ uint32_t lane_fresh() {
+    uint32_t r;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(r));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t r;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -638,8 +648,9 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                 constexpr bool LAST = decltype(lastc)::value;
                 constexpr bool FULLT = decltype(fullc)::value;
                 constexpr bool ZUNI = decltype(zunic)::value;
-                const uint32_t* Wr = W + c_beg * 64 + lane;
-                const float* Cr = CH + c_beg * 64 + lane;
+                const int vl = (int)lane_fresh();
+                const uint32_t* Wr = W + c_beg * 64 + vl;
+                const float* Cr = CH + c_beg * 64 + vl;
                 for (int c = c_beg; c < c_end; c += 4, Wr += 256, Cr += 256) {
                     uint32_t wv[4];
                     float chv[4], bv[4];
@@ -652,7 +663,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                                 const uint32_t col = __umulhi((uint32_t)((c + j) * SLOTS), a.zmagic);
                                 bv[j] = bnext[__builtin_amdgcn_readfirstlane(col)];
                             } else {
-                                const uint32_t v = (uint32_t)((c + j) * 64 + lane) >> LOGCW;
+                                const uint32_t v = (uint32_t)((c + j) * 64 + vl) >> LOGCW;
                                 bv[j] = bnext[__umulhi(v, a.zmagic)];
                             }
                         }
@@ -673,7 +684,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                                 if (FULLT) {
                                     aor |= apph;
                                 } else {
-                                    const int v = ((c + j) * 64 + lane) >> LOGCW;
+                                    const int v = ((c + j) * 64 + vl) >> LOGCW;
                                     aor |= (v < tb) ? apph : 0u;
                                 }
                                 const float yb = __builtin_amdgcn_fmed3f(chv[j] * bv[j], -qmf, qmf);
@@ -692,7 +703,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
                             const int appb = qc + s;
                             int appt = appb;
                             if (!FULLT) {
-                                const int v = ((c + j) * 64 + lane) >> LOGCW;
+                                const int v = ((c + j) * 64 + vl) >> LOGCW;
                                 appt = (v < tb) ? appb : INT_MIN;
                             }
                             amax = max(amax, appt);
@@ -715,7 +726,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
             }
             // the partial last chunk (n_vars*CW not a multiple of 64), per-lane checks
             if (a.nfull * 64 < total && wave == (a.nfull / max(a.cpw, 1)) % NWV && !(a.ablate & 4)) {
-                const int e = a.nfull * 64 + lane;
+                const int e = a.nfull * 64 + (int)lane_fresh();
                 if (e < total) {
                     const uint32_t v = (uint32_t)e >> LOGCW;
                     const int s = (int)(W[e] & 0x7FFFu);

@@ -1,0 +1,130 @@
+// ldpc_host.cpp — host-only graph tables, weight analysis and argument validation of the C ABI
+// (see ldpc_host.h).  No HIP: built into libldpc_nms.so by hipcc and, for the sanitized check,
+// by g++ -fsanitize=address,undefined.
+#include "ldpc_host.h"
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+
+namespace ldpc {
+namespace host {
+
+int build_graph(const int32_t* proto, int32_t M, int32_t N, int32_t z, GraphTables& g) {
+    g = GraphTables{};
+    if (!proto || M <= 0 || N <= 0 || z <= 0) return LDPC_ERR_ARG;
+    // every lifted count the device code indexes with int: checks, variables, edges (<= M*N*z)
+    if ((int64_t)M * N * z > INT32_MAX) return LDPC_ERR_ARG;
+    g.M = M;
+    g.N = N;
+    g.z = z;
+    g.row_ptr.assign((size_t)M + 1, 0);
+    for (int i = 0; i < M; ++i)
+        for (int j = 0; j < N; ++j) {
+            const int32_t s = proto[(size_t)i * N + j];
+            if (s < -1) return LDPC_ERR_ARG;
+            if (s != -1) {
+                g.pe_row.push_back(i);
+                g.pe_col.push_back(j);
+                g.pe_shift.push_back(s % z);
+            }
+        }
+    g.E = (int)g.pe_row.size();
+    if (g.E == 0) return LDPC_ERR_ARG;
+    for (int e = 0; e < g.E; ++e) g.row_ptr[(size_t)g.pe_row[e] + 1]++;
+    for (int i = 0; i < M; ++i) {
+        g.max_cdeg = std::max(g.max_cdeg, g.row_ptr[(size_t)i + 1]);
+        g.row_ptr[(size_t)i + 1] += g.row_ptr[i];
+    }
+    if (g.max_cdeg > kMaxCheckDegree) return LDPC_ERR_UNSUPPORTED;
+    g.col_ptr.assign((size_t)N + 1, 0);
+    for (int e = 0; e < g.E; ++e) g.col_ptr[(size_t)g.pe_col[e] + 1]++;
+    for (int j = 0; j < N; ++j) {
+        g.max_vdeg = std::max(g.max_vdeg, g.col_ptr[(size_t)j + 1]);
+        g.col_ptr[(size_t)j + 1] += g.col_ptr[j];
+    }
+    g.col_pe.assign((size_t)g.E, 0);
+    {
+        std::vector<int32_t> fill(g.col_ptr.begin(), g.col_ptr.end() - 1);
+        for (int e = 0; e < g.E; ++e) g.col_pe[(size_t)fill[(size_t)g.pe_col[e]]++] = e;   // ascending row
+    }
+    std::vector<int32_t>& h = g.device_block;
+    h.insert(h.end(), g.row_ptr.begin(), g.row_ptr.end());
+    h.insert(h.end(), g.pe_row.begin(), g.pe_row.end());
+    h.insert(h.end(), g.pe_col.begin(), g.pe_col.end());
+    h.insert(h.end(), g.pe_shift.begin(), g.pe_shift.end());
+    h.insert(h.end(), g.col_ptr.begin(), g.col_ptr.end());
+    h.insert(h.end(), g.col_pe.begin(), g.col_pe.end());
+    while (h.size() % 4) h.push_back(0);
+    g.off_vn = h.size();
+    for (int e = 0; e < g.E; ++e) {
+        const int pe = g.col_pe[(size_t)e], i = g.pe_row[(size_t)pe], r0 = g.row_ptr[(size_t)i];
+        h.push_back(r0 * z + (pe - r0));
+        h.push_back(g.row_ptr[(size_t)i + 1] - r0);
+        h.push_back(g.pe_shift[(size_t)pe]);
+        h.push_back(0);
+    }
+    return LDPC_OK;
+}
+
+int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const float* alpha_ucn,
+                    const float* beta, WeightInfo& w) {
+    w = WeightInfo{};
+    if (T <= 0 || !alpha || !beta || g.E <= 0) return LDPC_ERR_ARG;
+    if ((int64_t)T * g.E > INT32_MAX || (int64_t)T * g.N > INT32_MAX) return LDPC_ERR_ARG;
+    for (int t = 0; t < T && !w.per_edge_w; ++t)
+        for (int i = 0; i < g.M && !w.per_edge_w; ++i)
+            for (int e = g.row_ptr[(size_t)i] + 1; e < g.row_ptr[(size_t)i + 1]; ++e) {
+                const size_t a0 = (size_t)t * g.E + g.row_ptr[(size_t)i], a1 = (size_t)t * g.E + e;
+                if (alpha[a1] != alpha[a0] || (alpha_ucn && alpha_ucn[a1] != alpha_ucn[a0])) {
+                    w.per_edge_w = 1;
+                    break;
+                }
+            }
+    w.row_merge.assign((size_t)g.M, 0);
+    for (int i = 1; i < g.M && !w.per_edge_w; ++i) {
+        const int deg = g.row_ptr[(size_t)i + 1] - g.row_ptr[(size_t)i];
+        bool same = deg == g.row_ptr[(size_t)i] - g.row_ptr[(size_t)i - 1];
+        // (an all -1 proto row has no weights to compare: row_ptr[i] may then be E, one past
+        // the last weight of the iteration — found by the sanitized host check)
+        for (int t = 0; t < T && same && deg > 0; ++t) {
+            const size_t a0 = (size_t)t * g.E + g.row_ptr[(size_t)i - 1];
+            const size_t a1 = (size_t)t * g.E + g.row_ptr[(size_t)i];
+            same = alpha[a1] == alpha[a0] && (!alpha_ucn || alpha_ucn[a1] == alpha_ucn[a0]);
+        }
+        w.row_merge[(size_t)i] = same ? 1 : 0;
+    }
+    return LDPC_OK;
+}
+
+int check_decode(const GraphTables& g, int64_t B, int64_t B_max, int32_t T_max, int32_t T_w,
+                 const ldpc_decode_params* p, int* mode) {
+    if (!p) return LDPC_ERR_ARG;
+    if (B <= 0 || B > B_max || p->T <= 0 || p->T > T_max) return LDPC_ERR_STATE;
+    if (T_w < p->T) return LDPC_ERR_STATE;
+    const int m = mode_of(p->decoding_type, p->q_bit);
+    if (m < 0) return LDPC_ERR_ARG;
+    if (p->target_bits <= 0 || p->target_bits > g.N * g.z) return LDPC_ERR_ARG;
+    if (!(p->clip_llr > 0.f) || !std::isfinite(p->clip_llr)) return LDPC_ERR_ARG;
+    if (p->kernel != LDPC_KERNEL_AUTO && p->kernel != LDPC_KERNEL_FLOOD &&
+        p->kernel != LDPC_KERNEL_FUSED)
+        return LDPC_ERR_ARG;
+    if (mode) *mode = m;
+    return LDPC_OK;
+}
+
+int check_channel(int64_t B, int32_t n_vars, double sigma, int64_t offset, int32_t decoding_type,
+                  int32_t q_bit, int32_t punct_start, int32_t punct_end, int32_t short_start,
+                  int32_t short_end, float clip_llr) {
+    if (B <= 0 || n_vars <= 0 || !(sigma > 0.0) || !std::isfinite(sigma) || offset < 0)
+        return LDPC_ERR_ARG;
+    if (mode_of(decoding_type, q_bit) < 0) return LDPC_ERR_ARG;
+    if (punct_start < 0 || short_start < 0) return LDPC_ERR_ARG;
+    if (punct_start > 0 && punct_end < punct_start) return LDPC_ERR_ARG;
+    if (short_start > 0 && short_end < short_start) return LDPC_ERR_ARG;
+    if (!(clip_llr > 0.f) || !std::isfinite(clip_llr)) return LDPC_ERR_ARG;
+    return LDPC_OK;
+}
+
+}  // namespace host
+}  // namespace ldpc

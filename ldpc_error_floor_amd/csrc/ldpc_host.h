@@ -1,0 +1,86 @@
+// ldpc_host.h — the host-only half of the C ABI: graph tables, weight analysis and argument
+// validation.  Plain C++17 with no HIP dependency, so that it builds with g++ under
+// -fsanitize=address,undefined (tests/native/host_check.cpp, tests/test_host_sanitized.py) and
+// is the same code ldpc_capi.hip runs before it touches the device.
+//
+// What it replaces in the reference: init_parameter / init_connecting_matrix
+// (Main_Functions.py:8-150) build the lifted Tanner graph as dense (E z)^2 matrices; here the
+// same graph is a row-major proto-edge list E(C) (the weight order, :69-71) with CSR offsets
+// per proto row and column.  check_params (:498-523) is the reference's only validation; the
+// decode-argument checks below are the ABI's own.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "ldpc_nms.h"
+
+namespace ldpc {
+
+// decoding modes (decoding_type x q_bit)
+enum Mode : int { MODE_Q6 = 0, MODE_Q5, MODE_QM5, MODE_Q4, MODE_Q3, MODE_MS, MODE_MSNN, MODE_SP };
+constexpr bool mode_is_qms(int m) { return m >= 0 && m <= MODE_Q3; }
+
+inline int mode_of(int decoding_type, int q_bit) {
+    if (decoding_type == LDPC_DEC_SP) return MODE_SP;
+    if (decoding_type == LDPC_DEC_MS) return MODE_MS;
+    if (decoding_type == LDPC_DEC_MS_NONUDGE) return MODE_MSNN;
+    if (decoding_type != LDPC_DEC_QMS) return -1;
+    switch (q_bit) {
+        case 6: return MODE_Q6;
+        case 5: return MODE_Q5;
+        case -5: return MODE_QM5;
+        case 4: return MODE_Q4;
+        case 3: return MODE_Q3;
+        default: return -1;
+    }
+}
+
+namespace host {
+
+constexpr int kMaxCheckDegree = 64;
+
+// Lifted graph of a QC proto matrix (-1 = no edge, else cyclic shift, taken mod z).
+struct GraphTables {
+    int M = 0, N = 0, z = 0, E = 0;
+    int max_cdeg = 0, max_vdeg = 0;
+    std::vector<int32_t> row_ptr;    // [M+1] proto edges of row i: row_ptr[i] .. row_ptr[i+1]-1
+    std::vector<int32_t> pe_row;     // [E] E(C) order (row-major)
+    std::vector<int32_t> pe_col;     // [E]
+    std::vector<int32_t> pe_shift;   // [E] P[i,j] mod z
+    std::vector<int32_t> col_ptr;    // [N+1]
+    std::vector<int32_t> col_pe;     // [E] proto edges of each column, ascending row
+    // the device image: row_ptr | pe_row | pe_col | pe_shift | col_ptr | col_pe | pad to 16 B |
+    // vn_edge [E] int4 {r0*z + (pe - r0), row degree, shift, 0} in column order
+    std::vector<int32_t> device_block;
+    size_t off_vn = 0;               // int32 offset of vn_edge inside device_block
+};
+
+// LDPC_OK, LDPC_ERR_ARG (null / non-positive sizes / entry < -1 / no edge / sizes whose lifted
+// counts overflow int32) or LDPC_ERR_UNSUPPORTED (check degree above kMaxCheckDegree).
+int build_graph(const int32_t* proto, int32_t M, int32_t N, int32_t z, GraphTables& out);
+
+// Per-iteration weight tables alpha [T][E], alpha_ucn [T][E] or null, beta [T][N]:
+// per_edge_w = some row's CN / UCN weights differ inside the row at some t (sharing 1 / 4);
+// row_merge[i] = row i may share fused-kernel check groups with row i-1 (equal degree, uniform
+// row weights, the previous row's weights at every t).
+struct WeightInfo {
+    int per_edge_w = 0;
+    std::vector<int32_t> row_merge;
+};
+int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const float* alpha_ucn,
+                    const float* beta, WeightInfo& out);
+
+// ldpc_decode / ldpc_decode_awgn argument checks.  Returns LDPC_OK and the mode, or the status
+// the ABI reports: LDPC_ERR_ARG (null params, bad mode, target_bits, clip_llr, kernel) or
+// LDPC_ERR_STATE (B or T outside the context limits, weights missing or shorter than T).
+int check_decode(const GraphTables& g, int64_t B, int64_t B_max, int32_t T_max, int32_t T_w,
+                 const ldpc_decode_params* p, int* mode);
+
+// ldpc_channel_awgn argument checks (LDPC_OK or LDPC_ERR_ARG).
+int check_channel(int64_t B, int32_t n_vars, double sigma, int64_t offset, int32_t decoding_type,
+                  int32_t q_bit, int32_t punct_start, int32_t punct_end, int32_t short_start,
+                  int32_t short_end, float clip_llr);
+
+}  // namespace host
+}  // namespace ldpc

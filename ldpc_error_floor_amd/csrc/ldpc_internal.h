@@ -3,31 +3,13 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "ldpc_host.h"
 #include "ldpc_nms.h"
 
 namespace ldpc {
 
 constexpr int TILE = 256;          // codewords per tile: 64 lanes x float4
 constexpr int VN_PER_WAVE = 8;     // variables handled by one wave in vn_update
-
-// decoding modes (decoding_type x q_bit)
-enum Mode : int { MODE_Q6 = 0, MODE_Q5, MODE_QM5, MODE_Q4, MODE_Q3, MODE_MS, MODE_MSNN, MODE_SP };
-__host__ __device__ constexpr bool mode_is_qms(int m) { return m <= MODE_Q3; }
-
-inline int mode_of(int decoding_type, int q_bit) {
-    if (decoding_type == LDPC_DEC_SP) return MODE_SP;
-    if (decoding_type == LDPC_DEC_MS) return MODE_MS;
-    if (decoding_type == LDPC_DEC_MS_NONUDGE) return MODE_MSNN;
-    if (decoding_type != LDPC_DEC_QMS) return -1;
-    switch (q_bit) {
-        case 6: return MODE_Q6;
-        case 5: return MODE_Q5;
-        case -5: return MODE_QM5;
-        case 4: return MODE_Q4;
-        case 3: return MODE_Q3;
-        default: return -1;
-    }
-}
 
 // Graph tables on the device (E(C) = row-major proto-edge order).
 struct DevGraph {

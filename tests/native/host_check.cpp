@@ -1,0 +1,218 @@
+// host_check.cpp — drives the host-only half of the C ABI (ldpc_host.cpp: graph tables, weight
+// analysis, argument validation) under -fsanitize=address,undefined on the CPU.
+// Built and run by tests/test_host_sanitized.py; test infrastructure, not product code.
+//
+//   host_check selftest              argument-validation cases + randomized graphs / weights
+//   host_check tables FILE Z         the tables of a BaseGraph/*.txt proto as JSON on stdout
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <limits>
+#include <random>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "ldpc_host.h"
+
+using namespace ldpc;
+
+static int failures = 0;
+#define CHECK(cond)                                                              \
+    do {                                                                         \
+        if (!(cond)) {                                                           \
+            std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+            ++failures;                                                          \
+        }                                                                        \
+    } while (0)
+
+// structural invariants of a built graph against the proto matrix it came from
+static void check_tables(const std::vector<int32_t>& P, int M, int N, int z, const host::GraphTables& g) {
+    int E = 0;
+    for (int v : P) E += v != -1;
+    CHECK(g.E == E && g.M == M && g.N == N && g.z == z);
+    CHECK((int)g.row_ptr.size() == M + 1 && g.row_ptr[0] == 0 && g.row_ptr[M] == E);
+    CHECK((int)g.col_ptr.size() == N + 1 && g.col_ptr[0] == 0 && g.col_ptr[N] == E);
+    int e = 0, maxc = 0, maxv = 0;
+    for (int i = 0; i < M; ++i) {
+        CHECK(g.row_ptr[i] <= g.row_ptr[i + 1]);
+        maxc = std::max(maxc, g.row_ptr[i + 1] - g.row_ptr[i]);
+        for (int j = 0; j < N; ++j) {
+            const int s = P[(size_t)i * N + j];
+            if (s == -1) continue;
+            CHECK(g.pe_row[e] == i && g.pe_col[e] == j && g.pe_shift[e] == s % z);
+            CHECK(g.pe_shift[e] >= 0 && g.pe_shift[e] < z);
+            ++e;
+        }
+    }
+    for (int j = 0; j < N; ++j) {
+        maxv = std::max(maxv, g.col_ptr[j + 1] - g.col_ptr[j]);
+        for (int k = g.col_ptr[j]; k < g.col_ptr[j + 1]; ++k) {
+            const int pe = g.col_pe[k];
+            CHECK(pe >= 0 && pe < E && g.pe_col[pe] == j);
+            if (k > g.col_ptr[j]) CHECK(g.pe_row[g.col_pe[k - 1]] < g.pe_row[pe]);
+        }
+    }
+    CHECK(g.max_cdeg == maxc && g.max_vdeg == maxv);
+    CHECK(g.off_vn % 4 == 0 && g.device_block.size() == g.off_vn + 4 * (size_t)E);
+    for (int k = 0; k < E; ++k) {
+        const int32_t* q = g.device_block.data() + g.off_vn + 4 * (size_t)k;
+        const int pe = g.col_pe[k], i = g.pe_row[pe], r0 = g.row_ptr[i];
+        CHECK(q[0] == r0 * z + (pe - r0) && q[1] == g.row_ptr[i + 1] - r0 && q[2] == g.pe_shift[pe] && q[3] == 0);
+    }
+}
+
+static void validation_cases() {
+    host::GraphTables g;
+    const int32_t p4[4] = {0, -1, 1, 0};
+    CHECK(host::build_graph(nullptr, 2, 2, 4, g) == LDPC_ERR_ARG);
+    CHECK(host::build_graph(p4, 0, 2, 4, g) == LDPC_ERR_ARG);
+    CHECK(host::build_graph(p4, 2, -1, 4, g) == LDPC_ERR_ARG);
+    CHECK(host::build_graph(p4, 2, 2, 0, g) == LDPC_ERR_ARG);
+    const int32_t bad[4] = {-3, -1, 1, 0};
+    CHECK(host::build_graph(bad, 2, 2, 4, g) == LDPC_ERR_ARG);
+    const int32_t none[4] = {-1, -1, -1, -1};
+    CHECK(host::build_graph(none, 2, 2, 4, g) == LDPC_ERR_ARG);
+    // lifted sizes beyond int32 are refused (M*N*z bounds the edge count)
+    CHECK(host::build_graph(p4, 2, 2, 1 << 29, g) == LDPC_ERR_ARG);
+    CHECK(host::build_graph(p4, 2, 2, INT32_MAX, g) == LDPC_ERR_ARG);
+    // check degree 65 > 64
+    std::vector<int32_t> wide(65, 0);
+    CHECK(host::build_graph(wide.data(), 1, 65, 1, g) == LDPC_ERR_UNSUPPORTED);
+    std::vector<int32_t> w64(64, 3);
+    CHECK(host::build_graph(w64.data(), 1, 64, 2, g) == LDPC_OK);
+    check_tables(w64, 1, 64, 2, g);
+    CHECK(host::build_graph(p4, 2, 2, 4, g) == LDPC_OK);
+    check_tables(std::vector<int32_t>(p4, p4 + 4), 2, 2, 4, g);
+
+    // weights
+    host::WeightInfo wi;
+    std::vector<float> a(3 * g.E, 0.75f), b(3 * g.N, 1.0f);
+    CHECK(host::analyze_weights(g, 0, a.data(), nullptr, b.data(), wi) == LDPC_ERR_ARG);
+    CHECK(host::analyze_weights(g, 3, nullptr, nullptr, b.data(), wi) == LDPC_ERR_ARG);
+    CHECK(host::analyze_weights(g, 3, a.data(), nullptr, nullptr, wi) == LDPC_ERR_ARG);
+    CHECK(host::analyze_weights(g, INT32_MAX, a.data(), nullptr, b.data(), wi) == LDPC_ERR_ARG);
+    CHECK(host::analyze_weights(g, 3, a.data(), nullptr, b.data(), wi) == LDPC_OK);
+    CHECK(wi.per_edge_w == 0 && (int)wi.row_merge.size() == g.M);
+
+    // decode parameters
+    ldpc_decode_params p{};
+    p.T = 3; p.decoding_type = LDPC_DEC_QMS; p.q_bit = 5; p.target_bits = g.N * g.z;
+    p.clip_llr = 20.f; p.kernel = LDPC_KERNEL_AUTO;
+    int mode = -1;
+    CHECK(host::check_decode(g, 10, 16, 5, 3, &p, &mode) == LDPC_OK && mode == MODE_Q5);
+    CHECK(host::check_decode(g, 10, 16, 5, 3, nullptr, &mode) == LDPC_ERR_ARG);
+    CHECK(host::check_decode(g, 0, 16, 5, 3, &p, &mode) == LDPC_ERR_STATE);
+    CHECK(host::check_decode(g, 17, 16, 5, 3, &p, &mode) == LDPC_ERR_STATE);
+    CHECK(host::check_decode(g, 10, 16, 2, 3, &p, &mode) == LDPC_ERR_STATE);   // T > T_max
+    CHECK(host::check_decode(g, 10, 16, 5, 2, &p, &mode) == LDPC_ERR_STATE);   // T > T_w
+    ldpc_decode_params q = p;
+    q.q_bit = 7;
+    CHECK(host::check_decode(g, 10, 16, 5, 3, &q, &mode) == LDPC_ERR_ARG);
+    q = p; q.decoding_type = 9;
+    CHECK(host::check_decode(g, 10, 16, 5, 3, &q, &mode) == LDPC_ERR_ARG);
+    q = p; q.target_bits = g.N * g.z + 1;
+    CHECK(host::check_decode(g, 10, 16, 5, 3, &q, &mode) == LDPC_ERR_ARG);
+    q = p; q.target_bits = 0;
+    CHECK(host::check_decode(g, 10, 16, 5, 3, &q, &mode) == LDPC_ERR_ARG);
+    q = p; q.clip_llr = std::numeric_limits<float>::quiet_NaN();
+    CHECK(host::check_decode(g, 10, 16, 5, 3, &q, &mode) == LDPC_ERR_ARG);
+    q = p; q.clip_llr = std::numeric_limits<float>::infinity();
+    CHECK(host::check_decode(g, 10, 16, 5, 3, &q, &mode) == LDPC_ERR_ARG);
+    q = p; q.kernel = 3;
+    CHECK(host::check_decode(g, 10, 16, 5, 3, &q, &mode) == LDPC_ERR_ARG);
+    q = p; q.decoding_type = LDPC_DEC_SP; q.q_bit = 99;     // q_bit is ignored outside QMS
+    CHECK(host::check_decode(g, 10, 16, 5, 3, &q, &mode) == LDPC_OK && mode == MODE_SP);
+
+    // channel parameters
+    CHECK(host::check_channel(4, 10, 0.5, 0, 2, 5, 0, 0, 0, 0, 20.f) == LDPC_OK);
+    CHECK(host::check_channel(0, 10, 0.5, 0, 2, 5, 0, 0, 0, 0, 20.f) == LDPC_ERR_ARG);
+    CHECK(host::check_channel(4, 0, 0.5, 0, 2, 5, 0, 0, 0, 0, 20.f) == LDPC_ERR_ARG);
+    CHECK(host::check_channel(4, 10, 0.0, 0, 2, 5, 0, 0, 0, 0, 20.f) == LDPC_ERR_ARG);
+    CHECK(host::check_channel(4, 10, std::nan(""), 0, 2, 5, 0, 0, 0, 0, 20.f) == LDPC_ERR_ARG);
+    CHECK(host::check_channel(4, 10, 0.5, -1, 2, 5, 0, 0, 0, 0, 20.f) == LDPC_ERR_ARG);
+    CHECK(host::check_channel(4, 10, 0.5, 0, 2, 2, 0, 0, 0, 0, 20.f) == LDPC_ERR_ARG);
+    CHECK(host::check_channel(4, 10, 0.5, 0, 5, 5, 0, 0, 0, 0, 20.f) == LDPC_ERR_ARG);
+    CHECK(host::check_channel(4, 10, 0.5, 0, 2, 5, 5, 3, 0, 0, 20.f) == LDPC_ERR_ARG);
+    CHECK(host::check_channel(4, 10, 0.5, 0, 2, 5, 0, 0, -1, 0, 20.f) == LDPC_ERR_ARG);
+    CHECK(host::check_channel(4, 10, 0.5, 0, 2, 5, 1, 2, 3, 4, 0.f) == LDPC_ERR_ARG);
+}
+
+// randomized protos (including empty rows / columns, shifts >= z, z = 1) and weight tables
+static void fuzz(int rounds) {
+    std::mt19937 rng(20251016);
+    for (int r = 0; r < rounds; ++r) {
+        const int M = 1 + rng() % 12, N = 1 + rng() % 40, z = 1 + rng() % 80;
+        const double dens = (rng() % 100) / 100.0;
+        std::vector<int32_t> P((size_t)M * N);
+        for (auto& v : P) v = (rng() % 1000) / 1000.0 < dens ? (int32_t)(rng() % 400) : -1;
+        host::GraphTables g;
+        const int st = host::build_graph(P.data(), M, N, z, g);
+        int E = 0;
+        for (int v : P) E += v != -1;
+        if (E == 0) { CHECK(st == LDPC_ERR_ARG); continue; }
+        CHECK(st == LDPC_OK);
+        if (st != LDPC_OK) continue;
+        check_tables(P, M, N, z, g);
+        const int T = 1 + rng() % 6;
+        std::vector<float> a((size_t)T * g.E), u((size_t)T * g.E), b((size_t)T * g.N, 1.f);
+        const bool per_row = rng() % 2;
+        for (int t = 0; t < T; ++t)
+            for (int e = 0; e < g.E; ++e) {
+                const float w = per_row ? 0.5f + 0.01f * (float)(g.pe_row[e] % 3) : 0.5f + 0.01f * (float)(rng() % 50);
+                a[(size_t)t * g.E + e] = w;
+                u[(size_t)t * g.E + e] = w * 0.5f;
+            }
+        host::WeightInfo wi;
+        CHECK(host::analyze_weights(g, T, a.data(), (rng() % 2) ? u.data() : nullptr, b.data(), wi) == LDPC_OK);
+        CHECK((int)wi.row_merge.size() == M);
+        if (per_row) CHECK(wi.per_edge_w == 0);
+        for (int i = 1; i < M; ++i)
+            if (wi.row_merge[i])
+                CHECK(g.row_ptr[i + 1] - g.row_ptr[i] == g.row_ptr[i] - g.row_ptr[i - 1]);
+    }
+}
+
+static int tables(const char* path, int z) {
+    std::ifstream f(path);
+    std::vector<int32_t> P;
+    std::string line;
+    int M = 0, N = -1;
+    while (std::getline(f, line)) {
+        std::istringstream ss(line);
+        int v, n = 0;
+        while (ss >> v) { P.push_back(v); ++n; }
+        if (n == 0) continue;
+        if (N < 0) N = n;
+        if (n != N) { std::fprintf(stderr, "ragged proto\n"); return 2; }
+        ++M;
+    }
+    host::GraphTables g;
+    const int st = host::build_graph(P.data(), M, N, z, g);
+    if (st != LDPC_OK) { std::printf("{\"status\": %d}\n", st); return 0; }
+    check_tables(P, M, N, z, g);
+    auto arr = [](const std::vector<int32_t>& v) {
+        std::string s = "[";
+        for (size_t i = 0; i < v.size(); ++i) s += (i ? "," : "") + std::to_string(v[i]);
+        return s + "]";
+    };
+    std::printf("{\"status\": 0, \"M\": %d, \"N\": %d, \"E\": %d, \"max_cdeg\": %d, \"max_vdeg\": %d, "
+                "\"row_ptr\": %s, \"pe_col\": %s, \"pe_shift\": %s, \"col_ptr\": %s, \"col_pe\": %s}\n",
+                g.M, g.N, g.E, g.max_cdeg, g.max_vdeg, arr(g.row_ptr).c_str(), arr(g.pe_col).c_str(),
+                arr(g.pe_shift).c_str(), arr(g.col_ptr).c_str(), arr(g.col_pe).c_str());
+    return failures ? 1 : 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc >= 4 && std::string(argv[1]) == "tables") return tables(argv[2], std::atoi(argv[3]));
+    if (argc >= 2 && std::string(argv[1]) == "selftest") {
+        validation_cases();
+        fuzz(argc >= 3 ? std::atoi(argv[2]) : 3000);
+        std::printf("host_check: %d failures\n", failures);
+        return failures ? 1 : 0;
+    }
+    std::fprintf(stderr, "usage: host_check selftest [rounds] | tables FILE Z\n");
+    return 2;
+}
