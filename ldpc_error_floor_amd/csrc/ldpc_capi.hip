@@ -241,6 +241,7 @@ int ldpc_graph_create(const int32_t* proto, int32_t M, int32_t N, int32_t z, int
     d.col_pe = p;
     d.vn_edge = reinterpret_cast<const int4*>(g->d_tables + h.off_vn);
     d.h_row_ptr = h.row_ptr.data();
+    d.host = &g->h;
     *out = g;
     return LDPC_OK;
 }
@@ -401,7 +402,7 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
         nm = "flood";
     } else {
         bytes = fused_bytes_per_cw(g->dev, p->T);
-        nm = fused_kernel_name(g->dev, mode, p->T, p->clip_llr);
+        nm = fused_kernel_name(g->dev, mode, p->T, p->clip_llr, ucn, g->per_edge_w != 0);
     }
     if (bytes_per_cw) *bytes_per_cw = bytes;
     if (name && name_len > 0) {

@@ -9,6 +9,11 @@ struct FusedWorkspace {
     int64_t hd_elems = 0;
     void* tables = nullptr;        // per-decode tables shared by all workgroups (v5)
     size_t tables_bytes = 0;
+    void* bs_graph = nullptr;      // bit-sliced kernel: graph tables (built once per context)
+    void* bs_lut = nullptr;        // bit-sliced kernel: per-decode weight tables
+    size_t bs_lut_bytes = 0;
+    uint32_t* bs_bad = nullptr;    // [packs] 1: pack decoded by the v5 fixup
+    int64_t bs_bad_n = 0;
 };
 
 // fused v5 serves this request (QMS q in {5,-5,4,3}, clip_llr on the grid, a shape fits)
@@ -18,14 +23,25 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
                  bool ucn, bool want_bits, int ntiles_max, int T_max, int per_edge_w,
                  int64_t* counters, uint8_t* flags, hipStream_t s);
 void fused_bits_view(const FusedWorkspace& ws, Bufs& b);
-const char* fused_kernel_name(const DevGraph& g, int mode, int T, float clip_llr);
+const char* fused_kernel_name(const DevGraph& g, int mode, int T, float clip_llr, bool ucn,
+                              bool per_edge_w);
 
 // v5 (ldpc_fused5.hip): byte-packed check state, default when a shape fits
 bool fused5_supported(const DevGraph& g, int T);
 const char* fused5_shape_name(const DevGraph& g, int T);
+// only: null, or per-32-codeword pack flags: decode just the blocks of flagged packs (the
+// bit-sliced kernel's fixup; needs a shape with CW <= 32, fused5_cw)
 int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr,
                   int qmax, float step, int clip_u, bool per_edge_w, uint64_t* hd_out,
-                  int64_t* counters, uint8_t* flags, hipStream_t s);
+                  int64_t* counters, uint8_t* flags, hipStream_t s, const uint32_t* only = nullptr);
+int fused5_cw(const DevGraph& g, int T);
+
+// bit-sliced (ldpc_bs.hip): 32 codewords per word, counters / flags only, QMS q = 5 / -5
+bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w);
+const char* bs_kernel_name(const DevGraph& g);
+int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
+              bool arow_uniform, bool bcol_uniform, int64_t* counters, uint8_t* flags,
+              uint32_t* bad, hipStream_t s);
 void fused_free(FusedWorkspace& ws);
 
 }  // namespace ldpc

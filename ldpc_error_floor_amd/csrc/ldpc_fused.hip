@@ -7,6 +7,7 @@
 // plan5 can map to a shape; everything else (q = 6, the float modes, graphs no shape fits, a
 // clip_LLR off the quantizer grid) is the flood kernel's, which the AUTO selection falls back
 // to.  There are no other fused variants: only kernels with parity tests can be selected.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
@@ -46,8 +47,17 @@ bool fused_supported(const DevGraph& g, int mode, int T, float clip_llr) {
     return fused5_supported(g, T);
 }
 
-const char* fused_kernel_name(const DevGraph& g, int mode, int T, float clip_llr) {
+// counters-only decodes (throughput mode) run the bit-sliced kernel when it applies
+static bool use_bs(const DevGraph& g, int mode, int T, bool ucn, bool per_edge_w) {
+    const int cw = fused5_cw(g, T);
+    return cw > 0 && cw <= 32 && bs_supported(g, mode, ucn, per_edge_w);
+}
+
+// the kernel a counters-only decode runs (the throughput / roofline report)
+const char* fused_kernel_name(const DevGraph& g, int mode, int T, float clip_llr, bool ucn,
+                              bool per_edge_w) {
     if (!fused_supported(g, mode, T, clip_llr)) return "";
+    if (use_bs(g, mode, T, ucn, per_edge_w)) return bs_kernel_name(g);
     return fused5_shape_name(g, T);
 }
 
@@ -81,6 +91,25 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
             return LDPC_ERR_HIP;
         hd_out = ws.hd;
     }
+    if (!want_bits && !b.app_out && !b.awgn && use_bs(g, mode, b.T, ucn, per_edge_w != 0)) {
+        // bit-sliced kernel; packs whose LLRs are off the quantizer grid go to the v5 kernel
+        const int64_t npk = (b.B + 31) / 32;
+        if (npk > ws.bs_bad_n) {
+            if (ws.bs_bad) (void)hipFree(ws.bs_bad);
+            ws.bs_bad = nullptr;
+            ws.bs_bad_n = 0;
+            const int64_t n = std::max<int64_t>(npk, (int64_t)(ntiles_max) * 8);
+            if (hipMalloc(reinterpret_cast<void**>(&ws.bs_bad), (size_t)n * 4) != hipSuccess) {
+                (void)hipGetLastError();
+                return LDPC_ERR_OOM;
+            }
+            ws.bs_bad_n = n;
+        }
+        int st = bs_decode(g, b, ws, llr, mode, false, false, counters, flags, ws.bs_bad, s);
+        if (st != LDPC_OK) return st;
+        return fused5_decode(g, b, ws, llr, mode_qmax(mode), step, cu, per_edge_w != 0, nullptr,
+                             counters, flags, s, ws.bs_bad);
+    }
     return fused5_decode(g, b, ws, llr, mode_qmax(mode), step, cu, per_edge_w != 0, hd_out,
                          counters, flags, s);
 }
@@ -97,6 +126,14 @@ void fused_free(FusedWorkspace& ws) {
     if (ws.tables) (void)hipFree(ws.tables);
     ws.tables = nullptr;
     ws.tables_bytes = 0;
+    if (ws.bs_graph) (void)hipFree(ws.bs_graph);
+    ws.bs_graph = nullptr;
+    if (ws.bs_lut) (void)hipFree(ws.bs_lut);
+    ws.bs_lut = nullptr;
+    ws.bs_lut_bytes = 0;
+    if (ws.bs_bad) (void)hipFree(ws.bs_bad);
+    ws.bs_bad = nullptr;
+    ws.bs_bad_n = 0;
 }
 
 }  // namespace ldpc

@@ -245,9 +245,14 @@ const char* fused5_shape_name(const DevGraph& g, int T) {
     return buf;
 }
 
+int fused5_cw(const DevGraph& g, int T) {
+    const Plan5 p = plan5(g, T);
+    return p.shape < 0 ? 0 : kShapes5[p.shape].cw;
+}
+
 int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr,
                   int qmax, float step, int clip_u, bool per_edge_w, uint64_t* hd_out,
-                  int64_t* counters, uint8_t* flags, hipStream_t s) {
+                  int64_t* counters, uint8_t* flags, hipStream_t s, const uint32_t* only) {
     Plan5 p = plan5(g, b.T);
     if (p.shape < 0 || qmax > 31) return LDPC_ERR_UNSUPPORTED;   // pass 1's 8-bit V->C range
     const Shape5& sh = kShapes5[p.shape];
@@ -295,6 +300,7 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
         a.awgn = *reinterpret_cast<const AwgnParams*>(b.awgn);
     }
     a.zmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.z - 1) / (uint64_t)g.z);
+    a.only = only;
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // timing only
     // shared tables: one small launch per decode instead of per-workgroup dependent loads
     const size_t nqt = (size_t)b.T * qslice;

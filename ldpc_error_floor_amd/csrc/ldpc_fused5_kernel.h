@@ -107,6 +107,7 @@ struct F5Args {
     AwgnParams awgn;
     uint32_t zmagic;
     int ablate;        // diagnostic only (LDPC_DIAG_ABLATE): 1 skip CN pass 1, 2 skip pass 2, 4 skip VN
+    const uint32_t* only;  // null, or [packs of 32 codewords]: decode only blocks of flagged packs
 };
 
 __device__ __forceinline__ int q_units5(float x, float inv, int qmax) {
@@ -262,6 +263,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     uint16_t* QT = reinterpret_cast<uint16_t*>(RED + 8);                          // [2][qslice]
 
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();   // edge addresses are LDS-absolute
+    if (a.only && a.only[((int64_t)blockIdx.x * CW) >> 5] == 0u) return;   // bit-sliced fixup
     const int tid = threadIdx.x;
     const int NT = blockDim.x;
     const int NWV = NT >> 6;

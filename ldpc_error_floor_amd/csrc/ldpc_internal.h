@@ -27,6 +27,7 @@ struct DevGraph {
     // ldpc_weights_set): host copy for planning, device copy for the address tables
     const int32_t* h_row_merge;
     const int32_t* row_merge;
+    const host::GraphTables* host;   // host tables (ldpc_host.h)
 };
 
 // Per-decode buffers and scalars.

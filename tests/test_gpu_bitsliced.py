@@ -1,0 +1,73 @@
+"""The bit-sliced fused kernel (csrc/ldpc_bs.hip: 32 codewords per 32-bit word) that serves
+counters-only QMS decodes (GPU only).  Its counters and per-frame flags must equal the flood
+kernel's (pinned to the reference fixtures) bit for bit: on ragged batches, with per-row /
+per-column weights, for q = 5 and q = -5, and with LLRs off the quantizer grid (those packs are
+decoded by the v5 kernel instead, so the result stays exact for any input)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+DATA = os.path.join(ROOT, "ldpc_error_floor_amd", "data")
+
+
+def _wman(device, sharing=(3, 0, 3), q=5, T=20, seed=3):
+    from ldpc_error_floor_amd.code import CodeParams, TannerGraph, load_base_graph
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    from ldpc_error_floor_amd.weights import expand_weights, read_weight_file
+    proto = load_base_graph(os.path.join(DATA, "BaseGraph", "wman_N0576_R34_z24.txt"))
+    g = TannerGraph(proto, 24)
+    if sharing == (3, 0, 3):
+        wf = read_weight_file(os.path.join(DATA, "Weights",
+                                           "C0_wman_N0576_R34_z24_Opt_Weight_End20.txt"))
+        W = expand_weights(sharing, {0: wf.blocks[0], 2: wf.blocks[2]}, T, g)
+    else:
+        rng = np.random.RandomState(seed)
+        rows = {0: rng.uniform(0.5, 1.2, (T, g.M)), 2: rng.uniform(0.6, 1.3, (T, g.N))}
+        W = expand_weights(sharing, rows, T, g)
+    return NMSDecoder(proto, 24, W, 2, q, device=device), CodeParams(proto, 24)
+
+
+def _both(dec, llr):
+    out = {}
+    for k in ("flood", "fused"):
+        r = dec.decode(llr, app=False, counters=True, flags=True, kernel=k)
+        out[k] = (r.counters.cpu().numpy(), r.flags.cpu().numpy())
+    return out
+
+
+@pytest.mark.parametrize("B", [1, 31, 33, 3001, 40000])
+def test_bitsliced_equals_flood(cuda_device, B):
+    dec, cp = _wman(cuda_device)
+    assert dec.kernel_info()[1].startswith("bsl"), dec.kernel_info()
+    llr = dec.awgn(B, float(cp.sigma(2.0)), seed=7, offset=123)
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
+
+
+@pytest.mark.parametrize("q", [5, -5])
+def test_bitsliced_per_row_weights(cuda_device, q):
+    dec, cp = _wman(cuda_device, sharing=(2, 0, 2), q=q, T=12)
+    assert dec.kernel_info()[1].startswith("bsl")
+    llr = dec.awgn(9000, float(cp.sigma(2.25)), seed=11)
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
+    assert 0 < out["fused"][0][1] < 9000
+
+
+def test_off_grid_packs_fall_back_exactly(cuda_device):
+    import torch
+    dec, cp = _wman(cuda_device)
+    llr = dec.awgn(5000, float(cp.sigma(2.0)), seed=9)
+    llr[40, 3] += 0.1            # pack 1 off the grid
+    llr[4000:4010, 100] = 30.0   # pack 125 out of the quantizer range
+    llr[4999, 0] = -0.3          # the last (ragged) pack
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
+    torch.cuda.synchronize()
