@@ -3,28 +3,26 @@
 // Same semantics as the v5 kernel (ldpc_fused5_kernel.h) and the reference graph
 // (Main_Functions.py:157-335): all T flooding iterations of a block in one launch, integer
 // arithmetic in units of the q-bit grid (q = 5 / -5: qmax = 15).  What changes is the data
-// layout.  A workgroup decodes one PACK of 32 codewords and every quantity is held as bit
-// planes: plane word p of a value holds bit p of that value for the 32 codewords (bit r =
-// codeword b0 + r).  The min-sum arithmetic — the V->C subtraction, |.| with saturation, the
-// two-minimum / argmin search, the sign parity, the weighted quantization (a 16-entry table
-// per iteration and proto row, evaluated as a mux tree) and the variable-node sums — becomes
-// boolean algebra on whole words, which gfx950 executes as v_bitop3_b32 (any function of three
-// words in one VALU op).  One lane does the work of 32 codeword-lanes of v5: per edge and
-// codeword the check side costs ~2 lane-ops instead of ~6 wave-ops/64, and LDS traffic falls
-// by the same factor.
+// layout: a workgroup decodes one PACK of 32 codewords and every quantity is held as bit
+// planes (plane word p of a value holds bit p of that value for the 32 codewords, bit r =
+// codeword b0 + r).  The min-sum arithmetic — V->C subtraction, |.| with saturation, the
+// two-minimum search, the sign parity, the weighted quantization (a 16-entry table per
+// iteration, evaluated as a mux tree) and the variable-node sums — is boolean algebra on whole
+// words, which gfx950 issues as v_bitop3_b32 (any function of three words in one VALU op).
+// One lane does the work of 32 codeword-lanes of v5.
 //
-// Representation (grid units):
-//   channel c = Q(ch) on the grid, |c| <= qmax: sign plane + 4 magnitude planes (the LLRs must
-//     be on the grid, which they are for the QMS channel; a pack with an off-grid or
-//     out-of-range value is flagged in `bad` and decoded by the v5 kernel instead: exact for
-//     any input)
-//   C->V message: negative flag + 4 magnitude planes, derived from the check record
-//     {q1, q2 (weighted quantized minima), idx (argmin edge), ns[k] (message k negative)}
-//   Tv = clamp(Q(beta_{t+1} ch) + S, [-32, 31]): 6 planes, two's complement (any bound >= 2 qmax
-//     gives the reference's V->C = clamp(Tv - C->V, +-qmax))
-//   S = sum of C->V over the variable's edges: SB planes, two's complement
-// A variable record in LDS is 16 words: Tv planes 0..5, channel sign 8, magnitude 9..12.
-// A check record is 12 + DMAX words: q1 0..3, q2 4..7, idx 8..11, ns 12..12+DMAX-1.
+// LDS holds one 5-word SLOT per lifted edge (slot s = proto edge * z + check index within the
+// row, so lanes on consecutive checks or variables touch consecutive slots):
+//   between the variable and the check phase: V->C = clamp(Tv - C->V, +-15), as a negative flag
+//     and 4 magnitude planes (the nudged zero is positive, Main_Functions.py:229-230);
+//   between the check and the variable phase: C->V, as a negative flag and 4 magnitude planes.
+// Each slot is read and then rewritten by exactly one lane per phase, so the two share it.
+// Check phase: one lane per check (up to D edges, padding edges read the all-ones PAD slot:
+// negative, magnitude 15, so they change neither minimum nor parity).  Variable phase: one lane
+// per variable (variables ordered by degree so a wave's loop bound is tight; padding edges read
+// the all-zero ZERO slot); the channel stays in the lane's registers for the whole decode.
+// Packs with an LLR off the quantizer grid are flagged in `bad` and decoded by the v5 kernel
+// instead, so the result is exact for any input.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -37,8 +35,8 @@ namespace ldpc {
 namespace bs {
 
 constexpr int PACK = 32;                 // codewords per workgroup
-constexpr int VREC_W = 16;               // words per variable record
-constexpr int VREC_B = VREC_W * 4;
+constexpr int SLOT_W = 5;                // words per edge slot: negative flag, magnitude 0..3
+constexpr int SLOT_B = SLOT_W * 4;
 constexpr int LUT_W = 64;                // words per 16-entry table: [bit j][pair p] {X, Y}
 constexpr int QMAX = 15;
 constexpr size_t BS_LDS_MAX = 160 * 1024;
@@ -46,73 +44,99 @@ constexpr size_t BS_LDS_MAX = 160 * 1024;
 struct BsArgs {
     const float* llr;
     int64_t B;
-    int n_vars, n_checks, N, M, T, target_bits;
+    int n_vars, T, target_bits, cn_lanes, cn_dmin;
     float inv;
-    const uint32_t* cn_addr;     // [n_checks][DMAX/2] VREC byte addresses, two per word
-    const uint32_t* cn_row;      // [n_checks] proto row
-    const uint32_t* vn_edges;    // [n_vars][dvmax] CREC byte address | k << 16 (zero record if unused)
-    int dvmax;
-    const uint32_t* alut;        // [T][M][LUT_W] alpha tables, Q(relu(alpha m step)) for m = 0..15
-    const uint32_t* blut;        // [T][N][LUT_W] beta tables, Q(beta m) for m = 0..15 (grid units)
+    const uint32_t* cn_tab;      // [cn_lanes][CNW]: slot byte addresses (2 per word), table offset
+    const uint32_t* vn_tab;      // [64 nw][VNW]: slot byte addresses (2 per word), variable (-1 idle)
+    const int32_t* vn_wdeg;      // [nw][2] most and fewest edges of a variable of each wave
+    const uint32_t* alut;        // [T][arows][LUT_W]: Q(relu(alpha m step)) for m = 0..15
+    const uint32_t* blut;        // [T][bcols][LUT_W]: |Q(beta m)| for m = 0..15 (grid units)
+    int arows, bcols;
     int64_t* counters;
     uint8_t* flags;
-    uint32_t* bad;               // [blocks] 1: decoded by the v5 fixup instead
-    uint32_t off_crec, off_alut, off_blut, off_red, off_stage;   // LDS byte offsets
-    int crec_w;                  // words per check record
-    int arows, bcols;            // tables per iteration: 1 (one weight for all rows / columns) or M / N
+    uint32_t* bad;               // [packs] 1: decoded by the v5 fixup instead
+    uint32_t off_pad, off_zero, off_red, off_alut, off_blut;   // LDS byte offsets
 };
 
-// ---- bit-plane arithmetic (the compiler maps these 3-input functions to v_bitop3_b32) ---------
-__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) { return (a & b) | (a & c) | (b & c); }
-__device__ __forceinline__ uint32_t mux(uint32_t s, uint32_t a, uint32_t b) { return (s & a) | (~s & b); }  // s ? a : b
+// ---- bit-plane arithmetic ---------------------------------------------------------------------
+// Every 3-input function is one v_bitop3_b32 with an explicit truth table (the compiler's own
+// boolean synthesis often emits two or three ops for one such function); 2-input functions are
+// left to the compiler, which emits the 2-cycle VOP2 forms (v_and / v_or / v_xor / v_xnor).
+// Truth table of f: f(0xF0, 0xCC, 0xAA) for operands (a, b, c).
+#define B3(F, a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), (F))
+constexpr unsigned TA = 0xF0, TB = 0xCC, TC = 0xAA;
+constexpr unsigned T_XOR3 = (TA ^ TB ^ TC) & 0xFF;                       // a ^ b ^ c
+constexpr unsigned T_XNOR3 = ~(TA ^ TB ^ TC) & 0xFF;                     // ~(a ^ b ^ c)
+constexpr unsigned T_MAJ = ((TA & TB) | (TA & TC) | (TB & TC)) & 0xFF;   // maj(a, b, c)
+constexpr unsigned T_MAJNB = ((TA & ~TB) | (TA & TC) | (~TB & TC)) & 0xFF;   // maj(a, ~b, c)
+constexpr unsigned T_MUX = ((TA & TB) | (~TA & TC)) & 0xFF;              // a ? b : c
+constexpr unsigned T_LT = ((~TA & TB) | (~(TA ^ TB) & TC)) & 0xFF;       // a < b at this bit, else c
+constexpr unsigned T_ANDN = (~TA & TB) & 0xFF;                           // ~a & b
+constexpr unsigned T_LEAF = ((TA & TB) ^ TC) & 0xFF;                     // (a & b) ^ c
+constexpr unsigned T_AND3 = (TA & TB & TC) & 0xFF;                       // a & b & c
+constexpr unsigned T_SAT = ((TA & ~TB) | (~TA & TC)) & 0xFF;             // a ? ~b : c
+constexpr unsigned T_XAND = (TA ^ (TB & TC)) & 0xFF;                     // a ^ (b & c)
+constexpr unsigned T_ANDNA = (TA & ~TB) & 0xFF;                          // a & ~b
+constexpr unsigned T_ORXOR = (TA | (TB ^ TC)) & 0xFF;                    // a | (b ^ c)
+__device__ __forceinline__ uint32_t mux(uint32_t s, uint32_t a, uint32_t b) { return B3(T_MUX, s, a, b); }
 
-// S + m for m given as (negative flag n, 4 magnitude planes M): two's complement, SB planes
+// S += m for m = (negative flag n, b) with b_i = M_i ^ n (M the 4 magnitude planes): the
+// two's complement of m is b sign-extended with n, plus n
 template <int SB>
-__device__ __forceinline__ void add_sm(uint32_t (&S)[SB], const uint32_t (&M)[4], uint32_t n) {
+__device__ __forceinline__ void add_b(uint32_t (&S)[SB], const uint32_t (&b)[4], uint32_t n) {
     uint32_t c = n;
 #pragma unroll
     for (int i = 0; i < SB; ++i) {
-        const uint32_t b = (i < 4) ? (M[i] ^ n) : n;
-        const uint32_t s = S[i] ^ b ^ c;
-        if (i + 1 < SB) c = maj3(S[i], b, c);
+        const uint32_t bi = (i < 4) ? b[i] : n;
+        const uint32_t s = B3(T_XOR3, S[i], bi, c);
+        if (i + 1 < SB) c = B3(T_MAJ, S[i], bi, c);
         S[i] = s;
     }
 }
-
-// V->C before the clamp: x = Tv - m (7 planes, two's complement; Tv in [-32, 31], |m| <= 15)
-__device__ __forceinline__ void sub_tv(uint32_t (&x)[7], const uint32_t (&T)[6], const uint32_t (&M)[4],
-                                       uint32_t n) {
-    const uint32_t p = ~n;          // m >= 0: add ~M + 1 (subtract); m < 0: add M
-    uint32_t c = p;
+// S = m (same operand form), S previously zero
+template <int SB>
+__device__ __forceinline__ void set_b(uint32_t (&S)[SB], const uint32_t (&b)[4], uint32_t n) {
+    uint32_t c = n;
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        const uint32_t t = T[i < 6 ? i : 5];
-        const uint32_t b = (i < 4) ? (M[i] ^ p) : p;
-        x[i] = t ^ b ^ c;
-        if (i < 6) c = maj3(t, b, c);
+    for (int i = 0; i < SB; ++i) {
+        const uint32_t bi = (i < 4) ? b[i] : n;
+        S[i] = bi ^ c;
+        c = bi & c;
     }
 }
 
-// |x| saturated at 15 (4 planes) for x in 7-plane two's complement; sign = x[6]
+// x = Tv - m (7 planes, two's complement; Tv in [-32, 31], |m| <= 15) with m = (n, b) as above:
+// -m is ~b sign-extended with ~n, plus ~n
+__device__ __forceinline__ void sub_tv(uint32_t (&x)[7], const uint32_t (&T)[6], const uint32_t (&b)[4],
+                                       uint32_t n) {
+    uint32_t c = ~n;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        const uint32_t t = T[i < 6 ? i : 5];
+        const uint32_t bi = (i < 4) ? b[i] : n;
+        x[i] = B3(T_XNOR3, t, bi, c);
+        if (i < 6) c = B3(T_MAJNB, t, bi, c);
+    }
+}
+
+// min(|x|, 15) (4 planes) of a 7-plane two's complement x in [-64, 63]; the sign is x[6].
+// For x < 0 the low bits of -x are x_i ^ OR(x_j, j < i); |x| >= 16 is x5 | x4 for x >= 0 and
+// "not (x5 & x4 & low 4 bits nonzero)" for x < 0.
 __device__ __forceinline__ void abs_sat(uint32_t (&X)[4], const uint32_t (&x)[7]) {
     const uint32_t neg = x[6];
-    uint32_t c = neg, r[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const uint32_t y = x[i] ^ neg;
-        r[i] = y ^ c;
-        if (i < 5) c = y & c;
-    }
-    const uint32_t hi = r[4] | r[5];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) X[i] = r[i] | hi;
+    const uint32_t o2 = x[0] | x[1], o3 = o2 | x[2], o4 = o3 | x[3];
+    const uint32_t sat = B3(T_SAT, neg, B3(T_AND3, x[5], x[4], o4), x[5] | x[4]);
+    X[0] = x[0] | sat;
+    X[1] = B3(T_XAND, x[1], neg, x[0]) | sat;
+    X[2] = B3(T_XAND, x[2], neg, o2) | sat;
+    X[3] = B3(T_XAND, x[3], neg, o3) | sat;
 }
 
 // a < b for 4-plane unsigned values
 __device__ __forceinline__ uint32_t lt4(const uint32_t (&a)[4], const uint32_t (&b)[4]) {
-    uint32_t l = ~a[0] & b[0];
+    uint32_t l = B3(T_ANDN, a[0], b[0], 0u);
 #pragma unroll
-    for (int i = 1; i < 4; ++i) l = (~a[i] & b[i]) | (~(a[i] ^ b[i]) & l);
+    for (int i = 1; i < 4; ++i) l = B3(T_LT, a[i], b[i], l);
     return l;
 }
 
@@ -124,191 +148,267 @@ __device__ __forceinline__ void clamp6(uint32_t (&T)[6], const uint32_t (&v)[SB]
     for (int i = 5; i < SB - 1; ++i) ovf |= v[i] ^ v[i + 1];
     const uint32_t s = v[SB - 1];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) T[i] = mux(ovf, ~s, v[i]);
+    for (int i = 0; i < 5; ++i) T[i] = B3(T_SAT, ovf, s, v[i]);
     T[5] = mux(ovf, s, v[5]);
 }
 
-// LDS accesses by byte address (all records and tables are LDS-absolute: the kernel's dynamic
+// LDS accesses by byte address (all slots and tables are LDS-absolute: the kernel's dynamic
 // LDS starts at 0, checked at entry)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) uint32_t LdsW;
 typedef __attribute__((address_space(3))) v4u LdsQ;
-typedef __attribute__((address_space(3))) v2u LdsD;
 
 __device__ __forceinline__ uint32_t lds_w(uint32_t addr) { return *reinterpret_cast<const LdsW*>(addr); }
 __device__ __forceinline__ v4u lds_q(uint32_t addr) { return *reinterpret_cast<const LdsQ*>(addr); }
-__device__ __forceinline__ void st_q(uint32_t addr, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
-    v4u v = {x, y, z, w};
-    *reinterpret_cast<LdsQ*>(addr) = v;
+
+__device__ __forceinline__ void read_slot(uint32_t& n, uint32_t (&M)[4], uint32_t addr) {
+    const LdsW* p = reinterpret_cast<const LdsW*>(addr);
+    n = p[0];
+    M[0] = p[1];
+    M[1] = p[2];
+    M[2] = p[3];
+    M[3] = p[4];
 }
-__device__ __forceinline__ void st_d(uint32_t addr, uint32_t x, uint32_t y) {
-    v2u v = {x, y};
-    *reinterpret_cast<LdsD*>(addr) = v;
+__device__ __forceinline__ void write_slot(uint32_t addr, uint32_t n, const uint32_t (&M)[4]) {
+    LdsW* p = reinterpret_cast<LdsW*>(addr);
+    p[0] = n;
+    p[1] = M[0];
+    p[2] = M[1];
+    p[3] = M[2];
+    p[4] = M[3];
 }
 
-// the Tv planes of the variable record at `addr`
-__device__ __forceinline__ void read_tv(uint32_t (&T)[6], uint32_t addr) {
-    const v4u a = lds_q(addr);
-    const v2u b = *reinterpret_cast<const LdsD*>(addr + 16);
-    T[0] = a.x; T[1] = a.y; T[2] = a.z; T[3] = a.w; T[4] = b.x; T[5] = b.y;
-}
-
-// 16-entry table g(m) (4 -> 4 bits) at LDS byte address `tab`, for two inputs at once
-__device__ __forceinline__ void lut2(uint32_t (&oa)[4], uint32_t (&ob)[4], const uint32_t (&a)[4],
-                                     const uint32_t (&b)[4], uint32_t tab) {
+// 16-entry table g(m) (4 -> 4 bits) at LDS byte address `tab`: level 1 of the mux tree is
+// (m0 & X) ^ Y per pair of entries, levels 2-4 select by m1, m2, m3
+template <int NI>
+__device__ __forceinline__ void lut(uint32_t (&o)[NI][4], const uint32_t (&in)[NI][4], uint32_t tab) {
+    uint32_t tj = tab;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        uint32_t xy[16];
+        // one output bit at a time (the next bit's table loads wait for this bit's result), so
+        // that the scheduler cannot hoist all 16 table loads into 64 registers
+        if (j > 0) asm volatile("" : "+v"(tj) : "v"(o[0][j - 1]));
+        uint32_t g[NI][4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const v4u w = lds_q(tab + (uint32_t)(j * 64 + q * 16));
-            xy[4 * q] = w.x; xy[4 * q + 1] = w.y; xy[4 * q + 2] = w.z; xy[4 * q + 3] = w.w;
-        }
-        uint32_t ga[8], gb[8];
+            const v4u w = lds_q(tj + (uint32_t)(j * 64 + q * 16));      // pairs 2q, 2q + 1
 #pragma unroll
-        for (int p = 0; p < 8; ++p) {
-            ga[p] = (a[0] & xy[2 * p]) ^ xy[2 * p + 1];
-            gb[p] = (b[0] & xy[2 * p]) ^ xy[2 * p + 1];
+            for (int u = 0; u < NI; ++u) {
+                const uint32_t l0 = B3(T_LEAF, in[u][0], w.x, w.y), l1 = B3(T_LEAF, in[u][0], w.z, w.w);
+                g[u][q] = mux(in[u][1], l1, l0);
+            }
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            ga[q] = mux(a[1], ga[2 * q + 1], ga[2 * q]);
-            gb[q] = mux(b[1], gb[2 * q + 1], gb[2 * q]);
-        }
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            ga[r] = mux(a[2], ga[2 * r + 1], ga[2 * r]);
-            gb[r] = mux(b[2], gb[2 * r + 1], gb[2 * r]);
-        }
-        oa[j] = mux(a[3], ga[1], ga[0]);
-        ob[j] = mux(b[3], gb[1], gb[0]);
+        for (int u = 0; u < NI; ++u)
+            o[u][j] = mux(in[u][3], mux(in[u][2], g[u][3], g[u][2]), mux(in[u][2], g[u][1], g[u][0]));
     }
 }
-
-__device__ __forceinline__ void lut1(uint32_t (&oa)[4], const uint32_t (&a)[4], uint32_t tab) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        uint32_t xy[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const v4u w = lds_q(tab + (uint32_t)(j * 64 + q * 16));
-            xy[4 * q] = w.x; xy[4 * q + 1] = w.y; xy[4 * q + 2] = w.z; xy[4 * q + 3] = w.w;
-        }
-        uint32_t g[8];
-#pragma unroll
-        for (int p = 0; p < 8; ++p) g[p] = (a[0] & xy[2 * p]) ^ xy[2 * p + 1];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) g[q] = mux(a[1], g[2 * q + 1], g[2 * q]);
-#pragma unroll
-        for (int r = 0; r < 2; ++r) g[r] = mux(a[2], g[2 * r + 1], g[2 * r]);
-        oa[j] = mux(a[3], g[1], g[0]);
-    }
-}
-
-
 
 #ifndef BS_WPE
-#define BS_WPE 4
+#define BS_WPE 7
 #endif
-template <int DMAX, int SB>
+#ifndef BS_KEEP
+#define BS_KEEP 0
+#endif
+template <int D, int DV>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(BS_WPE)))
 k_bs(BsArgs a) {
+    constexpr int SB = (DV * QMAX + QMAX <= 127) ? 8 : 9;     // planes of S and of lw + S
+    constexpr int CNW = (D + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();          // records are LDS-absolute
+    if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();          // slots are LDS-absolute
     const int tid = threadIdx.x;
     const int NT = blockDim.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int nwv = NT >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nv = a.n_vars;
-    const int z = nv / a.N;
     const int64_t b0 = (int64_t)blockIdx.x * PACK;
     const int nvalid = (int)min<int64_t>(PACK, a.B - b0);
     const uint32_t valid = (nvalid >= 32) ? 0xFFFFFFFFu : ((1u << nvalid) - 1u);
     uint32_t* RED = reinterpret_cast<uint32_t*>(smem + a.off_red);   // [0] wrong_t, [1] all t, [2] APP > 0, [3] bits
-    const uint32_t crec = a.off_crec;
-    const int CW = a.crec_w;
     const int AL = a.arows * LUT_W, BL = a.bcols * LUT_W;
-    LdsW* ALUT = reinterpret_cast<LdsW*>(a.off_alut);   // [2][arows][LUT_W]
-    LdsW* BLUT = reinterpret_cast<LdsW*>(a.off_blut);   // [2][bcols][LUT_W]
+    uint32_t* ALUT = reinterpret_cast<uint32_t*>(smem + a.off_alut);   // [2][arows][LUT_W]
+    uint32_t* BLUT = reinterpret_cast<uint32_t*>(smem + a.off_blut);   // [2][bcols][LUT_W]
 
-    // ---- prologue: LLRs -> grid integers (int8 staging, coalesced along each codeword) -------
-    signed char* STG = reinterpret_cast<signed char*>(smem + a.off_stage);   // [32][nv]
-    if (tid == 0) RED[7] = 0u;             // "some LLR of the pack is off the grid" (RED is past STG)
+    // ---- per-lane tables -----------------------------------------------------------------------
+    // (the slot addresses are reloaded from the L2-resident tables in each phase rather than
+    // held in registers through the whole decode)
+    const uint32_t* vt = a.vn_tab + (size_t)tid * VNW;
+    const int v = (int)vt[VNW - 1];                       // -1: no variable
+    int dw = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * wave]);
+    int dwmin = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * wave + 1]);
+    int cn_dmin = a.cn_dmin;
+    const bool counted = v >= 0 && v < a.target_bits;
+    const uint32_t tab_b = (a.bcols > 1 && v >= 0) ? (uint32_t)((v / (nv / a.bcols)) * LUT_W * 4) : 0u;
+    const bool is_cn = tid < a.cn_lanes;
+
+    // ---- channel planes: the lane's variable for the 32 codewords of the pack --------------------
+    // (no __syncthreads_or: it allocates static LDS, which would move the dynamic LDS base
+    // away from 0; the flag word lives in RED)
+    if (tid == 0) RED[7] = 0u;
     __syncthreads();
+    uint32_t cs = 0u, cm[4] = {0u, 0u, 0u, 0u};
     int off = 0;
-    for (int e = tid; e < PACK * nv; e += NT) {
-        const int r = e / nv, v = e - r * nv;
-        int xi = 0;
-        if (r < nvalid) {
-            const float x = a.llr[(b0 + r) * nv + v] * a.inv;
+    if (v >= 0) {
+        const float* src = a.llr + b0 * nv + v;
+#pragma unroll 8
+        for (int r = 0; r < PACK; ++r) {
+            const int rr = min(r, nvalid - 1);
+            const float x = src[(int64_t)rr * nv] * a.inv;
             const float xr = rintf(x);
             off |= (xr != x || fabsf(xr) > (float)QMAX) ? 1 : 0;
-            xi = (int)xr;
+            const int xi = (r < nvalid) ? (int)xr : 0;
+            const uint32_t m = (uint32_t)(xi < 0 ? -xi : xi);
+            cs |= (xi < 0 ? 1u : 0u) << r;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) cm[p] |= ((m >> p) & 1u) << r;
         }
-        STG[e] = (signed char)xi;
     }
     if (off) atomicOr(&RED[7], 1u);
     __syncthreads();
-    if (RED[7]) {                             // off the grid: the v5 fixup decodes this pack
+    if (RED[7]) {                              // off the grid: the v5 fixup decodes this pack
         if (tid == 0) a.bad[blockIdx.x] = 1u;
         return;
     }
     if (tid == 0) a.bad[blockIdx.x] = 0u;
-    // channel planes by ballot: lanes 0..31 = codewords of variable v, 32..63 of v + 1
-    {
-        const int r = lane & 31, half = lane >> 5;
-        for (int base = 2 * wave; base < nv; base += 2 * nwv) {
-            const int v = base + half;
-            const int x = (v < nv) ? (int)STG[r * nv + v] : 0;
-            const int m = x < 0 ? -x : x;
-            const uint64_t bs = __ballot(x < 0);
-            const uint64_t c0 = __ballot(m & 1), c1 = __ballot(m & 2), c2 = __ballot(m & 4),
-                           c3 = __ballot(m & 8);
-            if (r == 0 && v < nv) {
-                const int sh = 32 * half;
-                const uint32_t rec = (uint32_t)(v * VREC_B);
-                st_q(rec + 32, (uint32_t)(bs >> sh), (uint32_t)(c0 >> sh), (uint32_t)(c1 >> sh),
-                               (uint32_t)(c2 >> sh));
-                reinterpret_cast<LdsW*>(rec + 48)[0] = (uint32_t)(c3 >> sh);
-            }
-        }
+    // PAD slot (all ones: V->C negative, magnitude 15), ZERO slot (a zero C->V), counters,
+    // iteration 0's tables
+    if (tid < SLOT_W) {
+        reinterpret_cast<uint32_t*>(smem + a.off_pad)[tid] = 0xFFFFFFFFu;
+        reinterpret_cast<uint32_t*>(smem + a.off_zero)[tid] = 0u;
     }
-    __syncthreads();
-    // zero check records (+ the zero record at n_checks), dummy variable record Tv = -32,
-    // counters, iteration 0's tables
-    for (int w = tid; w < (a.n_checks + 1) * CW; w += NT) reinterpret_cast<LdsW*>(crec)[w] = 0u;
-    if (tid < 16) reinterpret_cast<LdsW*>((uint32_t)(nv * VREC_B))[tid] = (tid == 5) ? 0xFFFFFFFFu : 0u;
-    if (tid < 7) RED[tid] = (tid == 1) ? 0xFFFFFFFFu : 0u;
+    if (tid < 8) RED[tid] = (tid == 1) ? 0xFFFFFFFFu : 0u;
     for (int w = tid; w < AL; w += NT) ALUT[w] = a.alut[w];
     for (int w = tid; w < BL; w += NT) BLUT[w] = a.blut[w];
     __syncthreads();
-    // Tv_0 = Q(beta_0 ch): the table gives the magnitude, the channel sign the sign
-    for (int v = tid; v < nv; v += NT) {
-        const uint32_t rec = (uint32_t)(v * VREC_B);
-        const v4u cq = lds_q(rec + 32);
-        const uint32_t cm[4] = {cq.y, cq.z, cq.w, lds_w(rec + 48)};
-        uint32_t lw[4];
-        lut1(lw, cm, a.off_blut + (uint32_t)((a.bcols > 1 ? v / z : 0) * LUT_W * 4));
+
+    // ---- variable phase -------------------------------------------------------------------------
+    //   first: lw_0 as every edge's V->C (no C->V yet);
+    //   else:  S = sum of the C->V, APP_t = Q(ch) + S (hard decision, counters); unless last,
+    //          Tv = clamp(Q(beta_{t+1} ch) + S) and V->C_e = clamp(Tv - C->V_e, +-15) per edge
+    auto vn_phase = [&](const bool first, const bool last, const uint32_t btab)
+                        __attribute__((always_inline)) {
+        uint32_t va[VNW - 1];
+        {
+            const uint32_t* vp = vt;
+            asm volatile("" : "+v"(vp));                  // a load per phase, not hoisted
+#pragma unroll
+            for (int p = 0; p < VNW - 1; ++p) va[p] = vp[p];
+        }
+        auto vaddr = [&](int f) __attribute__((always_inline)) -> uint32_t {
+            return (f & 1) ? (va[f >> 1] >> 16) : (va[f >> 1] & 0xFFFFu);
+        };
+        uint32_t lw[1][4];                   // |Q(beta_{t+1} ch)| (before the C->V: fewer live registers)
+        if (!last) {
+            const uint32_t cmi[1][4] = {{cm[0], cm[1], cm[2], cm[3]}};
+            lut<1>(lw, cmi, btab);
+        }
+        // C->V of the first KEEP edges stay in registers for the V->C pass, the others are read
+        // again (the register budget of three 9-wave workgroups per CU)
+        constexpr int KEEP = BS_KEEP < DV ? BS_KEEP : DV;
+        uint32_t mn[KEEP > 0 ? KEEP : 1], mb[KEEP > 0 ? KEEP : 1][4];
         uint32_t S[SB];
 #pragma unroll
         for (int i = 0; i < SB; ++i) S[i] = 0u;
-        add_sm<SB>(S, lw, cq.x);
-        uint32_t T[6];
-        clamp6<SB>(T, S);
-        st_q(rec, T[0], T[1], T[2], T[3]);
-        st_d(rec + 16, T[4], T[5]);
-    }
-    // per-lane graph tables (one check per lane: checked on the host)
-    uint32_t pk[DMAX / 2];
-    uint32_t tab_a = a.off_alut;
-    const bool is_check = tid < a.n_checks;
-    if (is_check) {
+        if (!first) {
 #pragma unroll
-        for (int p = 0; p < DMAX / 2; ++p) pk[p] = a.cn_addr[(size_t)tid * (DMAX / 2) + p];
-        if (a.arows > 1) tab_a += a.cn_row[tid] * (LUT_W * 4);
-    }
+            for (int f = 0; f < DV; ++f) {
+                if (f < dw) {
+                    uint32_t M[4], n, b[4];
+                    read_slot(n, M, vaddr(f));
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) b[i] = M[i] ^ n;
+                    if (f == 0) set_b<SB>(S, b, n);
+                    else add_b<SB>(S, b, n);
+                    if (f < KEEP) {
+                        mn[f < KEEP ? f : 0] = n;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) mb[f < KEEP ? f : 0][i] = b[i];
+                    }
+                }
+            }
+            // APP_t = Q(ch) + S: the sign (hard decision) from the carry chain alone, the full
+            // sum only in the last iteration (APP > 0 for the loss counter)
+            uint32_t hd, nz = 0u;
+            if (last) {
+                uint32_t A[SB];
+#pragma unroll
+                for (int i = 0; i < SB; ++i) A[i] = S[i];
+                const uint32_t cb[4] = {cm[0] ^ cs, cm[1] ^ cs, cm[2] ^ cs, cm[3] ^ cs};
+                add_b<SB>(A, cb, cs);
+                hd = ~A[SB - 1];
+#pragma unroll
+                for (int i = 0; i < SB; ++i) nz |= A[i];
+            } else {
+                uint32_t c = cs;
+#pragma unroll
+                for (int i = 0; i < SB - 1; ++i) c = B3(T_MAJ, S[i], i < 4 ? (cm[i] ^ cs) : cs, c);
+                hd = B3(T_XNOR3, S[SB - 1], cs, c);
+            }
+            hd &= valid;                                     // APP >= 0 -> hard decision 1
+            uint32_t wr = counted ? hd : 0u, apos = 0u, nb = 0u;
+            if (last && counted) {
+                apos = hd & nz;
+                nb = (uint32_t)__popc(hd);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                wr |= __shfl_xor(wr, o);
+                if (last) {
+                    apos |= __shfl_xor(apos, o);
+                    nb += __shfl_xor(nb, o);
+                }
+            }
+            if (lane == 0) {
+                if (wr) atomicOr(&RED[0], wr);
+                if (last) {
+                    if (apos) atomicOr(&RED[2], apos);
+                    if (nb) atomicAdd(&RED[3], nb);
+                }
+            }
+        }
+        if (last) return;
+        // Tv = clamp(Q(beta ch) + S): the table gives |Q(beta ch)|, the channel the sign
+        uint32_t lb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) lb[i] = lw[0][i] ^ cs;
+        add_b<SB>(S, lb, cs);
+        uint32_t Tv[6];
+        clamp6<SB>(Tv, S);
+        if (first) {
+            uint32_t x[7], X[4];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) x[i] = Tv[i < 6 ? i : 5];
+            abs_sat(X, x);
+#pragma unroll
+            for (int f = 0; f < DV; ++f)
+                if (f < dw && (f < dwmin || vaddr(f) != a.off_zero)) write_slot(vaddr(f), x[6], X);
+        } else {
+#pragma unroll
+            for (int f = 0; f < DV; ++f) {
+                if (f < dw) {
+                    uint32_t x[7], X[4], n, b[4];
+                    if (f < KEEP) {
+                        n = mn[f < KEEP ? f : 0];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) b[i] = mb[f < KEEP ? f : 0][i];
+                    } else {
+                        uint32_t M[4];
+                        read_slot(n, M, vaddr(f));
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) b[i] = M[i] ^ n;
+                    }
+                    sub_tv(x, Tv, b, n);
+                    abs_sat(X, x);
+                    if (f < dwmin || vaddr(f) != a.off_zero) write_slot(vaddr(f), x[6], X);
+                }
+            }
+        }
+    };
+
+    vn_phase(true, false, a.off_blut + tab_b);
+    const uint32_t* ct = a.cn_tab + (size_t)tid * CNW;
+    const uint32_t tab_a = a.off_alut + (is_cn ? ct[CNW - 1] : 0u);
     __syncthreads();
 
     for (int t = 0; t < a.T; ++t) {
@@ -317,129 +417,68 @@ k_bs(BsArgs a) {
             RED[0] = 0u;
         }
         const int nx = (t + 1) & 1;
-        // beta_{t+1} for this iteration's variable phase (its slot was last read two phases ago)
-        if (t + 1 < a.T)
+        asm volatile("" : "+s"(dw), "+s"(dwmin), "+s"(cn_dmin));   // compared per use, not hoisted as masks
+        // next iteration's tables (their slots were last read two phases ago)
+        if (t + 1 < a.T) {
+            for (int w = tid; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
             for (int w = tid; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
+        }
         // ======== check nodes ===================================================================
-        if (is_check) {
-            const uint32_t rec = crec + (uint32_t)(tid * CW * 4);
-            const v4u q1v = lds_q(rec), q2v = lds_q(rec + 16), ixv = lds_q(rec + 32);
-            const uint32_t q1[4] = {q1v.x, q1v.y, q1v.z, q1v.w};
-            const uint32_t q2[4] = {q2v.x, q2v.y, q2v.z, q2v.w};
-            const uint32_t ix[4] = {ixv.x, ixv.y, ixv.z, ixv.w};
-            uint32_t m1[4] = {~0u, ~0u, ~0u, ~0u}, m2[4] = {~0u, ~0u, ~0u, ~0u};
-            uint32_t id[4] = {0u, 0u, 0u, 0u};
-            uint32_t pos[DMAX];
+        if (is_cn) {
+            uint32_t ca[CNW - 1];
+            {
+                const uint32_t* cp = ct;
+                asm volatile("" : "+v"(cp));              // a load per phase, not hoisted
 #pragma unroll
-            for (int k = 0; k < DMAX; ++k) {
-                const uint32_t addr = (k & 1) ? (pk[k >> 1] >> 16) : (pk[k >> 1] & 0xFFFFu);
-                uint32_t T[6];
-                read_tv(T, addr);
-                // old message of edge k: magnitude q2 at the argmin edge, else q1
-                uint32_t am = ~0u;
+                for (int p = 0; p < CNW - 1; ++p) ca[p] = cp[p];
+            }
+            auto caddr = [&](int k) __attribute__((always_inline)) -> uint32_t {
+                return (k & 1) ? (ca[k >> 1] >> 16) : (ca[k >> 1] & 0xFFFFu);
+            };
+            // pass 1: two minima of |V->C| and the parity of [V->C >= 0] (padding edges:
+            // negative, magnitude 15)
+            uint32_t m1[4], m2[4] = {~0u, ~0u, ~0u, ~0u}, par;
+            read_slot(par, m1, caddr(0));
 #pragma unroll
-                for (int i = 0; i < 4; ++i) am &= ((k >> i) & 1) ? ix[i] : ~ix[i];
-                const uint32_t ns = lds_w(rec + 48 + 4 * k);
-                uint32_t Mg[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) Mg[i] = mux(am, q2[i], q1[i]);
-                uint32_t x[7], X[4];
-                sub_tv(x, T, Mg, ns);
-                abs_sat(X, x);
-                pos[k] = ~x[6];                                 // V->C >= 0 (the nudged zero too)
+            for (int k = 1; k < D; ++k) {
+                uint32_t X[4], n;
+                read_slot(n, X, caddr(k));
                 const uint32_t l1 = lt4(X, m1), l2 = lt4(X, m2);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     m2[i] = mux(l1, m1[i], mux(l2, X[i], m2[i]));
                     m1[i] = mux(l1, X[i], m1[i]);
-                    id[i] = ((k >> i) & 1) ? (id[i] | l1) : (id[i] & ~l1);
+                }
+                par ^= n;
+            }
+            // message k is negative iff an even number of the OTHER edges have V->C >= 0
+            // (Main_Functions.py:251-254): par ^ n_k, with par the parity of [V->C >= 0]
+            if (D & 1) par = ~par;
+            uint32_t q[2][4];
+            const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
+            lut<2>(q, mm, tab_a + (uint32_t)((t & 1) * AL * 4));
+            // pass 2: an edge whose |V->C| equals the minimum gets the weighted second minimum
+            // (if it is not the only one, the two minima are equal), the others the minimum
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                const uint32_t addr = caddr(k);
+                if (k < cn_dmin || addr != a.off_pad) {
+                    uint32_t X[4], n, Mg[4];
+                    read_slot(n, X, addr);
+                    uint32_t ne = X[0] ^ m1[0];
+#pragma unroll
+                    for (int i = 1; i < 4; ++i) ne = B3(T_ORXOR, ne, X[i], m1[i]);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) Mg[i] = mux(ne, q[0][i], q[1][i]);
+                    write_slot(addr, par ^ n, Mg);
                 }
             }
-            uint32_t par = 0u;
-#pragma unroll
-            for (int k = 0; k < DMAX; ++k) par ^= pos[k];
-            uint32_t q1n[4], q2n[4];
-            lut2(q1n, q2n, m1, m2, tab_a + (uint32_t)((t & 1) * AL * 4));
-            st_q(rec, q1n[0], q1n[1], q1n[2], q1n[3]);
-            st_q(rec + 16, q2n[0], q2n[1], q2n[2], q2n[3]);
-            st_q(rec + 32, id[0], id[1], id[2], id[3]);
-            // message k negative iff an even number of the OTHER edges have V->C >= 0
-            // (Main_Functions.py:251-254: sgn = -prod(1 - 2 [v2c < 0]) ... o = m * sign(sgn))
-#pragma unroll
-            for (int k = 0; k < DMAX; k += 4)
-                st_q(rec + 48 + 4 * k, ~(par ^ pos[k]), ~(par ^ pos[k + 1]), ~(par ^ pos[k + 2]),
-                               ~(par ^ pos[k + 3]));
         }
         __syncthreads();
-        const bool last = (t == a.T - 1);
-        // alpha_{t+1} for the next check phase (slot last read by the check phase of t - 1)
-        if (t + 1 < a.T)
-            for (int w = tid; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
         // ======== variable nodes ================================================================
-        uint32_t wr = 0u, apos = 0u, nb = 0u;
-        for (int v = tid; v < nv; v += NT) {
-            const uint32_t vrec = (uint32_t)(v * VREC_B);
-            uint32_t S[SB];
-#pragma unroll
-            for (int i = 0; i < SB; ++i) S[i] = 0u;
-            for (int e = 0; e < a.dvmax; ++e) {
-                const uint32_t ed = a.vn_edges[(size_t)v * a.dvmax + e];
-                const uint32_t r = crec + (ed & 0xFFFFu);
-                const uint32_t k = ed >> 16;
-                const v4u q1v = lds_q(r), q2v = lds_q(r + 16), ixv = lds_q(r + 32);
-                const uint32_t ns = lds_w(r + 48 + 4 * k);
-                const uint32_t k0 = 0u - (k & 1u), k1 = 0u - ((k >> 1) & 1u), k2 = 0u - ((k >> 2) & 1u),
-                               k3 = 0u - ((k >> 3) & 1u);
-                const uint32_t am = ~((ixv.x ^ k0) | (ixv.y ^ k1) | (ixv.z ^ k2) | (ixv.w ^ k3));
-                const uint32_t Mg[4] = {mux(am, q2v.x, q1v.x), mux(am, q2v.y, q1v.y),
-                                        mux(am, q2v.z, q1v.z), mux(am, q2v.w, q1v.w)};
-                add_sm<SB>(S, Mg, ns);
-            }
-            const v4u cq = lds_q(vrec + 32);
-            const uint32_t cs = cq.x;
-            const uint32_t cm[4] = {cq.y, cq.z, cq.w, lds_w(vrec + 48)};
-            // APP_t = clip(Q(ch) + S, +-clip_LLR): its sign and zero-ness are all the counters need
-            uint32_t A[SB];
-#pragma unroll
-            for (int i = 0; i < SB; ++i) A[i] = S[i];
-            add_sm<SB>(A, cm, cs);
-            const uint32_t hd = ~A[SB - 1] & valid;          // APP >= 0 -> hard decision 1
-            if (v < a.target_bits) {
-                wr |= hd;
-                if (last) {
-                    uint32_t nz = 0u;
-#pragma unroll
-                    for (int i = 0; i < SB; ++i) nz |= A[i];
-                    apos |= hd & nz;
-                    nb += (uint32_t)__popc(hd);
-                }
-            }
-            if (!last) {          // Tv_{t+1} = clamp(Q(beta_{t+1} ch) + S_{t+1})
-                uint32_t lw[4];
-                lut1(lw, cm, a.off_blut + (uint32_t)((nx * BL + (a.bcols > 1 ? v / z : 0) * LUT_W) * 4));
-                add_sm<SB>(S, lw, cs);
-                uint32_t T[6];
-                clamp6<SB>(T, S);
-                st_q(vrec, T[0], T[1], T[2], T[3]);
-                st_d(vrec + 16, T[4], T[5]);
-            }
-        }
-        // reductions over the block
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            wr |= __shfl_xor(wr, o);
-            if (last) {
-                apos |= __shfl_xor(apos, o);
-                nb += __shfl_xor(nb, o);
-            }
-        }
-        if (lane == 0) {
-            if (wr) atomicOr(&RED[0], wr);
-            if (last) {
-                if (apos) atomicOr(&RED[2], apos);
-                if (nb) atomicAdd(&RED[3], nb);
-            }
-        }
+        const uint32_t btab = a.off_blut + (uint32_t)(nx * BL * 4) + tab_b;
+        if (t == a.T - 1) vn_phase(false, true, btab);
+        else vn_phase(false, false, btab);
         __syncthreads();
     }
     if (tid == 0) {
@@ -469,11 +508,10 @@ k_bs(BsArgs a) {
 // with Y = bit j of g(2p) (as a 0 / ~0 word) and X = Y ^ (bit j of g(2p + 1)):
 // level 1 of the tree is (m0 & X) ^ Y.
 //   alpha: g(m) = Q(relu(fl32(m step * alpha_{t,row}))) (Main_Functions.py:266-316), m = min(|V->C|)
-//   beta:  g(m) = Q(fl32(m * beta_{t,col})) in grid units (lw = Q(beta ch), :164-177)
+//   beta:  g(m) = Q(fl32(m * beta_{t,col})) in grid units (lw = Q(beta ch), :164-177; beta >= 0)
 __global__ void k_bs_tables(const float* __restrict__ alpha, const float* __restrict__ beta,
-                            const int32_t* __restrict__ row_ptr, int T, int E, int N, int z,
-                            int arows, int bcols, float step, float inv, uint32_t* alut,
-                            uint32_t* blut) {
+                            const int32_t* __restrict__ row_ptr, int T, int E, int N, int arows,
+                            int bcols, float step, float inv, uint32_t* alut, uint32_t* blut) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;    // one table per thread
     const int na = T * arows, nbt = T * bcols;
     if (f >= na + nbt) return;
@@ -490,7 +528,7 @@ __global__ void k_bs_tables(const float* __restrict__ alpha, const float* __rest
         const float b = beta[(size_t)t * N + col];
         for (int m = 0; m < 16; ++m) {
             const int q = (int)__builtin_amdgcn_fmed3f(rintf((float)m * b), -(float)QMAX, (float)QMAX);
-            g[m] = q < 0 ? -q : q;       // beta >= 0 in practice; the sign comes from the channel
+            g[m] = q < 0 ? -q : q;       // beta >= 0 (checked on the host)
         }
         out = blut + (size_t)f2 * LUT_W;
     }
@@ -504,56 +542,51 @@ __global__ void k_bs_tables(const float* __restrict__ alpha, const float* __rest
 }
 
 // ---- host: planning, graph tables, launch -------------------------------------------------
+// kernel instances (D = check-degree bound, DV = variable-degree bound)
+struct BsInst { int D, DV; };
+constexpr BsInst kInst[] = {{15, 6}, {16, 8}};
+
 struct BsPlan {
     bool ok = false;
-    int nw = 0, dmax = 16, sb = 8, dvmax = 0, crec_w = 0, arows = 1, bcols = 1;
-    uint32_t off_crec = 0, off_alut = 0, off_blut = 0, off_red = 0, off_stage = 0;
+    int inst = -1, nw = 0, cn_lanes = 0, arows = 1, bcols = 1;
+    uint32_t off_pad = 0, off_zero = 0, off_sink = 0, off_red = 0, off_alut = 0, off_blut = 0;
+    int cn_dmin = 0;
     size_t lds = 0;
 };
 
-static int bits_for(int maxabs) {        // two's complement planes holding [-maxabs, maxabs]
-    int b = 1;
-    while ((1 << (b - 1)) - 1 < maxabs) ++b;
-    return b;
-}
-
-BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, bool arow_uniform,
-               bool bcol_uniform) {
+BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
     BsPlan p;
     const char* e = getenv("LDPC_BS");
     if (e && atoi(e) == 0) return p;
     if (mode != MODE_Q5 && mode != MODE_QM5) return p;           // qmax 15: 4 magnitude planes
-    if (ucn || per_edge_w || !g.host) return p;
+    if (ucn || per_edge_w || !g.host || !g.w_beta_nonneg) return p;
     const host::GraphTables& h = *g.host;
     int min_cdeg = 1 << 30;
     for (int i = 0; i < h.M; ++i) min_cdeg = std::min(min_cdeg, h.row_ptr[i + 1] - h.row_ptr[i]);
-    if (h.max_cdeg > 16 || min_cdeg < 2) return p;               // ("no other edge" rule unneeded)
+    if (min_cdeg < 2) return p;                                   // ("no other edge" rule unneeded)
+    for (int i = 0; i < (int)(sizeof(kInst) / sizeof(kInst[0])); ++i)
+        if (h.max_cdeg <= kInst[i].D && h.max_vdeg <= kInst[i].DV) { p.inst = i; break; }
+    if (p.inst < 0) return p;
     const int nv = g.n_vars, nc = g.n_checks;
-    p.nw = std::min(16, (std::max(nv, nc) + 63) / 64);
-    if (nc > 64 * p.nw) return p;                                 // one check per lane
-    if ((size_t)(nv + 1) * VREC_B > 65535) return p;              // 16-bit record addresses
-    p.sb = bits_for(h.max_vdeg * QMAX + QMAX);
-    if (p.sb != 8 && p.sb != 10) p.sb = (p.sb < 8) ? 8 : (p.sb <= 10 ? 10 : 0);
-    if (p.sb == 0) return p;
-    p.dvmax = h.max_vdeg;
-    p.crec_w = 12 + p.dmax;
-    p.arows = arow_uniform ? 1 : h.M;
-    p.bcols = bcol_uniform ? 1 : h.N;
-    size_t o = (size_t)(nv + 1) * VREC_B;
-    p.off_crec = (uint32_t)o;
-    o += (size_t)(nc + 1) * p.crec_w * 4;
-    if (o > 65535) return p;                                      // 16-bit check record addresses
+    p.nw = (std::max(nv, nc) + 63) / 64;
+    if (p.nw > 16) return p;                                      // one variable / check per lane
+    p.cn_lanes = 64 * ((nc + 63) / 64);
+    p.arows = g.w_alpha_uniform ? 1 : h.M;
+    p.bcols = g.w_beta_uniform ? 1 : h.N;
+    const size_t nslot = (size_t)h.E * h.z;
+    p.off_pad = (uint32_t)(nslot * SLOT_B);
+    p.off_zero = p.off_pad + SLOT_B;
+    p.off_sink = p.off_zero + SLOT_B;
+    p.cn_dmin = min_cdeg;
+    const size_t sink_end = (size_t)p.off_sink + (size_t)(p.cn_lanes - nc) * SLOT_B;
+    if (sink_end > 65535) return p;                               // 16-bit slot addresses
+    size_t o = (sink_end + 15) & ~(size_t)15;
+    p.off_red = (uint32_t)o;
+    o += 64;
     p.off_alut = (uint32_t)o;
     o += (size_t)2 * p.arows * LUT_W * 4;
     p.off_blut = (uint32_t)o;
     o += (size_t)2 * p.bcols * LUT_W * 4;
-    // int8 staging of the LLR block: over the check records and tables (used before them);
-    // the counters (RED) after both, since the prologue uses RED[7] while staging
-    p.off_stage = p.off_crec;
-    o = std::max(o, (size_t)p.off_stage + (size_t)PACK * nv);
-    o = (o + 15) & ~(size_t)15;
-    p.off_red = (uint32_t)o;
-    o += 64;
     p.lds = (o + 15) & ~(size_t)15;
     if (p.lds > BS_LDS_MAX) return p;
     p.ok = true;
@@ -565,13 +598,14 @@ BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, bool arow
 using namespace bs;
 
 bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
-    return bs_plan(g, mode, ucn, per_edge_w, true, true).ok;
+    return bs_plan(g, mode, ucn, per_edge_w).ok;
 }
 
 const char* bs_kernel_name(const DevGraph& g) {
     static thread_local char buf[48];
-    const BsPlan p = bs_plan(g, MODE_Q5, false, false, true, true);
-    snprintf(buf, sizeof(buf), "bsl[p32,w%d,s%d]", p.nw, p.sb);
+    const BsPlan p = bs_plan(g, MODE_Q5, false, false);
+    snprintf(buf, sizeof(buf), "bsl[p32,w%d,d%d,v%d]", p.nw, p.inst >= 0 ? kInst[p.inst].D : 0,
+             p.inst >= 0 ? kInst[p.inst].DV : 0);
     return buf;
 }
 
@@ -579,72 +613,91 @@ const char* bs_kernel_name(const DevGraph& g) {
 static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& ws, hipStream_t s) {
     if (ws.bs_graph) return LDPC_OK;
     const host::GraphTables& h = *g.host;
-    const int nv = g.n_vars, nc = g.n_checks, z = g.z;
-    const int npk = p.dmax / 2;
-    std::vector<uint32_t> tab;
-    tab.reserve((size_t)nc * npk + nc + (size_t)nv * p.dvmax);
-    // cn_addr: VREC byte address of each edge's variable, the dummy record past the degree
-    std::vector<int> kpos((size_t)nv * p.dvmax, -1);
-    std::vector<int> kchk((size_t)nv * p.dvmax, -1);
-    std::vector<int> nfill(nv, 0);
-    for (int c = 0; c < nc; ++c) {
-        const int i = c / z, hh = c - i * z, r0 = h.row_ptr[i], deg = h.row_ptr[i + 1] - r0;
-        for (int q = 0; q < npk; ++q) {
-            uint32_t w = 0;
-            for (int j = 0; j < 2; ++j) {
-                const int k = 2 * q + j;
-                uint32_t addr = (uint32_t)(nv * VREC_B);
-                if (k < deg) {
-                    int sh = hh + h.pe_shift[r0 + k];
-                    sh = sh >= z ? sh - z : sh;
-                    const int v = h.pe_col[r0 + k] * z + sh;
-                    addr = (uint32_t)(v * VREC_B);
-                    const int f = nfill[v]++;
-                    kpos[(size_t)v * p.dvmax + f] = k;
-                    kchk[(size_t)v * p.dvmax + f] = c;
-                }
-                w |= addr << (16 * j);
-            }
-            tab.push_back(w);
-        }
+    const int nv = g.n_vars, nc = g.n_checks, z = h.z;
+    const int D = kInst[p.inst].D, DV = kInst[p.inst].DV;
+    const int CNW = (D + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
+    const int nl = 64 * p.nw;
+    std::vector<uint32_t> cn((size_t)p.cn_lanes * CNW, 0u), vn((size_t)nl * VNW, 0u);
+    std::vector<int32_t> wdeg(2 * p.nw, 0);
+    for (int w = 0; w < p.nw; ++w) wdeg[2 * w + 1] = 1 << 30;
+    auto put16 = [](uint32_t* w, int k, uint32_t addr) { w[k >> 1] |= addr << (16 * (k & 1)); };
+    // check lanes: lane c = check c (row i, index h); edge k is slot (row_ptr[i] + k) z + h
+    for (int c = 0; c < p.cn_lanes; ++c) {
+        uint32_t* w = &cn[(size_t)c * CNW];
+        const int i = c < nc ? c / z : 0, hh = c - i * z;
+        const int r0 = c < nc ? h.row_ptr[i] : 0, deg = c < nc ? h.row_ptr[i + 1] - r0 : 0;
+        // an idle lane reads and writes its own sink slot
+        const uint32_t sink = p.off_sink + (uint32_t)((c >= nc ? c - nc : 0) * SLOT_B);
+        for (int k = 0; k < D; ++k)
+            put16(w, k, c >= nc ? sink : k < deg ? (uint32_t)(((size_t)(r0 + k) * z + hh) * SLOT_B) : p.off_pad);
+        w[CNW - 1] = (p.arows > 1 && c < nc) ? (uint32_t)(i * LUT_W * 4) : 0u;
     }
-    for (int c = 0; c < nc; ++c) tab.push_back((uint32_t)(c / z));
-    // vn_edges: check record offset (from the CREC base) | position k << 16; unused slots read the
-    // zero record at n_checks (a zero message)
-    for (int v = 0; v < nv; ++v)
-        for (int f = 0; f < p.dvmax; ++f) {
-            const int c = kchk[(size_t)v * p.dvmax + f];
-            const uint32_t rec = (uint32_t)((c >= 0 ? c : nc) * p.crec_w * 4);
-            tab.push_back(rec | ((uint32_t)(c >= 0 ? kpos[(size_t)v * p.dvmax + f] : 0) << 16));
+    // variable lanes: variables by descending degree (stable), edge f of variable (col j, index
+    // hh) through proto edge pe of row i is slot pe z + (hh - shift) mod z
+    std::vector<int> order(nv);
+    for (int v = 0; v < nv; ++v) order[v] = v;
+    auto vdeg = [&](int v) { const int j = v / z; return h.col_ptr[j + 1] - h.col_ptr[j]; };
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return vdeg(x) > vdeg(y); });
+    for (int l = 0; l < nl; ++l) {
+        uint32_t* w = &vn[(size_t)l * VNW];
+        if (l >= nv) {
+            for (int f = 0; f < DV; ++f) put16(w, f, p.off_zero);
+            w[VNW - 1] = 0xFFFFFFFFu;
+            wdeg[2 * (l / 64) + 1] = 0;
+            continue;
         }
+        const int v = order[l], j = v / z, hh = v - j * z;
+        const int c0 = h.col_ptr[j], dv = h.col_ptr[j + 1] - c0;
+        for (int f = 0; f < DV; ++f) {
+            uint32_t addr = p.off_zero;
+            if (f < dv) {
+                const int pe = h.col_pe[c0 + f];
+                int hc = hh - h.pe_shift[pe];
+                hc = hc < 0 ? hc + z : hc;
+                addr = (uint32_t)(((size_t)pe * z + hc) * SLOT_B);
+            }
+            put16(w, f, addr);
+        }
+        w[VNW - 1] = (uint32_t)v;
+        wdeg[2 * (l / 64)] = std::max(wdeg[2 * (l / 64)], dv);
+        wdeg[2 * (l / 64) + 1] = std::min(wdeg[2 * (l / 64) + 1], dv);
+    }
+    const size_t bytes = (cn.size() + vn.size() + wdeg.size()) * 4;
     void* d = nullptr;
-    if (hipMalloc(&d, tab.size() * 4) != hipSuccess) { (void)hipGetLastError(); return LDPC_ERR_OOM; }
-    if (hipMemcpyAsync(d, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+    if (hipMalloc(&d, bytes) != hipSuccess) { (void)hipGetLastError(); return LDPC_ERR_OOM; }
+    uint32_t* dp = reinterpret_cast<uint32_t*>(d);
+    if (hipMemcpyAsync(dp, cn.data(), cn.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(dp + cn.size(), vn.data(), vn.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(dp + cn.size() + vn.size(), wdeg.data(), wdeg.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
         (void)hipFree(d);
         return LDPC_ERR_HIP;
     }
     ws.bs_graph = d;
+    ws.bs_graph_inst = p.inst;
     return LDPC_OK;
 }
 
-template <int DMAX, int SB>
+template <int D, int DV>
 static int launch_bs(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bs<DMAX, SB>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bs<D, DV>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)BS_LDS_MAX);
         attr = true;
     }
-    hipLaunchKernelGGL((k_bs<DMAX, SB>), dim3(nblocks), dim3(64 * nw), lds, s, a);
+    hipLaunchKernelGGL((k_bs<D, DV>), dim3(nblocks), dim3(64 * nw), lds, s, a);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 
 int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
-              bool arow_uniform, bool bcol_uniform, int64_t* counters, uint8_t* flags,
-              uint32_t* bad, hipStream_t s) {
-    const BsPlan p = bs_plan(g, mode, false, false, arow_uniform, bcol_uniform);
+              int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s) {
+    const BsPlan p = bs_plan(g, mode, false, false);
     if (!p.ok) return LDPC_ERR_UNSUPPORTED;
+    if (ws.bs_graph && ws.bs_graph_inst != p.inst) {
+        (void)hipFree(ws.bs_graph);
+        ws.bs_graph = nullptr;
+    }
     int st = bs_graph_tables(g, p, ws, s);
     if (st != LDPC_OK) return st;
     const float step = (mode == MODE_Q5) ? 0.5f : 1.0f;
@@ -661,40 +714,41 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     uint32_t* blut = alut + na;
     const int ntab = b.T * (p.arows + p.bcols);
     hipLaunchKernelGGL(k_bs_tables, dim3((unsigned)((ntab + 127) / 128)), dim3(128), 0, s, b.alpha,
-                       b.beta, g.row_ptr, b.T, g.E, g.N, g.z, p.arows, p.bcols, step, 1.0f / step,
+                       b.beta, g.row_ptr, b.T, g.E, g.N, p.arows, p.bcols, step, 1.0f / step,
                        alut, blut);
     if (hipGetLastError() != hipSuccess) return LDPC_ERR_HIP;
+    const int D = kInst[p.inst].D, DV = kInst[p.inst].DV;
+    const int CNW = (D + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
     const uint32_t* gt = reinterpret_cast<const uint32_t*>(ws.bs_graph);
     BsArgs a{};
     a.llr = llr;
     a.B = b.B;
     a.n_vars = g.n_vars;
-    a.n_checks = g.n_checks;
-    a.N = g.N;
-    a.M = g.M;
     a.T = b.T;
     a.target_bits = b.target_bits;
+    a.cn_lanes = p.cn_lanes;
+    a.cn_dmin = p.cn_dmin;
     a.inv = 1.0f / step;
-    a.cn_addr = gt;
-    a.cn_row = gt + (size_t)g.n_checks * (p.dmax / 2);
-    a.vn_edges = a.cn_row + g.n_checks;
-    a.dvmax = p.dvmax;
+    a.cn_tab = gt;
+    a.vn_tab = gt + (size_t)p.cn_lanes * CNW;
+    a.vn_wdeg = reinterpret_cast<const int32_t*>(a.vn_tab + (size_t)64 * p.nw * VNW);
     a.alut = alut;
     a.blut = blut;
+    a.arows = p.arows;
+    a.bcols = p.bcols;
     a.counters = counters;
     a.flags = flags;
     a.bad = bad;
-    a.off_crec = p.off_crec;
+    a.off_pad = p.off_pad;
+    a.off_zero = p.off_zero;
+    a.off_red = p.off_red;
     a.off_alut = p.off_alut;
     a.off_blut = p.off_blut;
-    a.off_red = p.off_red;
-    a.off_stage = p.off_stage;
-    a.crec_w = p.crec_w;
-    a.arows = p.arows;
-    a.bcols = p.bcols;
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
-    if (p.sb == 8) return launch_bs<16, 8>(a, nblocks, p.nw, p.lds, s);
-    return launch_bs<16, 10>(a, nblocks, p.nw, p.lds, s);
+    switch (p.inst) {
+        case 0: return launch_bs<15, 6>(a, nblocks, p.nw, p.lds, s);
+        default: return launch_bs<16, 8>(a, nblocks, p.nw, p.lds, s);
+    }
 }
 
 }  // namespace ldpc

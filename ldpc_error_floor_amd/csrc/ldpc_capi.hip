@@ -302,6 +302,9 @@ int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* 
         return LDPC_ERR_HIP;
     g->dev.h_row_merge = g->row_merge.data();
     g->dev.row_merge = g->d_row_merge;
+    g->dev.w_alpha_uniform = wi.alpha_uniform;
+    g->dev.w_beta_uniform = wi.beta_uniform;
+    g->dev.w_beta_nonneg = wi.beta_nonneg;
     return LDPC_OK;
 }
 

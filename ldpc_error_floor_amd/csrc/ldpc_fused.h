@@ -10,6 +10,7 @@ struct FusedWorkspace {
     void* tables = nullptr;        // per-decode tables shared by all workgroups (v5)
     size_t tables_bytes = 0;
     void* bs_graph = nullptr;      // bit-sliced kernel: graph tables (built once per context)
+    int bs_graph_inst = -1;        // the kernel instance they were built for
     void* bs_lut = nullptr;        // bit-sliced kernel: per-decode weight tables
     size_t bs_lut_bytes = 0;
     uint32_t* bs_bad = nullptr;    // [packs] 1: pack decoded by the v5 fixup
@@ -40,8 +41,7 @@ int fused5_cw(const DevGraph& g, int T);
 bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w);
 const char* bs_kernel_name(const DevGraph& g);
 int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
-              bool arow_uniform, bool bcol_uniform, int64_t* counters, uint8_t* flags,
-              uint32_t* bad, hipStream_t s);
+              int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s);
 void fused_free(FusedWorkspace& ws);
 
 }  // namespace ldpc

@@ -105,7 +105,7 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
             }
             ws.bs_bad_n = n;
         }
-        int st = bs_decode(g, b, ws, llr, mode, false, false, counters, flags, ws.bs_bad, s);
+        int st = bs_decode(g, b, ws, llr, mode, counters, flags, ws.bs_bad, s);
         if (st != LDPC_OK) return st;
         return fused5_decode(g, b, ws, llr, mode_qmax(mode), step, cu, per_edge_w != 0, nullptr,
                              counters, flags, s, ws.bs_bad);

@@ -64,8 +64,12 @@ int build_graph(const int32_t* proto, int32_t M, int32_t N, int32_t z, GraphTabl
 // per_edge_w = some row's CN / UCN weights differ inside the row at some t (sharing 1 / 4);
 // row_merge[i] = row i may share fused-kernel check groups with row i-1 (equal degree, uniform
 // row weights, the previous row's weights at every t).
+// alpha_uniform = one CN weight for every edge at each t (sharing type 3, no UCN weights);
+// beta_uniform = one VN weight for every column at each t; beta_nonneg = no beta below 0
+// (the bit-sliced kernel takes the sign of Q(beta ch) from the channel).
 struct WeightInfo {
     int per_edge_w = 0;
+    int alpha_uniform = 0, beta_uniform = 0, beta_nonneg = 0;
     std::vector<int32_t> row_merge;
 };
 int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const float* alpha_ucn,

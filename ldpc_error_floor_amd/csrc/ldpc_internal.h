@@ -28,6 +28,8 @@ struct DevGraph {
     const int32_t* h_row_merge;
     const int32_t* row_merge;
     const host::GraphTables* host;   // host tables (ldpc_host.h)
+    // weight properties of the current weights (host::WeightInfo, set by ldpc_weights_set)
+    int w_alpha_uniform, w_beta_uniform, w_beta_nonneg;
 };
 
 // Per-decode buffers and scalars.
