@@ -204,6 +204,58 @@ __device__ __forceinline__ void lut(uint32_t (&o)[NI][4], const uint32_t (&in)[N
     }
 }
 
+// bit j of the table output for NI inputs (4 b128 loads of the table's bit-j leaves at tab_j)
+template <int NI>
+__device__ __forceinline__ void lut_bit(uint32_t (&o)[NI], const uint32_t (&in)[NI][4], uint32_t tab_j) {
+    uint32_t g[NI][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const v4u w = lds_q(tab_j + (uint32_t)(q * 16));      // pairs 2q, 2q + 1
+#pragma unroll
+        for (int u = 0; u < NI; ++u) {
+            const uint32_t l0 = B3(T_LEAF, in[u][0], w.x, w.y), l1 = B3(T_LEAF, in[u][0], w.z, w.w);
+            g[u][q] = mux(in[u][1], l1, l0);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NI; ++u)
+        o[u] = mux(in[u][3], mux(in[u][2], g[u][3], g[u][2]), mux(in[u][2], g[u][1], g[u][0]));
+}
+
+// lane permutation inside each group of 4 lanes (DPP quad_perm, a VALU move)
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+constexpr int QP_X1 = 0xB1;          // [1, 0, 3, 2]
+constexpr int QP_X2 = 0x4E;          // [2, 3, 0, 1]
+
+// two smallest of {m1 <= m2} and {b1 <= b2} into m1 <= m2 (4-plane magnitudes)
+__device__ __forceinline__ void merge2(uint32_t (&m1)[4], uint32_t (&m2)[4], const uint32_t (&b1)[4],
+                                       const uint32_t (&b2)[4]) {
+    const uint32_t l = lt4(b1, m1);
+    uint32_t x[4], y[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[i] = mux(l, b2[i], m2[i]);      // the winner's second
+        y[i] = mux(l, m1[i], b1[i]);      // the loser's first
+        m1[i] = mux(l, b1[i], m1[i]);
+    }
+    const uint32_t l2 = lt4(x, y);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m2[i] = mux(l2, x[i], y[i]);
+}
+template <int CTRL>
+__device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]) {
+    uint32_t b1[4], b2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        b1[i] = qperm<CTRL>(m1[i]);
+        b2[i] = qperm<CTRL>(m2[i]);
+    }
+    merge2(m1, m2, b1, b2);
+}
+
 #ifndef BS_WPE
 #define BS_WPE 7
 #endif
@@ -214,7 +266,8 @@ template <int D, int DV>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(BS_WPE)))
 k_bs(BsArgs a) {
     constexpr int SB = (DV * QMAX + QMAX <= 127) ? 8 : 9;     // planes of S and of lw + S
-    constexpr int CNW = (D + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
+    constexpr int EPL = (D + 3) / 4;                             // edge slots per check lane
+    constexpr int CNW = (EPL + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();          // slots are LDS-absolute
     const int tid = threadIdx.x;
@@ -408,7 +461,8 @@ k_bs(BsArgs a) {
 
     vn_phase(true, false, a.off_blut + tab_b);
     const uint32_t* ct = a.cn_tab + (size_t)tid * CNW;
-    const uint32_t tab_a = a.off_alut + (is_cn ? ct[CNW - 1] : 0u);
+    // (lane j of a check's quad evaluates output bit j of the alpha table: 16 words at j * 64 B)
+    const uint32_t tab_a = a.off_alut + (is_cn ? ct[CNW - 1] : 0u) + (uint32_t)((tid & 3) * 64);
     __syncthreads();
 
     for (int t = 0; t < a.T; ++t) {
@@ -432,17 +486,18 @@ k_bs(BsArgs a) {
 #pragma unroll
                 for (int p = 0; p < CNW - 1; ++p) ca[p] = cp[p];
             }
-            auto caddr = [&](int k) __attribute__((always_inline)) -> uint32_t {
-                return (k & 1) ? (ca[k >> 1] >> 16) : (ca[k >> 1] & 0xFFFFu);
+            auto caddr = [&](int m) __attribute__((always_inline)) -> uint32_t {
+                return (m & 1) ? (ca[m >> 1] >> 16) : (ca[m >> 1] & 0xFFFFu);
             };
-            // pass 1: two minima of |V->C| and the parity of [V->C >= 0] (padding edges:
-            // negative, magnitude 15)
+            // four lanes per check, lane j taking edges k = 4m + j
+            // pass 1: two minima of |V->C| and the parity of [V->C >= 0] over the lane's edges
+            // (padding edges: negative, magnitude 15), then merged across the quad
             uint32_t m1[4], m2[4] = {~0u, ~0u, ~0u, ~0u}, par;
             read_slot(par, m1, caddr(0));
 #pragma unroll
-            for (int k = 1; k < D; ++k) {
+            for (int m = 1; m < EPL; ++m) {
                 uint32_t X[4], n;
-                read_slot(n, X, caddr(k));
+                read_slot(n, X, caddr(m));
                 const uint32_t l1 = lt4(X, m1), l2 = lt4(X, m2);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -451,25 +506,32 @@ k_bs(BsArgs a) {
                 }
                 par ^= n;
             }
+            par ^= qperm<QP_X1>(par);
+            par ^= qperm<QP_X2>(par);
+            merge_lanes<QP_X1>(m1, m2);
+            merge_lanes<QP_X2>(m1, m2);
             // message k is negative iff an even number of the OTHER edges have V->C >= 0
-            // (Main_Functions.py:251-254): par ^ n_k, with par the parity of [V->C >= 0]
-            if (D & 1) par = ~par;
-            uint32_t q[2][4];
+            // (Main_Functions.py:251-254): par ^ n_k, par the parity of [V->C >= 0] over the
+            // 4 EPL slots (an even count, padding included)
+            // weighted, quantized minima: lane j evaluates output bit j, the quad shares them
+            uint32_t qb[2];
             const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
-            lut<2>(q, mm, tab_a + (uint32_t)((t & 1) * AL * 4));
+            lut_bit<2>(qb, mm, tab_a + (uint32_t)((t & 1) * AL * 4));
+            const uint32_t q1[4] = {qperm<0x00>(qb[0]), qperm<0x55>(qb[0]), qperm<0xAA>(qb[0]), qperm<0xFF>(qb[0])};
+            const uint32_t q2[4] = {qperm<0x00>(qb[1]), qperm<0x55>(qb[1]), qperm<0xAA>(qb[1]), qperm<0xFF>(qb[1])};
             // pass 2: an edge whose |V->C| equals the minimum gets the weighted second minimum
             // (if it is not the only one, the two minima are equal), the others the minimum
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                const uint32_t addr = caddr(k);
-                if (k < cn_dmin || addr != a.off_pad) {
+            for (int m = 0; m < EPL; ++m) {
+                const uint32_t addr = caddr(m);
+                if (4 * m + 3 < cn_dmin || addr != a.off_pad) {
                     uint32_t X[4], n, Mg[4];
                     read_slot(n, X, addr);
                     uint32_t ne = X[0] ^ m1[0];
 #pragma unroll
                     for (int i = 1; i < 4; ++i) ne = B3(T_ORXOR, ne, X[i], m1[i]);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) Mg[i] = mux(ne, q[0][i], q[1][i]);
+                    for (int i = 0; i < 4; ++i) Mg[i] = mux(ne, q1[i], q2[i]);
                     write_slot(addr, par ^ n, Mg);
                 }
             }
@@ -552,7 +614,21 @@ struct BsPlan {
     uint32_t off_pad = 0, off_zero = 0, off_sink = 0, off_red = 0, off_alut = 0, off_blut = 0;
     int cn_dmin = 0;
     size_t lds = 0;
+    std::vector<int> rowbase;      // [M] first slot of proto row i: slot (i, k, h) = rowbase[i] + k z + h
 };
+
+// Slot layout.  A check lane quad reads slots rowbase[i] + (4m + j) z + h for 16 consecutive
+// checks: with z < 64 a wave's checks cross proto rows, so each row's base is padded to
+// rowbase[i-1] + z (mod 64) slots — the 64 lanes of a slot read then fall on 64 distinct
+// residues mod 64, i.e. distinct LDS banks (a slot's words are 5 s + p).
+static std::vector<int> slot_rows(const host::GraphTables& h, bool pad) {
+    std::vector<int> rb((size_t)h.M, 0);
+    for (int i = 1; i < h.M; ++i) {
+        const int base = rb[i - 1] + (h.row_ptr[i] - h.row_ptr[i - 1]) * h.z;
+        rb[i] = pad ? base + (((rb[i - 1] + h.z - base) % 64) + 64) % 64 : base;
+    }
+    return rb;
+}
 
 BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
     BsPlan p;
@@ -568,28 +644,32 @@ BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
         if (h.max_cdeg <= kInst[i].D && h.max_vdeg <= kInst[i].DV) { p.inst = i; break; }
     if (p.inst < 0) return p;
     const int nv = g.n_vars, nc = g.n_checks;
-    p.nw = (std::max(nv, nc) + 63) / 64;
-    if (p.nw > 16) return p;                                      // one variable / check per lane
-    p.cn_lanes = 64 * ((nc + 63) / 64);
+    p.cn_lanes = 64 * ((4 * nc + 63) / 64);                       // four lanes per check
+    p.nw = std::max((nv + 63) / 64, p.cn_lanes / 64);
+    if (p.nw > 16) return p;                                      // one variable per lane
     p.arows = g.w_alpha_uniform ? 1 : h.M;
     p.bcols = g.w_beta_uniform ? 1 : h.N;
-    const size_t nslot = (size_t)h.E * h.z;
-    p.off_pad = (uint32_t)(nslot * SLOT_B);
-    p.off_zero = p.off_pad + SLOT_B;
-    p.off_sink = p.off_zero + SLOT_B;
     p.cn_dmin = min_cdeg;
-    const size_t sink_end = (size_t)p.off_sink + (size_t)(p.cn_lanes - nc) * SLOT_B;
-    if (sink_end > 65535) return p;                               // 16-bit slot addresses
-    size_t o = (sink_end + 15) & ~(size_t)15;
-    p.off_red = (uint32_t)o;
-    o += 64;
-    p.off_alut = (uint32_t)o;
-    o += (size_t)2 * p.arows * LUT_W * 4;
-    p.off_blut = (uint32_t)o;
-    o += (size_t)2 * p.bcols * LUT_W * 4;
-    p.lds = (o + 15) & ~(size_t)15;
-    if (p.lds > BS_LDS_MAX) return p;
-    p.ok = true;
+    for (int pad = 1; pad >= 0; --pad) {                          // padded rows if they fit
+        p.rowbase = slot_rows(h, pad && h.z < 64);
+        const size_t nslot = (size_t)p.rowbase[h.M - 1] + (size_t)(h.row_ptr[h.M] - h.row_ptr[h.M - 1]) * h.z;
+        p.off_pad = (uint32_t)(nslot * SLOT_B);
+        p.off_zero = p.off_pad + SLOT_B;
+        p.off_sink = p.off_zero + SLOT_B;
+        const size_t sink_end = (size_t)p.off_sink + (size_t)(p.cn_lanes - 4 * nc) * SLOT_B;
+        if (sink_end > 65535) continue;                           // 16-bit slot addresses
+        size_t o = (sink_end + 15) & ~(size_t)15;
+        p.off_red = (uint32_t)o;
+        o += 64;
+        p.off_alut = (uint32_t)o;
+        o += (size_t)2 * p.arows * LUT_W * 4;
+        p.off_blut = (uint32_t)o;
+        o += (size_t)2 * p.bcols * LUT_W * 4;
+        p.lds = (o + 15) & ~(size_t)15;
+        if (p.lds > BS_LDS_MAX) continue;
+        p.ok = true;
+        break;
+    }
     return p;
 }
 
@@ -615,52 +695,90 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
     const host::GraphTables& h = *g.host;
     const int nv = g.n_vars, nc = g.n_checks, z = h.z;
     const int D = kInst[p.inst].D, DV = kInst[p.inst].DV;
-    const int CNW = (D + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
+    const int EPL = (D + 3) / 4;
+    const int CNW = (EPL + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
     const int nl = 64 * p.nw;
     std::vector<uint32_t> cn((size_t)p.cn_lanes * CNW, 0u), vn((size_t)nl * VNW, 0u);
     std::vector<int32_t> wdeg(2 * p.nw, 0);
-    for (int w = 0; w < p.nw; ++w) wdeg[2 * w + 1] = 1 << 30;
     auto put16 = [](uint32_t* w, int k, uint32_t addr) { w[k >> 1] |= addr << (16 * (k & 1)); };
-    // check lanes: lane c = check c (row i, index h); edge k is slot (row_ptr[i] + k) z + h
-    for (int c = 0; c < p.cn_lanes; ++c) {
-        uint32_t* w = &cn[(size_t)c * CNW];
+    auto slot_addr = [&](int i, int k, int hc) {
+        return (uint32_t)(((size_t)p.rowbase[i] + (size_t)k * z + hc) * SLOT_B);
+    };
+    // check lanes: lane L = 4 c + j (check c = row i, index h) takes edges k = 4 m + j
+    for (int L = 0; L < p.cn_lanes; ++L) {
+        uint32_t* w = &cn[(size_t)L * CNW];
+        const int c = L >> 2, j = L & 3;
         const int i = c < nc ? c / z : 0, hh = c - i * z;
-        const int r0 = c < nc ? h.row_ptr[i] : 0, deg = c < nc ? h.row_ptr[i + 1] - r0 : 0;
+        const int deg = c < nc ? h.row_ptr[i + 1] - h.row_ptr[i] : 0;
         // an idle lane reads and writes its own sink slot
-        const uint32_t sink = p.off_sink + (uint32_t)((c >= nc ? c - nc : 0) * SLOT_B);
-        for (int k = 0; k < D; ++k)
-            put16(w, k, c >= nc ? sink : k < deg ? (uint32_t)(((size_t)(r0 + k) * z + hh) * SLOT_B) : p.off_pad);
+        const uint32_t sink = p.off_sink + (uint32_t)((c >= nc ? L - 4 * nc : 0) * SLOT_B);
+        for (int m = 0; m < EPL; ++m) {
+            const int k = 4 * m + j;
+            put16(w, m, c >= nc ? sink : k < deg ? slot_addr(i, k, hh) : p.off_pad);
+        }
         w[CNW - 1] = (p.arows > 1 && c < nc) ? (uint32_t)(i * LUT_W * 4) : 0u;
     }
-    // variable lanes: variables by descending degree (stable), edge f of variable (col j, index
-    // hh) through proto edge pe of row i is slot pe z + (hh - shift) mod z
+    // variable lanes: variables by descending degree in chunks of 64; the chunks are dealt to
+    // waves so that the SIMDs (wave w on SIMD w mod 4) get similar work (a chunk costs about
+    // 3 + dw units, dw its largest degree); edge f of variable (col j, index hh) through proto
+    // edge pe (row i, position k) is slot (i, k, (hh - shift) mod z)
     std::vector<int> order(nv);
     for (int v = 0; v < nv; ++v) order[v] = v;
     auto vdeg = [&](int v) { const int j = v / z; return h.col_ptr[j + 1] - h.col_ptr[j]; };
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return vdeg(x) > vdeg(y); });
-    for (int l = 0; l < nl; ++l) {
-        uint32_t* w = &vn[(size_t)l * VNW];
-        if (l >= nv) {
-            for (int f = 0; f < DV; ++f) put16(w, f, p.off_zero);
-            w[VNW - 1] = 0xFFFFFFFFu;
-            wdeg[2 * (l / 64) + 1] = 0;
-            continue;
+    const int nch = (nv + 63) / 64;
+    std::vector<int> wave_of(nch, -1), simd_load(4, 0);
+    std::vector<char> used(p.nw, 0);
+    for (int ch = 0; ch < nch; ++ch) {                 // chunks come in descending cost order
+        const int cost = 3 + vdeg(order[64 * ch]);
+        int best = -1;
+        for (int sm = 0; sm < 4; ++sm) {
+            bool free_slot = false;
+            for (int w = sm; w < p.nw; w += 4) free_slot |= !used[w];
+            if (free_slot && (best < 0 || simd_load[sm] < simd_load[best])) best = sm;
         }
-        const int v = order[l], j = v / z, hh = v - j * z;
-        const int c0 = h.col_ptr[j], dv = h.col_ptr[j + 1] - c0;
-        for (int f = 0; f < DV; ++f) {
-            uint32_t addr = p.off_zero;
-            if (f < dv) {
-                const int pe = h.col_pe[c0 + f];
-                int hc = hh - h.pe_shift[pe];
-                hc = hc < 0 ? hc + z : hc;
-                addr = (uint32_t)(((size_t)pe * z + hc) * SLOT_B);
+        int w = best;
+        while (used[w]) w += 4;
+        used[w] = 1;
+        wave_of[ch] = w;
+        simd_load[best] += cost;
+    }
+    for (int w = 0; w < p.nw; ++w) {
+        wdeg[2 * w] = 0;
+        wdeg[2 * w + 1] = 0;
+        for (int l = 0; l < 64; ++l) {
+            uint32_t* q = &vn[(size_t)(64 * w + l) * VNW];
+            for (int f = 0; f < DV; ++f) put16(q, f, p.off_zero);
+            q[VNW - 1] = 0xFFFFFFFFu;
+        }
+    }
+    for (int ch = 0; ch < nch; ++ch) {
+        const int w = wave_of[ch];
+        int dmax = 0, dmin = 1 << 30;
+        for (int l = 0; l < 64; ++l) {
+            uint32_t* q = &vn[(size_t)(64 * w + l) * VNW];
+            const int o = 64 * ch + l;
+            if (o >= nv) { dmin = 0; continue; }
+            const int v = order[o], j = v / z, hh = v - j * z;
+            const int c0 = h.col_ptr[j], dv = h.col_ptr[j + 1] - c0;
+            q[0] = 0u;
+            for (int pw = 1; pw < VNW - 1; ++pw) q[pw] = 0u;
+            for (int f = 0; f < DV; ++f) {
+                uint32_t addr = p.off_zero;
+                if (f < dv) {
+                    const int pe = h.col_pe[c0 + f], i = h.pe_row[pe];
+                    int hc = hh - h.pe_shift[pe];
+                    hc = hc < 0 ? hc + z : hc;
+                    addr = slot_addr(i, pe - h.row_ptr[i], hc);
+                }
+                put16(q, f, addr);
             }
-            put16(w, f, addr);
+            q[VNW - 1] = (uint32_t)v;
+            dmax = std::max(dmax, dv);
+            dmin = std::min(dmin, dv);
         }
-        w[VNW - 1] = (uint32_t)v;
-        wdeg[2 * (l / 64)] = std::max(wdeg[2 * (l / 64)], dv);
-        wdeg[2 * (l / 64) + 1] = std::min(wdeg[2 * (l / 64) + 1], dv);
+        wdeg[2 * w] = dmax;
+        wdeg[2 * w + 1] = dmin;
     }
     const size_t bytes = (cn.size() + vn.size() + wdeg.size()) * 4;
     void* d = nullptr;
@@ -718,7 +836,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
                        alut, blut);
     if (hipGetLastError() != hipSuccess) return LDPC_ERR_HIP;
     const int D = kInst[p.inst].D, DV = kInst[p.inst].DV;
-    const int CNW = (D + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
+    const int CNW = ((D + 3) / 4 + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
     const uint32_t* gt = reinterpret_cast<const uint32_t*>(ws.bs_graph);
     BsArgs a{};
     a.llr = llr;
