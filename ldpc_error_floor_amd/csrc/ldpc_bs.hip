@@ -44,9 +44,10 @@ constexpr size_t BS_LDS_MAX = 160 * 1024;
 struct BsArgs {
     const float* llr;
     int64_t B;
-    int n_vars, T, target_bits, cn_lanes, cn_dmin;
+    int n_vars, n_checks, T, target_bits, cn_lanes, cn_dmin;
     float inv;
-    const uint32_t* cn_tab;      // [cn_lanes][CNW]: slot byte addresses (2 per word), table offset
+    const int32_t* row_ptr;      // [M + 1] proto edges of each row (the check degrees)
+    int z, row_slots;            // slots of a proto row's region: 4 EPL z + bank padding
     const uint32_t* vn_tab;      // [64 nw][VNW]: slot byte addresses (2 per word), variable (-1 idle)
     const int32_t* vn_wdeg;      // [nw][2] most and fewest edges of a variable of each wave
     const uint32_t* alut;        // [T][arows][LUT_W]: Q(relu(alpha m step)) for m = 0..15
@@ -267,7 +268,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(BS_WP
 k_bs(BsArgs a) {
     constexpr int SB = (DV * QMAX + QMAX <= 127) ? 8 : 9;     // planes of S and of lw + S
     constexpr int EPL = (D + 3) / 4;                             // edge slots per check lane
-    constexpr int CNW = (EPL + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
+    constexpr int VNW = (DV + 1) / 2 + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();          // slots are LDS-absolute
     const int tid = threadIdx.x;
@@ -287,6 +288,9 @@ k_bs(BsArgs a) {
     // (the slot addresses are reloaded from the L2-resident tables in each phase rather than
     // held in registers through the whole decode)
     const uint32_t* vt = a.vn_tab + (size_t)tid * VNW;
+    uint32_t va[VNW - 1];                                 // slot byte addresses, two per word
+#pragma unroll
+    for (int p = 0; p < VNW - 1; ++p) va[p] = vt[p];
     const int v = (int)vt[VNW - 1];                       // -1: no variable
     int dw = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * wave]);
     int dwmin = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * wave + 1]);
@@ -341,13 +345,8 @@ k_bs(BsArgs a) {
     //          Tv = clamp(Q(beta_{t+1} ch) + S) and V->C_e = clamp(Tv - C->V_e, +-15) per edge
     auto vn_phase = [&](const bool first, const bool last, const uint32_t btab)
                         __attribute__((always_inline)) {
-        uint32_t va[VNW - 1];
-        {
-            const uint32_t* vp = vt;
-            asm volatile("" : "+v"(vp));                  // a load per phase, not hoisted
 #pragma unroll
-            for (int p = 0; p < VNW - 1; ++p) va[p] = vp[p];
-        }
+        for (int p = 0; p < VNW - 1; ++p) asm volatile("" : "+v"(va[p]));   // unpacked per use
         auto vaddr = [&](int f) __attribute__((always_inline)) -> uint32_t {
             return (f & 1) ? (va[f >> 1] >> 16) : (va[f >> 1] & 0xFFFFu);
         };
@@ -460,9 +459,22 @@ k_bs(BsArgs a) {
     };
 
     vn_phase(true, false, a.off_blut + tab_b);
-    const uint32_t* ct = a.cn_tab + (size_t)tid * CNW;
+    // check lanes: lane 4 c + j (check c = row i, index h) takes edges k = 4 m + j, at slots
+    // i R + k z + h (R = a.row_slots); k >= deg are padding slots, set to all ones here and
+    // never written; idle lanes (c >= n_checks) read slot 0 onward and write nothing
+    const int cc = tid >> 2, cj = tid & 3;
+    const int ci = min(cc / a.z, a.n_checks / a.z - 1);
+    const int cdeg = (cc < a.n_checks) ? a.row_ptr[ci + 1] - a.row_ptr[ci] : 0;
+    uint32_t cbase = (cc < a.n_checks) ? (uint32_t)((ci * a.row_slots + cj * a.z + (cc - ci * a.z)) * SLOT_B) : 0u;
+    const uint32_t cstride = (uint32_t)(4 * a.z * SLOT_B);
+    if (is_cn) {
+        const uint32_t ones[4] = {~0u, ~0u, ~0u, ~0u};
+#pragma unroll
+        for (int m = 0; m < EPL; ++m)
+            if (cc < a.n_checks && 4 * m + cj >= cdeg) write_slot(cbase + m * cstride, ~0u, ones);
+    }
     // (lane j of a check's quad evaluates output bit j of the alpha table: 16 words at j * 64 B)
-    const uint32_t tab_a = a.off_alut + (is_cn ? ct[CNW - 1] : 0u) + (uint32_t)((tid & 3) * 64);
+    const uint32_t tab_a = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * 64);
     __syncthreads();
 
     for (int t = 0; t < a.T; ++t) {
@@ -479,16 +491,8 @@ k_bs(BsArgs a) {
         }
         // ======== check nodes ===================================================================
         if (is_cn) {
-            uint32_t ca[CNW - 1];
-            {
-                const uint32_t* cp = ct;
-                asm volatile("" : "+v"(cp));              // a load per phase, not hoisted
-#pragma unroll
-                for (int p = 0; p < CNW - 1; ++p) ca[p] = cp[p];
-            }
-            auto caddr = [&](int m) __attribute__((always_inline)) -> uint32_t {
-                return (m & 1) ? (ca[m >> 1] >> 16) : (ca[m >> 1] & 0xFFFFu);
-            };
+            asm volatile("" : "+v"(cbase));
+            auto caddr = [&](int m) __attribute__((always_inline)) -> uint32_t { return cbase + m * cstride; };
             // four lanes per check, lane j taking edges k = 4m + j
             // pass 1: two minima of |V->C| and the parity of [V->C >= 0] over the lane's edges
             // (padding edges: negative, magnitude 15), then merged across the quad
@@ -524,7 +528,7 @@ k_bs(BsArgs a) {
 #pragma unroll
             for (int m = 0; m < EPL; ++m) {
                 const uint32_t addr = caddr(m);
-                if (4 * m + 3 < cn_dmin || addr != a.off_pad) {
+                if (4 * m + 3 < cn_dmin || 4 * m + cj < cdeg) {
                     uint32_t X[4], n, Mg[4];
                     read_slot(n, X, addr);
                     uint32_t ne = X[0] ^ m1[0];
@@ -610,26 +614,17 @@ constexpr BsInst kInst[] = {{15, 6}, {16, 8}};
 
 struct BsPlan {
     bool ok = false;
-    int inst = -1, nw = 0, cn_lanes = 0, arows = 1, bcols = 1;
-    uint32_t off_pad = 0, off_zero = 0, off_sink = 0, off_red = 0, off_alut = 0, off_blut = 0;
+    int inst = -1, nw = 0, cn_lanes = 0, arows = 1, bcols = 1, row_slots = 0;
+    uint32_t off_pad = 0, off_zero = 0, off_red = 0, off_alut = 0, off_blut = 0;
     int cn_dmin = 0;
     size_t lds = 0;
-    std::vector<int> rowbase;      // [M] first slot of proto row i: slot (i, k, h) = rowbase[i] + k z + h
 };
 
-// Slot layout.  A check lane quad reads slots rowbase[i] + (4m + j) z + h for 16 consecutive
-// checks: with z < 64 a wave's checks cross proto rows, so each row's base is padded to
-// rowbase[i-1] + z (mod 64) slots — the 64 lanes of a slot read then fall on 64 distinct
-// residues mod 64, i.e. distinct LDS banks (a slot's words are 5 s + p).
-static std::vector<int> slot_rows(const host::GraphTables& h, bool pad) {
-    std::vector<int> rb((size_t)h.M, 0);
-    for (int i = 1; i < h.M; ++i) {
-        const int base = rb[i - 1] + (h.row_ptr[i] - h.row_ptr[i - 1]) * h.z;
-        rb[i] = pad ? base + (((rb[i - 1] + h.z - base) % 64) + 64) % 64 : base;
-    }
-    return rb;
-}
-
+// Slot layout: proto row i owns slots i R .. i R + 4 EPL z - 1, slot (i, k, h) = i R + k z + h
+// (k >= the row degree: padding slots).  A check lane quad reads slots i R + (4 m + j) z + h
+// for 16 consecutive checks; with z < 64 a wave's checks cross proto rows, so R is padded to
+// z (mod 64): the 64 lanes then read 64 distinct slot residues mod 64, i.e. distinct LDS
+// banks (a slot's words are 5 s + p).
 BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
     BsPlan p;
     const char* e = getenv("LDPC_BS");
@@ -643,22 +638,24 @@ BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
     for (int i = 0; i < (int)(sizeof(kInst) / sizeof(kInst[0])); ++i)
         if (h.max_cdeg <= kInst[i].D && h.max_vdeg <= kInst[i].DV) { p.inst = i; break; }
     if (p.inst < 0) return p;
+    const int EPL = (kInst[p.inst].D + 3) / 4;
     const int nv = g.n_vars, nc = g.n_checks;
     p.cn_lanes = 64 * ((4 * nc + 63) / 64);                       // four lanes per check
     p.nw = std::max((nv + 63) / 64, p.cn_lanes / 64);
     if (p.nw > 16) return p;                                      // one variable per lane
     p.arows = g.w_alpha_uniform ? 1 : h.M;
     p.bcols = g.w_beta_uniform ? 1 : h.N;
-    p.cn_dmin = min_cdeg;
+    // idle check lanes: every write is decided per lane
+    p.cn_dmin = (p.cn_lanes == 4 * nc) ? min_cdeg : 0;
     for (int pad = 1; pad >= 0; --pad) {                          // padded rows if they fit
-        p.rowbase = slot_rows(h, pad && h.z < 64);
-        const size_t nslot = (size_t)p.rowbase[h.M - 1] + (size_t)(h.row_ptr[h.M] - h.row_ptr[h.M - 1]) * h.z;
+        const int span = 4 * EPL * h.z;
+        p.row_slots = span + ((pad && h.z < 64) ? ((h.z - span) % 64 + 64) % 64 : 0);
+        const size_t nslot = (size_t)(h.M - 1) * p.row_slots + span;
         p.off_pad = (uint32_t)(nslot * SLOT_B);
         p.off_zero = p.off_pad + SLOT_B;
-        p.off_sink = p.off_zero + SLOT_B;
-        const size_t sink_end = (size_t)p.off_sink + (size_t)(p.cn_lanes - 4 * nc) * SLOT_B;
-        if (sink_end > 65535) continue;                           // 16-bit slot addresses
-        size_t o = (sink_end + 15) & ~(size_t)15;
+        const size_t slot_end = (size_t)p.off_zero + SLOT_B;
+        if (slot_end > 65535) continue;                           // 16-bit slot addresses
+        size_t o = (slot_end + 15) & ~(size_t)15;
         p.off_red = (uint32_t)o;
         o += 64;
         p.off_alut = (uint32_t)o;
@@ -694,30 +691,15 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
     if (ws.bs_graph) return LDPC_OK;
     const host::GraphTables& h = *g.host;
     const int nv = g.n_vars, nc = g.n_checks, z = h.z;
-    const int D = kInst[p.inst].D, DV = kInst[p.inst].DV;
-    const int EPL = (D + 3) / 4;
-    const int CNW = (EPL + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
+    const int DV = kInst[p.inst].DV;
+    const int VNW = (DV + 1) / 2 + 1;
     const int nl = 64 * p.nw;
-    std::vector<uint32_t> cn((size_t)p.cn_lanes * CNW, 0u), vn((size_t)nl * VNW, 0u);
+    std::vector<uint32_t> vn((size_t)nl * VNW, 0u);
     std::vector<int32_t> wdeg(2 * p.nw, 0);
     auto put16 = [](uint32_t* w, int k, uint32_t addr) { w[k >> 1] |= addr << (16 * (k & 1)); };
     auto slot_addr = [&](int i, int k, int hc) {
-        return (uint32_t)(((size_t)p.rowbase[i] + (size_t)k * z + hc) * SLOT_B);
+        return (uint32_t)(((size_t)i * p.row_slots + (size_t)k * z + hc) * SLOT_B);
     };
-    // check lanes: lane L = 4 c + j (check c = row i, index h) takes edges k = 4 m + j
-    for (int L = 0; L < p.cn_lanes; ++L) {
-        uint32_t* w = &cn[(size_t)L * CNW];
-        const int c = L >> 2, j = L & 3;
-        const int i = c < nc ? c / z : 0, hh = c - i * z;
-        const int deg = c < nc ? h.row_ptr[i + 1] - h.row_ptr[i] : 0;
-        // an idle lane reads and writes its own sink slot
-        const uint32_t sink = p.off_sink + (uint32_t)((c >= nc ? L - 4 * nc : 0) * SLOT_B);
-        for (int m = 0; m < EPL; ++m) {
-            const int k = 4 * m + j;
-            put16(w, m, c >= nc ? sink : k < deg ? slot_addr(i, k, hh) : p.off_pad);
-        }
-        w[CNW - 1] = (p.arows > 1 && c < nc) ? (uint32_t)(i * LUT_W * 4) : 0u;
-    }
     // variable lanes: variables by descending degree in chunks of 64; the chunks are dealt to
     // waves so that the SIMDs (wave w on SIMD w mod 4) get similar work (a chunk costs about
     // 3 + dw units, dw its largest degree); edge f of variable (col j, index hh) through proto
@@ -780,13 +762,12 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
         wdeg[2 * w] = dmax;
         wdeg[2 * w + 1] = dmin;
     }
-    const size_t bytes = (cn.size() + vn.size() + wdeg.size()) * 4;
+    const size_t bytes = (vn.size() + wdeg.size()) * 4;
     void* d = nullptr;
     if (hipMalloc(&d, bytes) != hipSuccess) { (void)hipGetLastError(); return LDPC_ERR_OOM; }
     uint32_t* dp = reinterpret_cast<uint32_t*>(d);
-    if (hipMemcpyAsync(dp, cn.data(), cn.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(dp + cn.size(), vn.data(), vn.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(dp + cn.size() + vn.size(), wdeg.data(), wdeg.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+    if (hipMemcpyAsync(dp, vn.data(), vn.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(dp + vn.size(), wdeg.data(), wdeg.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
         (void)hipFree(d);
         return LDPC_ERR_HIP;
@@ -836,19 +817,23 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
                        alut, blut);
     if (hipGetLastError() != hipSuccess) return LDPC_ERR_HIP;
     const int D = kInst[p.inst].D, DV = kInst[p.inst].DV;
-    const int CNW = ((D + 3) / 4 + 1) / 2 + 1, VNW = (DV + 1) / 2 + 1;
+    const int VNW = (DV + 1) / 2 + 1;
+    (void)D;
     const uint32_t* gt = reinterpret_cast<const uint32_t*>(ws.bs_graph);
     BsArgs a{};
     a.llr = llr;
     a.B = b.B;
     a.n_vars = g.n_vars;
+    a.n_checks = g.n_checks;
     a.T = b.T;
     a.target_bits = b.target_bits;
     a.cn_lanes = p.cn_lanes;
     a.cn_dmin = p.cn_dmin;
     a.inv = 1.0f / step;
-    a.cn_tab = gt;
-    a.vn_tab = gt + (size_t)p.cn_lanes * CNW;
+    a.row_ptr = g.row_ptr;
+    a.z = g.z;
+    a.row_slots = p.row_slots;
+    a.vn_tab = gt;
     a.vn_wdeg = reinterpret_cast<const int32_t*>(a.vn_tab + (size_t)64 * p.nw * VNW);
     a.alut = alut;
     a.blut = blut;
