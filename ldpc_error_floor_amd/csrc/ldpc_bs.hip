@@ -257,8 +257,11 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
     merge2(m1, m2, b1, b2);
 }
 
+// 8 waves per SIMD (64 VGPRs): three 9-wave workgroups per CU.  At a 72-register budget only
+// two were resident (the waves of a workgroup are not spread evenly over the SIMDs): measured
+// 7.56 ms (72 VGPRs) -> 6.51 ms (64) per 2^20-codeword C2 decode (tools/bs_variant.sh A/B).
 #ifndef BS_WPE
-#define BS_WPE 7
+#define BS_WPE 8
 #endif
 #ifndef BS_KEEP
 #define BS_KEEP 0
