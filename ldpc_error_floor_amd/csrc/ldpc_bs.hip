@@ -231,6 +231,29 @@ __device__ __forceinline__ uint32_t qperm(uint32_t x) {
 constexpr int QP_X1 = 0xB1;          // [1, 0, 3, 2]
 constexpr int QP_X2 = 0x4E;          // [2, 3, 0, 1]
 
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+// OR / sum over the wave (wave-uniform result): butterflies inside each row of 16 lanes by DPP
+// (quad_perm, row_half_mirror, row_mirror), then the four row results by readlane
+__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
+    x |= dpp<QP_X1>(x);
+    x |= dpp<QP_X2>(x);
+    x |= dpp<0x141>(x);
+    x |= dpp<0x140>(x);
+    return (uint32_t)(__builtin_amdgcn_readlane((int)x, 15) | __builtin_amdgcn_readlane((int)x, 31) |
+                      __builtin_amdgcn_readlane((int)x, 47) | __builtin_amdgcn_readlane((int)x, 63));
+}
+__device__ __forceinline__ uint32_t wave_add(uint32_t x) {
+    x += dpp<QP_X1>(x);
+    x += dpp<QP_X2>(x);
+    x += dpp<0x141>(x);
+    x += dpp<0x140>(x);
+    return (uint32_t)(__builtin_amdgcn_readlane((int)x, 15) + __builtin_amdgcn_readlane((int)x, 31) +
+                      __builtin_amdgcn_readlane((int)x, 47) + __builtin_amdgcn_readlane((int)x, 63));
+}
+
 // two smallest of {m1 <= m2} and {b1 <= b2} into m1 <= m2 (4-plane magnitudes)
 __device__ __forceinline__ void merge2(uint32_t (&m1)[4], uint32_t (&m2)[4], const uint32_t (&b1)[4],
                                        const uint32_t (&b2)[4]) {
@@ -406,13 +429,10 @@ k_bs(BsArgs a) {
                 apos = hd & nz;
                 nb = (uint32_t)__popc(hd);
             }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                wr |= __shfl_xor(wr, o);
-                if (last) {
-                    apos |= __shfl_xor(apos, o);
-                    nb += __shfl_xor(nb, o);
-                }
+            wr = wave_or(wr);
+            if (last) {
+                apos = wave_or(apos);
+                nb = wave_add(nb);
             }
             if (lane == 0) {
                 if (wr) atomicOr(&RED[0], wr);
