@@ -47,7 +47,8 @@ struct BsArgs {
     int n_vars, n_checks, T, target_bits, cn_lanes, cn_dmin;
     float inv;
     const int32_t* row_ptr;      // [M + 1] proto edges of each row (the check degrees)
-    int z, row_slots;            // slots of a proto row's region: 4 EPL z + bank padding
+    const int32_t* row_lay;      // [M][2] slot layout of each proto row: first slot, j-block stride
+    int z;
     const uint32_t* vn_tab;      // [64 nw][VNW]: slot byte addresses (2 per word), variable (-1 idle)
     const int32_t* vn_wdeg;      // [nw][2] most and fewest edges of a variable of each wave
     const uint32_t* alut;        // [T][arows][LUT_W]: Q(relu(alpha m step)) for m = 0..15
@@ -289,11 +290,13 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
 #ifndef BS_KEEP
 #define BS_KEEP 0
 #endif
-template <int D, int DV>
+template <int D, int DV, int LPC>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(BS_WPE)))
 k_bs(BsArgs a) {
+    static_assert(LPC == 2 || LPC == 4, "lanes per check");
     constexpr int SB = (DV * QMAX + QMAX <= 127) ? 8 : 9;     // planes of S and of lw + S
-    constexpr int EPL = (D + 3) / 4;                             // edge slots per check lane
+    constexpr int EPL = (D + LPC - 1) / LPC;                     // edge slots per check lane
+    constexpr int OB = 4 / LPC;                                  // alpha-table output bits per lane
     constexpr int VNW = (DV + 1) / 2 + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();          // slots are LDS-absolute
@@ -482,22 +485,17 @@ k_bs(BsArgs a) {
     };
 
     vn_phase(true, false, a.off_blut + tab_b);
-    // check lanes: lane 4 c + j (check c = row i, index h) takes edges k = 4 m + j, at slots
-    // i R + k z + h (R = a.row_slots); k >= deg are padding slots, set to all ones here and
-    // never written; idle lanes (c >= n_checks) read slot 0 onward and write nothing
-    const int cc = tid >> 2, cj = tid & 3;
+    // check lanes: lane LPC c + j (check c = row i, index h) takes edges k = LPC m + j, at slots
+    // first_i + j A_i + m z + h (a.row_lay); edges past the degree read the all-ones PAD slot
+    // and are not written; idle lanes (c >= n_checks) read PAD only
+    const int cc = tid / LPC, cj = tid % LPC;
     const int ci = min(cc / a.z, a.n_checks / a.z - 1);
     const int cdeg = (cc < a.n_checks) ? a.row_ptr[ci + 1] - a.row_ptr[ci] : 0;
-    uint32_t cbase = (cc < a.n_checks) ? (uint32_t)((ci * a.row_slots + cj * a.z + (cc - ci * a.z)) * SLOT_B) : 0u;
-    const uint32_t cstride = (uint32_t)(4 * a.z * SLOT_B);
-    if (is_cn) {
-        const uint32_t ones[4] = {~0u, ~0u, ~0u, ~0u};
-#pragma unroll
-        for (int m = 0; m < EPL; ++m)
-            if (cc < a.n_checks && 4 * m + cj >= cdeg) write_slot(cbase + m * cstride, ~0u, ones);
-    }
-    // (lane j of a check's quad evaluates output bit j of the alpha table: 16 words at j * 64 B)
-    const uint32_t tab_a = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * 64);
+    uint32_t cbase = (uint32_t)((a.row_lay[2 * ci] + cj * a.row_lay[2 * ci + 1] + (cc - ci * a.z)) * SLOT_B);
+    const uint32_t cstride = (uint32_t)(a.z * SLOT_B);
+    // (lane j of a check's group evaluates output bits OB j .. OB j + OB - 1 of the alpha table:
+    // 16 words per bit, at 64 B per bit)
+    const uint32_t tab_a = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * OB * 64);
     __syncthreads();
 
     for (int t = 0; t < a.T; ++t) {
@@ -515,10 +513,15 @@ k_bs(BsArgs a) {
         // ======== check nodes ===================================================================
         if (is_cn) {
             asm volatile("" : "+v"(cbase));
-            auto caddr = [&](int m) __attribute__((always_inline)) -> uint32_t { return cbase + m * cstride; };
-            // four lanes per check, lane j taking edges k = 4m + j
+            // slot m of the lane: always a real edge while LPC m + LPC - 1 < cn_dmin
+            auto real = [&](int m) __attribute__((always_inline)) -> bool {
+                return LPC * m + LPC - 1 < cn_dmin || LPC * m + cj < cdeg;
+            };
+            auto caddr = [&](int m) __attribute__((always_inline)) -> uint32_t {
+                return real(m) ? cbase + m * cstride : a.off_pad;
+            };
             // pass 1: two minima of |V->C| and the parity of [V->C >= 0] over the lane's edges
-            // (padding edges: negative, magnitude 15), then merged across the quad
+            // (padding edges: negative, magnitude 15), then merged across the lane group
             uint32_t m1[4], m2[4] = {~0u, ~0u, ~0u, ~0u}, par;
             read_slot(par, m1, caddr(0));
 #pragma unroll
@@ -534,24 +537,45 @@ k_bs(BsArgs a) {
                 par ^= n;
             }
             par ^= qperm<QP_X1>(par);
-            par ^= qperm<QP_X2>(par);
             merge_lanes<QP_X1>(m1, m2);
-            merge_lanes<QP_X2>(m1, m2);
+            if (LPC == 4) {
+                par ^= qperm<QP_X2>(par);
+                merge_lanes<QP_X2>(m1, m2);
+            }
             // message k is negative iff an even number of the OTHER edges have V->C >= 0
             // (Main_Functions.py:251-254): par ^ n_k, par the parity of [V->C >= 0] over the
-            // 4 EPL slots (an even count, padding included)
-            // weighted, quantized minima: lane j evaluates output bit j, the quad shares them
-            uint32_t qb[2];
-            const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
-            lut_bit<2>(qb, mm, tab_a + (uint32_t)((t & 1) * AL * 4));
-            const uint32_t q1[4] = {qperm<0x00>(qb[0]), qperm<0x55>(qb[0]), qperm<0xAA>(qb[0]), qperm<0xFF>(qb[0])};
-            const uint32_t q2[4] = {qperm<0x00>(qb[1]), qperm<0x55>(qb[1]), qperm<0xAA>(qb[1]), qperm<0xFF>(qb[1])};
+            // LPC EPL slots (an even count, padding included)
+            // weighted, quantized minima: each lane evaluates OB output bits, the group shares them
+            uint32_t q1[4], q2[4];
+            {
+                const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
+                const uint32_t tab = tab_a + (uint32_t)((t & 1) * AL * 4);
+                uint32_t qb[OB][2];
+#pragma unroll
+                for (int b = 0; b < OB; ++b) {
+                    uint32_t o[2];
+                    lut_bit<2>(o, mm, tab + (uint32_t)(b * 64));
+                    qb[b][0] = o[0];
+                    qb[b][1] = o[1];
+                }
+                if (LPC == 4) {
+                    q1[0] = qperm<0x00>(qb[0][0]); q1[1] = qperm<0x55>(qb[0][0]);
+                    q1[2] = qperm<0xAA>(qb[0][0]); q1[3] = qperm<0xFF>(qb[0][0]);
+                    q2[0] = qperm<0x00>(qb[0][1]); q2[1] = qperm<0x55>(qb[0][1]);
+                    q2[2] = qperm<0xAA>(qb[0][1]); q2[3] = qperm<0xFF>(qb[0][1]);
+                } else {                // lane 0 of a pair holds bits 0, 1; lane 1 bits 2, 3
+                    q1[0] = qperm<0xA0>(qb[0][0]); q1[1] = qperm<0xA0>(qb[OB - 1][0]);
+                    q1[2] = qperm<0xF5>(qb[0][0]); q1[3] = qperm<0xF5>(qb[OB - 1][0]);
+                    q2[0] = qperm<0xA0>(qb[0][1]); q2[1] = qperm<0xA0>(qb[OB - 1][1]);
+                    q2[2] = qperm<0xF5>(qb[0][1]); q2[3] = qperm<0xF5>(qb[OB - 1][1]);
+                }
+            }
             // pass 2: an edge whose |V->C| equals the minimum gets the weighted second minimum
             // (if it is not the only one, the two minima are equal), the others the minimum
 #pragma unroll
             for (int m = 0; m < EPL; ++m) {
-                const uint32_t addr = caddr(m);
-                if (4 * m + 3 < cn_dmin || 4 * m + cj < cdeg) {
+                if (real(m)) {
+                    const uint32_t addr = cbase + m * cstride;
                     uint32_t X[4], n, Mg[4];
                     read_slot(n, X, addr);
                     uint32_t ne = X[0] ^ m1[0];
@@ -632,26 +656,59 @@ __global__ void k_bs_tables(const float* __restrict__ alpha, const float* __rest
 
 // ---- host: planning, graph tables, launch -------------------------------------------------
 // kernel instances (D = check-degree bound, DV = variable-degree bound)
-struct BsInst { int D, DV; };
-constexpr BsInst kInst[] = {{15, 6}, {16, 8}};
+// (LPC = lanes per check: 4 measured 6.31 ms against 2's 6.73 ms per C2 decode, same box)
+struct BsInst { int D, DV, LPC; };
+constexpr BsInst kInst[] = {{15, 6, 4}, {16, 8, 4}, {15, 6, 2}};
 
 struct BsPlan {
     bool ok = false;
-    int inst = -1, nw = 0, cn_lanes = 0, arows = 1, bcols = 1, row_slots = 0;
+    int inst = -1, nw = 0, cn_lanes = 0, arows = 1, bcols = 1;
     uint32_t off_pad = 0, off_zero = 0, off_red = 0, off_alut = 0, off_blut = 0;
     int cn_dmin = 0;
     size_t lds = 0;
+    std::vector<int32_t> lay;      // [M][2] first slot of proto row i, stride A_i of its j-blocks
 };
 
-// Slot layout: proto row i owns slots i R .. i R + 4 EPL z - 1, slot (i, k, h) = i R + k z + h
-// (k >= the row degree: padding slots).  A check lane quad reads slots i R + (4 m + j) z + h
-// for 16 consecutive checks; with z < 64 a wave's checks cross proto rows, so R is padded to
-// z (mod 64): the 64 lanes then read 64 distinct slot residues mod 64, i.e. distinct LDS
-// banks (a slot's words are 5 s + p).
+// Slot layout: edge k of check (row i, index h) is slot first_i + (k mod LPC) A_i +
+// (k div LPC) z + h.  LDS banking (MI355X_MICROARCH.md, LDS): ds_read_b32 / ds_read2_b32 /
+// ds_write_b32 serve a wave in two 32-lane groups, bank = dword address mod 32; a slot's words
+// are 5 s + p, so a group is conflict-free when its 32 slot numbers are distinct mod 32.  The
+// 32 / LPC consecutive checks of a group read, for one m, slots first + j A + h: with
+// first_i = first_{i-1} + z (mod 32) the checks stay consecutive mod 32 across a row boundary,
+// and A_i is the smallest stride >= the j = 0 block whose multiples j A_i (j < LPC) are at
+// least 32 / LPC apart mod 32.
+static std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* nslot) {
+    std::vector<int32_t> lay((size_t)2 * h.M, 0);
+    const int sep = 32 / LPC;
+    auto ok = [&](int A) {
+        for (int d = 1; d < LPC; ++d) {
+            const int r = (d * A) % 32;
+            if (std::min(r, 32 - r) < sep) return false;
+        }
+        return true;
+    };
+    size_t cur = 0;
+    for (int i = 0; i < h.M; ++i) {
+        const int deg = h.row_ptr[i + 1] - h.row_ptr[i];
+        size_t first = cur;
+        if (i > 0) first += (size_t)((((int64_t)lay[2 * (i - 1)] + h.z - (int64_t)cur) % 32 + 32) % 32);
+        int A = ((deg + LPC - 1) / LPC) * h.z;
+        while (!ok(A)) ++A;
+        const int last_rows = (deg - (LPC - 1) + LPC - 1) / LPC;   // block j = LPC - 1
+        cur = first + (size_t)(LPC - 1) * A + (size_t)std::max(last_rows, 0) * h.z;
+        lay[2 * i] = (int32_t)first;
+        lay[2 * i + 1] = A;
+    }
+    *nslot = cur;
+    return lay;
+}
+
 BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
     BsPlan p;
     const char* e = getenv("LDPC_BS");
     if (e && atoi(e) == 0) return p;
+    const char* el = getenv("LDPC_BS_LPC");          // A/B: force 2 or 4 lanes per check
+    const int want_lpc = el ? atoi(el) : 0;
     if (mode != MODE_Q5 && mode != MODE_QM5) return p;           // qmax 15: 4 magnitude planes
     if (ucn || per_edge_w || !g.host || !g.w_beta_nonneg) return p;
     const host::GraphTables& h = *g.host;
@@ -659,37 +716,34 @@ BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
     for (int i = 0; i < h.M; ++i) min_cdeg = std::min(min_cdeg, h.row_ptr[i + 1] - h.row_ptr[i]);
     if (min_cdeg < 2) return p;                                   // ("no other edge" rule unneeded)
     for (int i = 0; i < (int)(sizeof(kInst) / sizeof(kInst[0])); ++i)
-        if (h.max_cdeg <= kInst[i].D && h.max_vdeg <= kInst[i].DV) { p.inst = i; break; }
+        if (h.max_cdeg <= kInst[i].D && h.max_vdeg <= kInst[i].DV &&
+            (want_lpc == 0 || want_lpc == kInst[i].LPC)) { p.inst = i; break; }
     if (p.inst < 0) return p;
-    const int EPL = (kInst[p.inst].D + 3) / 4;
+    const int LPC = kInst[p.inst].LPC;
     const int nv = g.n_vars, nc = g.n_checks;
-    p.cn_lanes = 64 * ((4 * nc + 63) / 64);                       // four lanes per check
+    p.cn_lanes = 64 * ((LPC * nc + 63) / 64);
     p.nw = std::max((nv + 63) / 64, p.cn_lanes / 64);
     if (p.nw > 16) return p;                                      // one variable per lane
     p.arows = g.w_alpha_uniform ? 1 : h.M;
     p.bcols = g.w_beta_uniform ? 1 : h.N;
-    // idle check lanes: every write is decided per lane
-    p.cn_dmin = (p.cn_lanes == 4 * nc) ? min_cdeg : 0;
-    for (int pad = 1; pad >= 0; --pad) {                          // padded rows if they fit
-        const int span = 4 * EPL * h.z;
-        p.row_slots = span + ((pad && h.z < 64) ? ((h.z - span) % 64 + 64) % 64 : 0);
-        const size_t nslot = (size_t)(h.M - 1) * p.row_slots + span;
-        p.off_pad = (uint32_t)(nslot * SLOT_B);
-        p.off_zero = p.off_pad + SLOT_B;
-        const size_t slot_end = (size_t)p.off_zero + SLOT_B;
-        if (slot_end > 65535) continue;                           // 16-bit slot addresses
-        size_t o = (slot_end + 15) & ~(size_t)15;
-        p.off_red = (uint32_t)o;
-        o += 64;
-        p.off_alut = (uint32_t)o;
-        o += (size_t)2 * p.arows * LUT_W * 4;
-        p.off_blut = (uint32_t)o;
-        o += (size_t)2 * p.bcols * LUT_W * 4;
-        p.lds = (o + 15) & ~(size_t)15;
-        if (p.lds > BS_LDS_MAX) continue;
-        p.ok = true;
-        break;
-    }
+    // idle check lanes: every slot is decided per lane
+    p.cn_dmin = (p.cn_lanes == LPC * nc) ? min_cdeg : 0;
+    size_t nslot = 0;
+    p.lay = slot_layout(h, LPC, &nslot);
+    p.off_pad = (uint32_t)(nslot * SLOT_B);
+    p.off_zero = p.off_pad + SLOT_B;
+    const size_t slot_end = (size_t)p.off_zero + SLOT_B;
+    if (slot_end > 65535) return p;                               // 16-bit slot addresses
+    size_t o = (slot_end + 15) & ~(size_t)15;
+    p.off_red = (uint32_t)o;
+    o += 64;
+    p.off_alut = (uint32_t)o;
+    o += (size_t)2 * p.arows * LUT_W * 4;
+    p.off_blut = (uint32_t)o;
+    o += (size_t)2 * p.bcols * LUT_W * 4;
+    p.lds = (o + 15) & ~(size_t)15;
+    if (p.lds > BS_LDS_MAX) return p;
+    p.ok = true;
     return p;
 }
 
@@ -704,8 +758,8 @@ bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
 const char* bs_kernel_name(const DevGraph& g) {
     static thread_local char buf[48];
     const BsPlan p = bs_plan(g, MODE_Q5, false, false);
-    snprintf(buf, sizeof(buf), "bsl[p32,w%d,d%d,v%d]", p.nw, p.inst >= 0 ? kInst[p.inst].D : 0,
-             p.inst >= 0 ? kInst[p.inst].DV : 0);
+    snprintf(buf, sizeof(buf), "bsl[p32,w%d,d%d,v%d,l%d]", p.nw, p.inst >= 0 ? kInst[p.inst].D : 0,
+             p.inst >= 0 ? kInst[p.inst].DV : 0, p.inst >= 0 ? kInst[p.inst].LPC : 0);
     return buf;
 }
 
@@ -721,7 +775,9 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
     std::vector<int32_t> wdeg(2 * p.nw, 0);
     auto put16 = [](uint32_t* w, int k, uint32_t addr) { w[k >> 1] |= addr << (16 * (k & 1)); };
     auto slot_addr = [&](int i, int k, int hc) {
-        return (uint32_t)(((size_t)i * p.row_slots + (size_t)k * z + hc) * SLOT_B);
+        const int LPC = kInst[p.inst].LPC;
+        return (uint32_t)(((size_t)p.lay[2 * i] + (size_t)(k % LPC) * p.lay[2 * i + 1] +
+                           (size_t)(k / LPC) * z + hc) * SLOT_B);
     };
     // variable lanes: variables by descending degree in chunks of 64; the chunks are dealt to
     // waves so that the SIMDs (wave w on SIMD w mod 4) get similar work (a chunk costs about
@@ -785,12 +841,13 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
         wdeg[2 * w] = dmax;
         wdeg[2 * w + 1] = dmin;
     }
-    const size_t bytes = (vn.size() + wdeg.size()) * 4;
+    const size_t bytes = (vn.size() + wdeg.size() + p.lay.size()) * 4;
     void* d = nullptr;
     if (hipMalloc(&d, bytes) != hipSuccess) { (void)hipGetLastError(); return LDPC_ERR_OOM; }
     uint32_t* dp = reinterpret_cast<uint32_t*>(d);
     if (hipMemcpyAsync(dp, vn.data(), vn.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(dp + vn.size(), wdeg.data(), wdeg.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(dp + vn.size() + wdeg.size(), p.lay.data(), p.lay.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
         (void)hipFree(d);
         return LDPC_ERR_HIP;
@@ -800,15 +857,15 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
     return LDPC_OK;
 }
 
-template <int D, int DV>
+template <int D, int DV, int LPC>
 static int launch_bs(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bs<D, DV>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bs<D, DV, LPC>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)BS_LDS_MAX);
         attr = true;
     }
-    hipLaunchKernelGGL((k_bs<D, DV>), dim3(nblocks), dim3(64 * nw), lds, s, a);
+    hipLaunchKernelGGL((k_bs<D, DV, LPC>), dim3(nblocks), dim3(64 * nw), lds, s, a);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 
@@ -855,9 +912,9 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.inv = 1.0f / step;
     a.row_ptr = g.row_ptr;
     a.z = g.z;
-    a.row_slots = p.row_slots;
     a.vn_tab = gt;
     a.vn_wdeg = reinterpret_cast<const int32_t*>(a.vn_tab + (size_t)64 * p.nw * VNW);
+    a.row_lay = a.vn_wdeg + 2 * p.nw;
     a.alut = alut;
     a.blut = blut;
     a.arows = p.arows;
@@ -872,8 +929,9 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.off_blut = p.off_blut;
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
     switch (p.inst) {
-        case 0: return launch_bs<15, 6>(a, nblocks, p.nw, p.lds, s);
-        default: return launch_bs<16, 8>(a, nblocks, p.nw, p.lds, s);
+        case 0: return launch_bs<15, 6, 4>(a, nblocks, p.nw, p.lds, s);
+        case 1: return launch_bs<16, 8, 4>(a, nblocks, p.nw, p.lds, s);
+        default: return launch_bs<15, 6, 2>(a, nblocks, p.nw, p.lds, s);
     }
 }
 

@@ -39,9 +39,17 @@ def _both(dec, llr):
     return out
 
 
+@pytest.fixture(params=["2", "4"], ids=["lpc2", "lpc4"])
+def lpc(request, monkeypatch):
+    """Both check-lane layouts (2 or 4 lanes per check, LDPC_BS_LPC)."""
+    monkeypatch.setenv("LDPC_BS_LPC", request.param)
+    return int(request.param)
+
+
 @pytest.mark.parametrize("B", [1, 31, 33, 3001, 40000])
-def test_bitsliced_equals_flood(cuda_device, B):
+def test_bitsliced_equals_flood(cuda_device, B, lpc):
     dec, cp = _wman(cuda_device)
+    assert dec.kernel_info()[1].endswith(f",l{lpc}]"), dec.kernel_info()
     assert dec.kernel_info()[1].startswith("bsl"), dec.kernel_info()
     llr = dec.awgn(B, float(cp.sigma(2.0)), seed=7, offset=123)
     out = _both(dec, llr)
@@ -50,7 +58,7 @@ def test_bitsliced_equals_flood(cuda_device, B):
 
 
 @pytest.mark.parametrize("q", [5, -5])
-def test_bitsliced_per_row_weights(cuda_device, q):
+def test_bitsliced_per_row_weights(cuda_device, q, lpc):
     dec, cp = _wman(cuda_device, sharing=(2, 0, 2), q=q, T=12)
     assert dec.kernel_info()[1].startswith("bsl")
     llr = dec.awgn(9000, float(cp.sigma(2.25)), seed=11)
@@ -60,7 +68,7 @@ def test_bitsliced_per_row_weights(cuda_device, q):
     assert 0 < out["fused"][0][1] < 9000
 
 
-def test_off_grid_packs_fall_back_exactly(cuda_device):
+def test_off_grid_packs_fall_back_exactly(cuda_device, lpc):
     import torch
     dec, cp = _wman(cuda_device)
     llr = dec.awgn(5000, float(cp.sigma(2.0)), seed=9)

@@ -12,8 +12,10 @@ pytestmark = pytest.mark.gpu
 B = 1 << 20
 
 
-@pytest.mark.parametrize("config", ["C2", "C5"])
-def test_full_batch_kernels_agree_and_match_oracle(cuda_device, config):
+@pytest.mark.parametrize("config,lpc", [("C2", "2"), ("C2", "4"), ("C5", "")])
+def test_full_batch_kernels_agree_and_match_oracle(cuda_device, config, lpc, monkeypatch):
+    if lpc:
+        monkeypatch.setenv("LDPC_BS_LPC", lpc)
     import torch
     import bench
     from ldpc_error_floor_amd.decoder import NMSDecoder
@@ -25,7 +27,8 @@ def test_full_batch_kernels_agree_and_match_oracle(cuda_device, config):
     snr = {"C2": 2.5, "C5": 2.5}[config]
     sigma = float(cp.sigma(snr))
     dec = NMSDecoder(proto, z, W, 2, 5, device=cuda_device, B_max=B)
-    assert dec.kernel_info(T)[1].startswith("fused5")
+    # counters-only decodes: the bit-sliced kernel where it applies (C2), else fused v5
+    assert dec.kernel_info(T)[1].startswith(("bsl[", "fused5[")), dec.kernel_info(T)
     llr = dec.awgn(B, sigma, seed=31, punct=punct, short=short)
     res = {}
     for k in ("fused", "flood"):

@@ -133,6 +133,7 @@ def test_fused5_every_shape_bit_exact(shape, cuda_device, monkeypatch):
     import torch
     from ldpc_error_floor_amd.decoder import NMSDecoder
     monkeypatch.setenv("LDPC_F5_SHAPE", str(shape))
+    monkeypatch.setenv("LDPC_BS", "0")      # kernel_info names the v5 shape, not the bit-sliced kernel
     ran = []
     for name in DECODER_CASES:
         c = load_case(name)
@@ -162,6 +163,7 @@ def test_fused5_group_dealing_bit_exact(balance, merge, cuda_device, monkeypatch
     from ldpc_error_floor_amd.decoder import NMSDecoder
     monkeypatch.setenv("LDPC_F5_BALANCE", balance)
     monkeypatch.setenv("LDPC_F5_MERGE", merge)
+    monkeypatch.setenv("LDPC_BS", "0")
     ran = 0
     for name in DECODER_CASES:
         c = load_case(name)
