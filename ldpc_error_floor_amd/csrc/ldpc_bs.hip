@@ -206,6 +206,25 @@ __device__ __forceinline__ void lut(uint32_t (&o)[NI][4], const uint32_t (&in)[N
     }
 }
 
+// the same 16-entry table when it is one table for the whole workgroup (uniform weights): its
+// 64 leaf words come by scalar loads (constant address space) into SGPRs, so the evaluation
+// costs no LDS traffic; a leaf is a v_and + v_xor with SGPR operands (the 2-cycle VOP2 forms,
+// one SGPR per instruction) in place of one v_bitop3 — the same issue cycles
+typedef __attribute__((address_space(4))) const uint32_t ConstW;
+__device__ __forceinline__ void lut_s(uint32_t (&o)[4], const uint32_t (&a)[4], const ConstW* tab) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t g[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t l0 = (a[0] & tab[j * 16 + 4 * q]) ^ tab[j * 16 + 4 * q + 1];
+            const uint32_t l1 = (a[0] & tab[j * 16 + 4 * q + 2]) ^ tab[j * 16 + 4 * q + 3];
+            g[q] = mux(a[1], l1, l0);
+        }
+        o[j] = mux(a[3], mux(a[2], g[3], g[2]), mux(a[2], g[1], g[0]));
+    }
+}
+
 // bit j of the table output for NI inputs (4 b128 loads of the table's bit-j leaves at tab_j)
 template <int NI>
 __device__ __forceinline__ void lut_bit(uint32_t (&o)[NI], const uint32_t (&in)[NI][4], uint32_t tab_j) {
@@ -372,7 +391,7 @@ k_bs(BsArgs a) {
     //   first: lw_0 as every edge's V->C (no C->V yet);
     //   else:  S = sum of the C->V, APP_t = Q(ch) + S (hard decision, counters); unless last,
     //          Tv = clamp(Q(beta_{t+1} ch) + S) and V->C_e = clamp(Tv - C->V_e, +-15) per edge
-    auto vn_phase = [&](const bool first, const bool last, const uint32_t btab)
+    auto vn_phase = [&](const bool first, const bool last, const uint32_t btab, const int tb)
                         __attribute__((always_inline)) {
 #pragma unroll
         for (int p = 0; p < VNW - 1; ++p) asm volatile("" : "+v"(va[p]));   // unpacked per use
@@ -381,8 +400,12 @@ k_bs(BsArgs a) {
         };
         uint32_t lw[1][4];                   // |Q(beta_{t+1} ch)| (before the C->V: fewer live registers)
         if (!last) {
-            const uint32_t cmi[1][4] = {{cm[0], cm[1], cm[2], cm[3]}};
-            lut<1>(lw, cmi, btab);
+            if (a.bcols == 1) {          // one beta per iteration: table in SGPRs
+                lut_s(lw[0], cm, (const ConstW*)(a.blut) + (size_t)tb * LUT_W);
+            } else {
+                const uint32_t cmi[1][4] = {{cm[0], cm[1], cm[2], cm[3]}};
+                lut<1>(lw, cmi, btab);
+            }
         }
         // C->V of the first KEEP edges stay in registers for the V->C pass, the others are read
         // again (the register budget of three 9-wave workgroups per CU)
@@ -484,7 +507,7 @@ k_bs(BsArgs a) {
         }
     };
 
-    vn_phase(true, false, a.off_blut + tab_b);
+    vn_phase(true, false, a.off_blut + tab_b, 0);
     // check lanes: lane LPC c + j (check c = row i, index h) takes edges k = LPC m + j, at slots
     // first_i + j A_i + m z + h (a.row_lay); edges past the degree read the all-ones PAD slot
     // and are not written; idle lanes (c >= n_checks) read PAD only
@@ -508,7 +531,8 @@ k_bs(BsArgs a) {
         // next iteration's tables (their slots were last read two phases ago)
         if (t + 1 < a.T) {
             for (int w = tid; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
-            for (int w = tid; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
+            if (a.bcols > 1)
+                for (int w = tid; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
         }
         // ======== check nodes ===================================================================
         if (is_cn) {
@@ -590,8 +614,8 @@ k_bs(BsArgs a) {
         __syncthreads();
         // ======== variable nodes ================================================================
         const uint32_t btab = a.off_blut + (uint32_t)(nx * BL * 4) + tab_b;
-        if (t == a.T - 1) vn_phase(false, true, btab);
-        else vn_phase(false, false, btab);
+        if (t == a.T - 1) vn_phase(false, true, btab, t + 1);
+        else vn_phase(false, false, btab, t + 1);
         __syncthreads();
     }
     if (tid == 0) {
