@@ -70,8 +70,12 @@ int64_t fused_bytes_per_cw(const DevGraph& g, int T) {
 int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
                  bool ucn, bool want_bits, int ntiles_max, int T_max, int per_edge_w,
                  int64_t* counters, uint8_t* flags, hipStream_t s) {
-    (void)ucn;
     if (!fused_supported(g, mode, b.T, b.clip)) return LDPC_ERR_UNSUPPORTED;
+    // counters-only decodes the bit-sliced kernel serves read their LLRs: with an in-kernel
+    // channel requested, the caller (ldpc_decode_awgn) generates them into HBM first — the
+    // channel kernel plus the bit-sliced decode beat the v5 kernel's in-prologue channel
+    if (b.awgn && !want_bits && !b.app_out && use_bs(g, mode, b.T, ucn, per_edge_w != 0))
+        return LDPC_ERR_UNSUPPORTED;
     const float step = mode_step(mode);
     const int cu = clip_units(mode, b.clip);
     uint64_t* hd_out = nullptr;
