@@ -308,10 +308,13 @@ def main():
                     "effective_frac": round(effective / HBM_PEAK_GBS, 4),
                     "valu_insts_per_launch": vi,
                     "valu_busy": vb or None,
+                    "lds_busy": prof.get("lds_busy") if prof else None,
                     "wait_any_frac": prof.get("wait_any_frac") if prof else None,
                     "profile": prof.get("source") if prof else None}
         roofline["note"] = ("fused: all T iterations per codeword block in LDS/VGPRs; the only "
-                            "HBM traffic is the LLR read, so the VALU pipe binds. frac = VALU "
+                            "HBM traffic is the LLR read, so the VALU pipe binds (the bit-sliced "
+                            "bsl kernel: VALU issue and the LDS array together, lds_busy = "
+                            "SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM cycles / 8)). frac = VALU "
                             "busy: quad-cycles with a VALU issue (SQ_INSTS_VALU - "
                             "SQ_ACTIVE_INST_VALU2) / (1024 SIMDs x GRBM_GUI_ACTIVE/8/4), PMC of "
                             "this build (profile above). issue_frac = achieved / peak with "

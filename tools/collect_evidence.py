@@ -26,6 +26,7 @@ def main():
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(dst, "bench_c2_rocprof_kernel_stats.csv"))
     for tj in glob.glob(os.path.join(src, "traffic_fused5_*.json")) + \
+            glob.glob(os.path.join(src, "traffic_bsl_*.json")) + \
             glob.glob(os.path.join(src, "traffic_flood*.json")):
         d = json.load(open(tj))
         old = d.get("source", "")

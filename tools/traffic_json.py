@@ -71,6 +71,19 @@ def valu_busy(pm, avg_ns):
             "clock_ghz": round(pm["GRBM_GUI_ACTIVE"] / 8.0 / avg_ns, 3)}
 
 
+def lds_busy(pm):
+    """Fraction of the CUs' LDS-array cycles in use: SQ_LDS_IDX_ACTIVE (LDS-array cycles summed
+    over the 256 CUs, bank-conflict cycles included: SQ_LDS_BANK_CONFLICT) over 256 x
+    (GRBM_GUI_ACTIVE / 8 XCDs) (MI355X_MICROARCH.md, LDS)."""
+    if "SQ_LDS_IDX_ACTIVE" not in pm or "GRBM_COUNT" not in pm:
+        return None
+    avail = 256 * pm["GRBM_COUNT"] / 8.0
+    out = {"frac": round(pm["SQ_LDS_IDX_ACTIVE"] / avail, 4)}
+    if "SQ_LDS_BANK_CONFLICT" in pm:
+        out["conflict_frac"] = round(pm["SQ_LDS_BANK_CONFLICT"] / pm["SQ_LDS_IDX_ACTIVE"], 4)
+    return out
+
+
 def display_name(prof):
     with open(os.path.join(prof, "trace.log")) as fh:
         for line in fh:
@@ -117,6 +130,7 @@ def main():
           "wait_any_frac": (round(pm["SQ_WAIT_ANY"] / pm["SQ_WAVE_CYCLES"], 4)
                             if "SQ_WAIT_ANY" in pm and pm.get("SQ_WAVE_CYCLES") else None),
           "valu_busy": valu_busy(pm, avg_ns),
+          "lds_busy": lds_busy(pm),
           "method": "2 x FETCH_SIZE + WRITE_SIZE (KiB), separate --pmc passes, gfx950 "
                     "FETCH_SIZE half-count correction (MI355X_MICROARCH.md, HBM)"}
     path = os.path.join(ROOT, "profiles", f"traffic_{sn}.json")
