@@ -546,19 +546,23 @@ k_bs(BsArgs a) {
             };
             // pass 1: two minima of |V->C| and the parity of [V->C >= 0] over the lane's edges
             // (padding edges: negative, magnitude 15), then merged across the lane group
-            uint32_t m1[4], m2[4] = {~0u, ~0u, ~0u, ~0u}, par;
-            read_slot(par, m1, caddr(0));
+            // (the lane's EPL slots are read once, all loads issued before any use, and kept
+            // in registers for pass 2)
+            uint32_t Xs[EPL][4], ns[EPL];
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) read_slot(ns[m], Xs[m], caddr(m));
+            uint32_t m1[4] = {Xs[0][0], Xs[0][1], Xs[0][2], Xs[0][3]}, m2[4] = {~0u, ~0u, ~0u, ~0u};
+            uint32_t par = ns[0];
 #pragma unroll
             for (int m = 1; m < EPL; ++m) {
-                uint32_t X[4], n;
-                read_slot(n, X, caddr(m));
+                const uint32_t(&X)[4] = Xs[m];
                 const uint32_t l1 = lt4(X, m1), l2 = lt4(X, m2);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     m2[i] = mux(l1, m1[i], mux(l2, X[i], m2[i]));
                     m1[i] = mux(l1, X[i], m1[i]);
                 }
-                par ^= n;
+                par ^= ns[m];
             }
             par ^= qperm<QP_X1>(par);
             merge_lanes<QP_X1>(m1, m2);
@@ -600,8 +604,9 @@ k_bs(BsArgs a) {
             for (int m = 0; m < EPL; ++m) {
                 if (real(m)) {
                     const uint32_t addr = cbase + m * cstride;
-                    uint32_t X[4], n, Mg[4];
-                    read_slot(n, X, addr);
+                    const uint32_t(&X)[4] = Xs[m];
+                    const uint32_t n = ns[m];
+                    uint32_t Mg[4];
                     uint32_t ne = X[0] ^ m1[0];
 #pragma unroll
                     for (int i = 1; i < 4; ++i) ne = B3(T_ORXOR, ne, X[i], m1[i]);
