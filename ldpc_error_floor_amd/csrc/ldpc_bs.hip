@@ -58,6 +58,10 @@ struct BsArgs {
     uint8_t* flags;
     uint32_t* bad;               // [packs] 1: decoded by the v5 fixup instead
     uint32_t off_pad, off_zero, off_red, off_alut, off_blut;   // LDS byte offsets
+    int ablate;   // timing diagnostics, builds with -DBS_DIAG only (LDPC_DIAG_ABLATE, wrong
+                  // results): 1 no check phase, 2 no beta table, 4 no V->C pass, 8 no frame
+                  // flags, 16 no iterations, 32 no LLR loads.  (Compiled in, the uniform
+                  // tests alone cost 4 %.)
 };
 
 // ---- bit-plane arithmetic ---------------------------------------------------------------------
@@ -303,6 +307,11 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
 // 8 waves per SIMD (64 VGPRs): three 9-wave workgroups per CU.  At a 72-register budget only
 // two were resident (the waves of a workgroup are not spread evenly over the SIMDs): measured
 // 7.56 ms (72 VGPRs) -> 6.51 ms (64) per 2^20-codeword C2 decode (tools/bs_variant.sh A/B).
+#ifdef BS_DIAG
+#define ABL(bit) (a.ablate & (bit))
+#else
+#define ABL(bit) 0
+#endif
 #ifndef BS_WPE
 #define BS_WPE 8
 #endif
@@ -354,12 +363,19 @@ k_bs(BsArgs a) {
     __syncthreads();
     uint32_t cs = 0u, cm[4] = {0u, 0u, 0u, 0u};
     int off = 0;
-    if (v >= 0) {
+    if (v >= 0 && !ABL(32)) {
         const float* src = a.llr + b0 * nv + v;
-#pragma unroll 8
+        // all 32 loads issued before any use: one HBM round trip per workgroup prologue (with
+        // batches of 8 the LLR fetch cost 0.75 ms of a 6.5 ms C2 decode, with this 0.44 ms:
+        // the workgroups stay in step, so every pack boundary is a chip-wide HBM burst; a
+        // persistent grid prefetching the next pack during the check phases needed 6 more
+        // loop-carried registers and spilled: 7.56 ms)
+        float xv[PACK];
+#pragma unroll
+        for (int r = 0; r < PACK; ++r) xv[r] = src[(int64_t)min(r, nvalid - 1) * nv];
+#pragma unroll
         for (int r = 0; r < PACK; ++r) {
-            const int rr = min(r, nvalid - 1);
-            const float x = src[(int64_t)rr * nv] * a.inv;
+            const float x = xv[r] * a.inv;
             const float xr = rintf(x);
             off |= (xr != x || fabsf(xr) > (float)QMAX) ? 1 : 0;
             const int xi = (r < nvalid) ? (int)xr : 0;
@@ -400,7 +416,10 @@ k_bs(BsArgs a) {
         };
         uint32_t lw[1][4];                   // |Q(beta_{t+1} ch)| (before the C->V: fewer live registers)
         if (!last) {
-            if (a.bcols == 1) {          // one beta per iteration: table in SGPRs
+            if (ABL(2)) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) lw[0][i] = cm[i];
+            } else if (a.bcols == 1) {          // one beta per iteration: table in SGPRs
                 lut_s(lw[0], cm, (const ConstW*)(a.blut) + (size_t)tb * LUT_W);
             } else {
                 const uint32_t cmi[1][4] = {{cm[0], cm[1], cm[2], cm[3]}};
@@ -450,12 +469,13 @@ k_bs(BsArgs a) {
                 hd = B3(T_XNOR3, S[SB - 1], cs, c);
             }
             hd &= valid;                                     // APP >= 0 -> hard decision 1
+            if (ABL(8)) hd = 0u;
             uint32_t wr = counted ? hd : 0u, apos = 0u, nb = 0u;
             if (last && counted) {
                 apos = hd & nz;
                 nb = (uint32_t)__popc(hd);
             }
-            wr = wave_or(wr);
+            if (!ABL(8)) wr = wave_or(wr);
             if (last) {
                 apos = wave_or(apos);
                 nb = wave_add(nb);
@@ -488,6 +508,7 @@ k_bs(BsArgs a) {
 #pragma unroll
             for (int f = 0; f < DV; ++f) {
                 if (f < dw) {
+                    if (ABL(4)) continue;
                     uint32_t x[7], X[4], n, b[4];
                     if (f < KEEP) {
                         n = mn[f < KEEP ? f : 0];
@@ -521,7 +542,7 @@ k_bs(BsArgs a) {
     const uint32_t tab_a = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * OB * 64);
     __syncthreads();
 
-    for (int t = 0; t < a.T; ++t) {
+    for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
         if (tid == 0 && t > 0) {            // fold iteration t-1's frame flags
             RED[1] &= RED[0];
             RED[0] = 0u;
@@ -535,7 +556,7 @@ k_bs(BsArgs a) {
                 for (int w = tid; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
         }
         // ======== check nodes ===================================================================
-        if (is_cn) {
+        if (is_cn && !ABL(1)) {
             asm volatile("" : "+v"(cbase));
             // slot m of the lane: always a real edge while LPC m + LPC - 1 < cn_dmin
             auto real = [&](int m) __attribute__((always_inline)) -> bool {
@@ -956,6 +977,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.off_red = p.off_red;
     a.off_alut = p.off_alut;
     a.off_blut = p.off_blut;
+    if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // -DBS_DIAG builds
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
     switch (p.inst) {
         case 0: return launch_bs<15, 6, 4>(a, nblocks, p.nw, p.lds, s);

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build a libldpc_nms.so variant of the bit-sliced kernel (ldpc_bs.hip) for A/B runs, without
 # touching the tree:   [BS_SRC=other/ldpc_bs.hip] bash tools/bs_variant.sh ab_libs/NAME.so [hipcc flags]
+# (-DBS_DIAG compiles in the LDPC_DIAG_ABLATE phase switches, for timing ablations)
 # Recompiles ldpc_bs.hip with the flags and links it with the in-tree objects of the other
 # sources (build those first: python -m ldpc_error_floor_amd.build).  Compare with tools/ab_lib.sh.
 set -euo pipefail
