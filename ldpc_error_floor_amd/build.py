@@ -25,19 +25,30 @@ ARCH = os.environ.get("LDPC_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["ldpc_capi.hip", "ldpc_flood.hip", "ldpc_fused.hip", "ldpc_fused5.hip",
                "ldpc_bs.hip", "ldpc_channel.hip", "ldpc_collect.hip"]
-HEADERS = ["ldpc_internal.h", "ldpc_fused.h", "ldpc_fused5_kernel.h", "ldpc_awgn.h", "ldpc_host.h"]
+HEADERS = ["ldpc_internal.h", "ldpc_fused.h", "ldpc_fused5_kernel.h", "ldpc_bs_kernel.h", "ldpc_awgn.h",
+           "ldpc_host.h"]
 # host-only C++ (no HIP): also built with g++ -fsanitize=address,undefined by
 # tests/test_host_sanitized.py
 HOST_SOURCES = ["ldpc_host.cpp"]
 # ldpc_fused5_shape.hip is compiled once per kShapes5 entry (-DF5_SHAPE=i), in parallel
 F5_SHAPE_SRC = "ldpc_fused5_shape.hip"
+# ldpc_bs_inst.hip is compiled once per kBsInst entry (-DBS_INST=i), in parallel
+BS_INST_SRC = "ldpc_bs_inst.hip"
+
+
+def _table_count(header, decl):
+    import re
+    src = open(os.path.join(CSRC, header)).read()
+    body = src.split(decl, 1)[1].split("\n};", 1)[0]
+    return len(re.findall(r"^\s*\{", body, re.M))
 
 
 def _f5_shape_count():
-    import re
-    src = open(os.path.join(CSRC, "ldpc_fused5_kernel.h")).read()
-    body = src.split("constexpr Shape5 kShapes5[] = {", 1)[1].split("\n};", 1)[0]
-    return len(re.findall(r"^\s*\{", body, re.M))
+    return _table_count("ldpc_fused5_kernel.h", "constexpr Shape5 kShapes5[] = {")
+
+
+def _bs_inst_count():
+    return _table_count("ldpc_bs_kernel.h", "constexpr BsInst kBsInst[] = {")
 LIB = os.path.join(PKG, "libldpc_nms.so")
 EXT = os.path.join(PKG, "_ldpc_nms" + sysconfig.get_config_var("EXT_SUFFIX"))
 
@@ -77,6 +88,7 @@ def build(force=False, jobs=4, verbose=False):
     units += [(src, src.replace(".cpp", ".o"), []) for src in HOST_SOURCES]
     units += [(F5_SHAPE_SRC, f"ldpc_fused5_s{i}.o", [f"-DF5_SHAPE={i}"])
               for i in range(_f5_shape_count())]
+    units += [(BS_INST_SRC, f"ldpc_bs_i{i}.o", [f"-DBS_INST={i}"]) for i in range(_bs_inst_count())]
     for src, obj, defs in units:
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, obj)

@@ -1,0 +1,800 @@
+// ldpc_bs_kernel.h — bit-sliced fused QMS decoder ("bsl"): 32 codewords per 32-bit word.
+//
+// Same semantics as the v5 kernel (ldpc_fused5_kernel.h) and the reference graph
+// (Main_Functions.py:157-335): all T flooding iterations of a block in one launch, integer
+// arithmetic in units of the q-bit grid (q = 5 / -5: qmax = 15).  What changes is the data
+// layout: a workgroup decodes one PACK of 32 codewords and every quantity is held as bit
+// planes (plane word p of a value holds bit p of that value for the 32 codewords, bit r =
+// codeword b0 + r).  The min-sum arithmetic — V->C subtraction, |.| with saturation, the
+// two-minimum search, the sign parity, the weighted quantization (a 16-entry table per
+// iteration, evaluated as a mux tree) and the variable-node sums — is boolean algebra on whole
+// words, which gfx950 issues as v_bitop3_b32 (any function of three words in one VALU op).
+// One lane does the work of 32 codeword-lanes of v5.
+//
+// LDS holds one 5-word SLOT per lifted edge:
+//   between the variable and the check phase: V->C = clamp(Tv - C->V, +-15), as a negative flag
+//     and 4 magnitude planes (the nudged zero is positive, Main_Functions.py:229-230);
+//   between the check and the variable phase: C->V, as a negative flag and 4 magnitude planes.
+// Each slot is read and then rewritten by exactly one lane per phase, so the two share it.
+// Check phase: LPC lanes per check (padding edges read the all-ones PAD slot: negative,
+// magnitude 15, so they change neither minimum nor parity).  Variable phase: one lane per
+// variable (variables ordered by degree so a wave's loop bound is tight; padding edges read the
+// all-zero ZERO slot); the channel stays in the lane's registers for the whole decode.
+//
+// Instances (kBsInst): the small graphs (wman, all variables and check lanes of a pack in one
+// <= 16-wave workgroup, 16-bit packed slot addresses, 64 VGPRs: three workgroups per CU) and
+// the large ones (5G BG2: VPL variables and CPL check groups per lane, 32-bit addresses, one
+// 16-wave workgroup per CU), with or without UCN (Main_Functions.py:180-209: the syndrome of the
+// previous hard decisions selects alpha' on unsatisfied checks) and shortened bits (LLR = the
+// clip value, off the quantizer grid: Q(ch) = +-15, |Q(beta ch)| from a per-column table).
+// Packs with any other LLR off the quantizer grid are flagged in `bad` and decoded by the v5
+// kernel instead, so the result is exact for any input.
+#pragma once
+#include <cstdint>
+
+#include "ldpc_fused.h"
+#include "ldpc_fused5_kernel.h"
+
+namespace ldpc {
+namespace bs {
+
+constexpr int PACK = 32;                 // codewords per workgroup
+constexpr int SLOT_W = 5;                // words per edge slot: negative flag, magnitude 0..3
+constexpr int SLOT_B = SLOT_W * 4;
+constexpr int LUT_W = 64;                // words per 16-entry table: [bit j][pair p] {X, Y}
+constexpr int BLUT_W = LUT_W + 4;        // beta tables: + |Q(beta clip)| planes (shortened bits)
+constexpr int QMAX = 15;
+constexpr size_t BS_LDS_MAX = 160 * 1024;
+
+// kernel instances: D = check-degree bound, DV = variable-degree bound, LPC = lanes per check,
+// VPL / CPL = variables / 64-lane check chunks per lane, UCN / BIG = unsatisfied-check weights /
+// shortened bits supported, PK = 16-bit packed slot addresses, WPE = waves per SIMD (registers)
+struct BsInst { int D, DV, LPC, VPL, CPL; bool UCN, BIG, PK; int WPE; };
+constexpr BsInst kBsInst[] = {
+    {15, 6, 4, 1, 1, false, false, true, 8},     // wman (C2), LPC 4 measured 6.31 ms vs 6.73
+    {16, 8, 4, 1, 1, false, false, true, 8},
+    {15, 6, 2, 1, 1, false, false, true, 8},     // LDPC_BS_LPC=2 A/B
+    {24, 4, 4, 1, 1, true, true, true, 6},       // 802.11n (C3): degree 22, UCN
+    {10, 8, 4, 2, 3, true, true, false, 4},      // 5G BG2 (C4): 1,280 variables, 640 checks
+    {10, 8, 2, 2, 2, true, true, false, 4},      // LDPC_BS_LPC=2 A/B
+};
+constexpr int kBsNInst = sizeof(kBsInst) / sizeof(kBsInst[0]);
+
+struct BsArgs {
+    const float* llr;
+    int64_t B;
+    int n_vars, n_checks, T, target_bits, cn_lanes, cn_dmin;
+    float inv;
+    float cu;                    // |LLR| / step of a shortened bit (BIG instances), > QMAX
+    int ucn;                     // UCN weights present (UCN instances)
+    const int32_t* row_ptr;      // [M + 1] proto edges of each row (the check degrees)
+    const int32_t* row_lay;      // [M][2] slot layout of each proto row: first slot, j-block stride
+    int z;
+    const uint32_t* vn_tab;      // [VPL][64 nw][VNW]: slot byte addresses (2 per word if PK), variable (-1 idle)
+    const int32_t* vn_wdeg;      // [VPL][nw][2] most and fewest edges of a variable of each wave
+    const int32_t* cn_chunk;     // [nw][CPL] 64-lane check chunk of each wave's group (-1 idle)
+    const uint32_t* cn_hd;       // [chunks * 64][HDW] UCN: LDS byte addresses of the edges' hard decisions
+    const uint32_t* alut;        // [T][AR][LUT_W]: Q(relu(alpha m step)) for m = 0..15 (AR = arows, x2 with UCN)
+    const uint32_t* blut;        // [T][bcols][BLUT_W]: |Q(beta m)| for m = 0..15 (grid units), |Q(beta cu)|
+    int arows, bcols;
+    int64_t* counters;
+    uint8_t* flags;
+    uint32_t* bad;               // [packs] 1: decoded by the v5 fixup instead
+    uint32_t off_slots, off_pad, off_zero, off_red, off_alut, off_blut, off_hdz;   // LDS byte offsets
+    int ablate;   // timing diagnostics, builds with -DBS_DIAG only (LDPC_DIAG_ABLATE, wrong
+                  // results): 1 no check phase, 2 no beta table, 4 no V->C pass, 8 no frame
+                  // flags, 16 no iterations, 32 no LLR loads.  (Compiled in, the uniform
+                  // tests alone cost 4 %.)
+};
+
+// ---- bit-plane arithmetic ---------------------------------------------------------------------
+// Every 3-input function is one v_bitop3_b32 with an explicit truth table (the compiler's own
+// boolean synthesis often emits two or three ops for one such function); 2-input functions are
+// left to the compiler, which emits the 2-cycle VOP2 forms (v_and / v_or / v_xor / v_xnor).
+// Truth table of f: f(0xF0, 0xCC, 0xAA) for operands (a, b, c).
+#define B3(F, a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), (F))
+constexpr unsigned TA = 0xF0, TB = 0xCC, TC = 0xAA;
+constexpr unsigned T_XOR3 = (TA ^ TB ^ TC) & 0xFF;                       // a ^ b ^ c
+constexpr unsigned T_XNOR3 = ~(TA ^ TB ^ TC) & 0xFF;                     // ~(a ^ b ^ c)
+constexpr unsigned T_MAJ = ((TA & TB) | (TA & TC) | (TB & TC)) & 0xFF;   // maj(a, b, c)
+constexpr unsigned T_MAJNB = ((TA & ~TB) | (TA & TC) | (~TB & TC)) & 0xFF;   // maj(a, ~b, c)
+constexpr unsigned T_MUX = ((TA & TB) | (~TA & TC)) & 0xFF;              // a ? b : c
+constexpr unsigned T_LT = ((~TA & TB) | (~(TA ^ TB) & TC)) & 0xFF;       // a < b at this bit, else c
+constexpr unsigned T_ANDN = (~TA & TB) & 0xFF;                           // ~a & b
+constexpr unsigned T_LEAF = ((TA & TB) ^ TC) & 0xFF;                     // (a & b) ^ c
+constexpr unsigned T_AND3 = (TA & TB & TC) & 0xFF;                       // a & b & c
+constexpr unsigned T_SAT = ((TA & ~TB) | (~TA & TC)) & 0xFF;             // a ? ~b : c
+constexpr unsigned T_XAND = (TA ^ (TB & TC)) & 0xFF;                     // a ^ (b & c)
+constexpr unsigned T_ORXOR = (TA | (TB ^ TC)) & 0xFF;                    // a | (b ^ c)
+__device__ __forceinline__ uint32_t mux(uint32_t s, uint32_t a, uint32_t b) { return B3(T_MUX, s, a, b); }
+
+// S += m for m = (negative flag n, b) with b_i = M_i ^ n (M the 4 magnitude planes): the
+// two's complement of m is b sign-extended with n, plus n
+template <int SB>
+__device__ __forceinline__ void add_b(uint32_t (&S)[SB], const uint32_t (&b)[4], uint32_t n) {
+    uint32_t c = n;
+#pragma unroll
+    for (int i = 0; i < SB; ++i) {
+        const uint32_t bi = (i < 4) ? b[i] : n;
+        const uint32_t s = B3(T_XOR3, S[i], bi, c);
+        if (i + 1 < SB) c = B3(T_MAJ, S[i], bi, c);
+        S[i] = s;
+    }
+}
+// S = m (same operand form), S previously zero
+template <int SB>
+__device__ __forceinline__ void set_b(uint32_t (&S)[SB], const uint32_t (&b)[4], uint32_t n) {
+    uint32_t c = n;
+#pragma unroll
+    for (int i = 0; i < SB; ++i) {
+        const uint32_t bi = (i < 4) ? b[i] : n;
+        S[i] = bi ^ c;
+        c = bi & c;
+    }
+}
+
+// x = Tv - m (7 planes, two's complement; Tv in [-32, 31], |m| <= 15) with m = (n, b) as above:
+// -m is ~b sign-extended with ~n, plus ~n
+__device__ __forceinline__ void sub_tv(uint32_t (&x)[7], const uint32_t (&T)[6], const uint32_t (&b)[4],
+                                       uint32_t n) {
+    uint32_t c = ~n;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        const uint32_t t = T[i < 6 ? i : 5];
+        const uint32_t bi = (i < 4) ? b[i] : n;
+        x[i] = B3(T_XNOR3, t, bi, c);
+        if (i < 6) c = B3(T_MAJNB, t, bi, c);
+    }
+}
+
+// min(|x|, 15) (4 planes) of a 7-plane two's complement x in [-64, 63]; the sign is x[6].
+// For x < 0 the low bits of -x are x_i ^ OR(x_j, j < i); |x| >= 16 is x5 | x4 for x >= 0 and
+// "not (x5 & x4 & low 4 bits nonzero)" for x < 0.
+__device__ __forceinline__ void abs_sat(uint32_t (&X)[4], const uint32_t (&x)[7]) {
+    const uint32_t neg = x[6];
+    const uint32_t o2 = x[0] | x[1], o3 = o2 | x[2], o4 = o3 | x[3];
+    const uint32_t sat = B3(T_SAT, neg, B3(T_AND3, x[5], x[4], o4), x[5] | x[4]);
+    X[0] = x[0] | sat;
+    X[1] = B3(T_XAND, x[1], neg, x[0]) | sat;
+    X[2] = B3(T_XAND, x[2], neg, o2) | sat;
+    X[3] = B3(T_XAND, x[3], neg, o3) | sat;
+}
+
+// a < b for 4-plane unsigned values
+__device__ __forceinline__ uint32_t lt4(const uint32_t (&a)[4], const uint32_t (&b)[4]) {
+    uint32_t l = B3(T_ANDN, a[0], b[0], 0u);
+#pragma unroll
+    for (int i = 1; i < 4; ++i) l = B3(T_LT, a[i], b[i], l);
+    return l;
+}
+
+// SB-plane two's complement -> 6 planes, saturated to [-32, 31]
+template <int SB>
+__device__ __forceinline__ void clamp6(uint32_t (&T)[6], const uint32_t (&v)[SB]) {
+    uint32_t ovf = 0;
+#pragma unroll
+    for (int i = 5; i < SB - 1; ++i) ovf |= v[i] ^ v[i + 1];
+    const uint32_t s = v[SB - 1];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) T[i] = B3(T_SAT, ovf, s, v[i]);
+    T[5] = mux(ovf, s, v[5]);
+}
+
+// LDS accesses by byte address (all slots and tables are LDS-absolute: the kernel's dynamic
+// LDS starts at 0, checked at entry)
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) uint32_t LdsW;
+typedef __attribute__((address_space(3))) v4u LdsQ;
+
+__device__ __forceinline__ uint32_t lds_w(uint32_t addr) { return *reinterpret_cast<const LdsW*>(addr); }
+__device__ __forceinline__ v4u lds_q(uint32_t addr) { return *reinterpret_cast<const LdsQ*>(addr); }
+__device__ __forceinline__ void lds_put(uint32_t addr, uint32_t x) { *reinterpret_cast<LdsW*>(addr) = x; }
+
+__device__ __forceinline__ void read_slot(uint32_t& n, uint32_t (&M)[4], uint32_t addr) {
+    const LdsW* p = reinterpret_cast<const LdsW*>(addr);
+    n = p[0];
+    M[0] = p[1];
+    M[1] = p[2];
+    M[2] = p[3];
+    M[3] = p[4];
+}
+__device__ __forceinline__ void write_slot(uint32_t addr, uint32_t n, const uint32_t (&M)[4]) {
+    LdsW* p = reinterpret_cast<LdsW*>(addr);
+    p[0] = n;
+    p[1] = M[0];
+    p[2] = M[1];
+    p[3] = M[2];
+    p[4] = M[3];
+}
+
+// 16-entry table g(m) (4 -> 4 bits) at LDS byte address `tab`: level 1 of the mux tree is
+// (m0 & X) ^ Y per pair of entries, levels 2-4 select by m1, m2, m3
+template <int NI>
+__device__ __forceinline__ void lut(uint32_t (&o)[NI][4], const uint32_t (&in)[NI][4], uint32_t tab) {
+    uint32_t tj = tab;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        // one output bit at a time (the next bit's table loads wait for this bit's result), so
+        // that the scheduler cannot hoist all 16 table loads into 64 registers
+        if (j > 0) asm volatile("" : "+v"(tj) : "v"(o[0][j - 1]));
+        uint32_t g[NI][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const v4u w = lds_q(tj + (uint32_t)(j * 64 + q * 16));      // pairs 2q, 2q + 1
+#pragma unroll
+            for (int u = 0; u < NI; ++u) {
+                const uint32_t l0 = B3(T_LEAF, in[u][0], w.x, w.y), l1 = B3(T_LEAF, in[u][0], w.z, w.w);
+                g[u][q] = mux(in[u][1], l1, l0);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NI; ++u)
+            o[u][j] = mux(in[u][3], mux(in[u][2], g[u][3], g[u][2]), mux(in[u][2], g[u][1], g[u][0]));
+    }
+}
+
+// the same 16-entry table when it is one table for the whole workgroup (uniform weights): its
+// 64 leaf words come by scalar loads (constant address space) into SGPRs, so the evaluation
+// costs no LDS traffic; a leaf is a v_and + v_xor with SGPR operands (the 2-cycle VOP2 forms,
+// one SGPR per instruction) in place of one v_bitop3 — the same issue cycles
+typedef __attribute__((address_space(4))) const uint32_t ConstW;
+__device__ __forceinline__ void lut_s(uint32_t (&o)[4], const uint32_t (&a)[4], const ConstW* tab) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t g[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t l0 = (a[0] & tab[j * 16 + 4 * q]) ^ tab[j * 16 + 4 * q + 1];
+            const uint32_t l1 = (a[0] & tab[j * 16 + 4 * q + 2]) ^ tab[j * 16 + 4 * q + 3];
+            g[q] = mux(a[1], l1, l0);
+        }
+        o[j] = mux(a[3], mux(a[2], g[3], g[2]), mux(a[2], g[1], g[0]));
+    }
+}
+
+// bit j of the table output for NI inputs (4 b128 loads of the table's bit-j leaves at tab_j)
+template <int NI>
+__device__ __forceinline__ void lut_bit(uint32_t (&o)[NI], const uint32_t (&in)[NI][4], uint32_t tab_j) {
+    uint32_t g[NI][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const v4u w = lds_q(tab_j + (uint32_t)(q * 16));      // pairs 2q, 2q + 1
+#pragma unroll
+        for (int u = 0; u < NI; ++u) {
+            const uint32_t l0 = B3(T_LEAF, in[u][0], w.x, w.y), l1 = B3(T_LEAF, in[u][0], w.z, w.w);
+            g[u][q] = mux(in[u][1], l1, l0);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NI; ++u)
+        o[u] = mux(in[u][3], mux(in[u][2], g[u][3], g[u][2]), mux(in[u][2], g[u][1], g[u][0]));
+}
+
+// lane permutation inside each group of 4 lanes (DPP quad_perm, a VALU move)
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+constexpr int QP_X1 = 0xB1;          // [1, 0, 3, 2]
+constexpr int QP_X2 = 0x4E;          // [2, 3, 0, 1]
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+// OR / sum over the wave (wave-uniform result): butterflies inside each row of 16 lanes by DPP
+// (quad_perm, row_half_mirror, row_mirror), then the four row results by readlane
+__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
+    x |= dpp<QP_X1>(x);
+    x |= dpp<QP_X2>(x);
+    x |= dpp<0x141>(x);
+    x |= dpp<0x140>(x);
+    return (uint32_t)(__builtin_amdgcn_readlane((int)x, 15) | __builtin_amdgcn_readlane((int)x, 31) |
+                      __builtin_amdgcn_readlane((int)x, 47) | __builtin_amdgcn_readlane((int)x, 63));
+}
+__device__ __forceinline__ uint32_t wave_add(uint32_t x) {
+    x += dpp<QP_X1>(x);
+    x += dpp<QP_X2>(x);
+    x += dpp<0x141>(x);
+    x += dpp<0x140>(x);
+    return (uint32_t)(__builtin_amdgcn_readlane((int)x, 15) + __builtin_amdgcn_readlane((int)x, 31) +
+                      __builtin_amdgcn_readlane((int)x, 47) + __builtin_amdgcn_readlane((int)x, 63));
+}
+
+// two smallest of {m1 <= m2} and {b1 <= b2} into m1 <= m2 (4-plane magnitudes)
+__device__ __forceinline__ void merge2(uint32_t (&m1)[4], uint32_t (&m2)[4], const uint32_t (&b1)[4],
+                                       const uint32_t (&b2)[4]) {
+    const uint32_t l = lt4(b1, m1);
+    uint32_t x[4], y[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[i] = mux(l, b2[i], m2[i]);      // the winner's second
+        y[i] = mux(l, m1[i], b1[i]);      // the loser's first
+        m1[i] = mux(l, b1[i], m1[i]);
+    }
+    const uint32_t l2 = lt4(x, y);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m2[i] = mux(l2, x[i], y[i]);
+}
+template <int CTRL>
+__device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]) {
+    uint32_t b1[4], b2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        b1[i] = qperm<CTRL>(m1[i]);
+        b2[i] = qperm<CTRL>(m2[i]);
+    }
+    merge2(m1, m2, b1, b2);
+}
+
+#ifdef BS_DIAG
+#define ABL(bit) (a.ablate & (bit))
+#else
+#define ABL(bit) 0
+#endif
+#ifndef BS_KEEP
+#define BS_KEEP 0
+#endif
+
+// Register budget: the small instances run at 64 VGPRs (WPE 8: three 9-wave workgroups per CU).
+// At a 72-register budget only two were resident (the waves of a workgroup are not spread evenly
+// over the SIMDs): measured 7.56 ms (72 VGPRs) -> 6.51 ms (64) per 2^20-codeword C2 decode.
+template <int D, int DV, int LPC, int VPL, int CPL, bool UCN, bool BIG, bool PK, int WPE>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_bs(BsArgs a) {
+    static_assert(LPC == 2 || LPC == 4, "lanes per check");
+    constexpr int SB = (DV * QMAX + QMAX <= 127) ? 8 : 9;     // planes of S and of lw + S
+    constexpr int EPL = (D + LPC - 1) / LPC;                     // edge slots per check lane
+    constexpr int OB = 4 / LPC;                                  // alpha-table output bits per lane
+    constexpr int VNA = PK ? (DV + 1) / 2 : DV;                  // address words per variable
+    constexpr int VNW = VNA + 1;
+    constexpr int HDW = (EPL + 1) / 2;                           // packed hd addresses per check lane
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();          // slots are LDS-absolute
+    const int tid = threadIdx.x;
+    const int NT = blockDim.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwv = NT >> 6;
+    const int nv = a.n_vars;
+    const int64_t b0 = (int64_t)blockIdx.x * PACK;
+    const int nvalid = (int)min<int64_t>(PACK, a.B - b0);
+    const uint32_t valid = (nvalid >= 32) ? 0xFFFFFFFFu : ((1u << nvalid) - 1u);
+    uint32_t* RED = reinterpret_cast<uint32_t*>(smem + a.off_red);   // [0] wrong_t, [1] all t, [2] APP > 0, [3] bits
+    const int AR = UCN ? 2 * a.arows : a.arows;
+    const int AL = AR * LUT_W, BL = a.bcols * BLUT_W;
+    uint32_t* ALUT = reinterpret_cast<uint32_t*>(smem + a.off_alut);   // [2][AR][LUT_W]
+    uint32_t* BLUT = reinterpret_cast<uint32_t*>(smem + a.off_blut);   // [2][bcols][BLUT_W]
+    const bool ucn = UCN && a.ucn;
+
+    // ---- per-lane variables: slot addresses, variable index, degree bounds of the wave ----------
+    uint32_t va[VPL][VNA];
+    int vv[VPL], dw[VPL], dwmin[VPL];
+    uint32_t tab_b[VPL];
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+        const uint32_t* vt = a.vn_tab + ((size_t)u * NT + tid) * VNW;
+#pragma unroll
+        for (int p = 0; p < VNA; ++p) va[u][p] = vt[p];
+        vv[u] = (int)vt[VNA];                                // -1: no variable
+        dw[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave)]);
+        dwmin[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave) + 1]);
+        tab_b[u] = (a.bcols > 1 && vv[u] >= 0) ? (uint32_t)((vv[u] / (nv / a.bcols)) * BLUT_W * 4) : 0u;
+    }
+    int cn_dmin = a.cn_dmin;
+
+    // ---- channel planes: the lane's variables for the 32 codewords of the pack ------------------
+    // (no __syncthreads_or: it allocates static LDS, which would move the dynamic LDS base
+    // away from 0; the flag word lives in RED)
+    if (tid == 0) RED[7] = 0u;
+    __syncthreads();
+    uint32_t cs[VPL], cm[VPL][4], bg[VPL];
+    int off = 0;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+        cs[u] = 0u;
+        bg[u] = 0u;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) cm[u][p] = 0u;
+        const int v = vv[u];
+        if (v >= 0 && !ABL(32)) {
+            const float* src = a.llr + b0 * nv + v;
+            // all 32 loads issued before any use: one HBM round trip per workgroup prologue (with
+            // batches of 8 the LLR fetch cost 0.75 ms of a 6.5 ms C2 decode, with this 0.44 ms:
+            // the workgroups stay in step, so every pack boundary is a chip-wide HBM burst; a
+            // persistent grid prefetching the next pack during the check phases needed 6 more
+            // loop-carried registers and spilled: 7.56 ms)
+            float xv[PACK];
+#pragma unroll
+            for (int r = 0; r < PACK; ++r) xv[r] = src[(int64_t)min(r, nvalid - 1) * nv];
+#pragma unroll
+            for (int r = 0; r < PACK; ++r) {
+                const float x = xv[r] * a.inv;
+                const float xr = rintf(x);
+                const bool big = BIG && fabsf(x) == a.cu;       // a shortened bit (a.cu > QMAX)
+                off |= ((xr != x || fabsf(xr) > (float)QMAX) && !big) ? 1 : 0;
+                const int xi = (r < nvalid) ? (big ? (x < 0.f ? -QMAX : QMAX) : (int)xr) : 0;
+                const uint32_t m = (uint32_t)(xi < 0 ? -xi : xi);
+                cs[u] |= (xi < 0 ? 1u : 0u) << r;
+                if (BIG) bg[u] |= (big && r < nvalid ? 1u : 0u) << r;
+#pragma unroll
+                for (int p = 0; p < 4; ++p) cm[u][p] |= ((m >> p) & 1u) << r;
+            }
+        }
+    }
+    if (off) atomicOr(&RED[7], 1u);
+    __syncthreads();
+    if (RED[7]) {                              // off the grid: the v5 fixup decodes this pack
+        if (tid == 0) a.bad[blockIdx.x] = 1u;
+        return;
+    }
+    if (tid == 0) a.bad[blockIdx.x] = 0u;
+    // PAD slot (all ones: V->C negative, magnitude 15), ZERO slot (a zero C->V), the zero hard
+    // decision word of UCN padding edges, counters, iteration 0's tables
+    if (tid < SLOT_W) {
+        reinterpret_cast<uint32_t*>(smem + a.off_pad)[tid] = 0xFFFFFFFFu;
+        reinterpret_cast<uint32_t*>(smem + a.off_zero)[tid] = 0u;
+    }
+    if (UCN && tid == 0) lds_put(a.off_hdz, 0u);
+    if (tid < 8) RED[tid] = (tid == 1) ? 0xFFFFFFFFu : 0u;
+    for (int w = tid; w < AL; w += NT) ALUT[w] = a.alut[w];
+    for (int w = tid; w < BL; w += NT) BLUT[w] = a.blut[w];
+    __syncthreads();
+
+    // ---- variable phase -------------------------------------------------------------------------
+    //   first: lw_0 as every edge's V->C (no C->V yet);
+    //   else:  S = sum of the C->V, APP_t = Q(ch) + S (hard decision, counters); unless last,
+    //          Tv = clamp(Q(beta_{t+1} ch) + S) and V->C_e = clamp(Tv - C->V_e, +-15) per edge
+    //   UCN:   the hard decision (APP_t >= 0; first: lw_0 >= 0) to HD[v] for the next check phase
+    auto vn_phase = [&](const bool first, const bool last, const uint32_t bslice, const int tb)
+                        __attribute__((always_inline)) {
+        uint32_t wr = 0u, apos = 0u, nb = 0u;
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) {
+#pragma unroll
+            for (int p = 0; p < VNA; ++p) asm volatile("" : "+v"(va[u][p]));   // unpacked per use
+            auto vaddr = [&](int f) __attribute__((always_inline)) -> uint32_t {
+                if constexpr (PK) return (f & 1) ? (va[u][f >> 1] >> 16) : (va[u][f >> 1] & 0xFFFFu);
+                else return va[u][f];
+            };
+            const int v = vv[u];
+            const bool counted = v >= 0 && v < a.target_bits;
+            uint32_t lw[1][4];                   // |Q(beta_{t+1} ch)| (before the C->V: fewer live registers)
+            if (!last) {
+                if (ABL(2)) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) lw[0][i] = cm[u][i];
+                } else if (a.bcols == 1) {          // one beta per iteration: table in SGPRs
+                    const ConstW* tg = (const ConstW*)(a.blut) + (size_t)tb * BLUT_W;
+                    lut_s(lw[0], cm[u], tg);
+                    if constexpr (BIG) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) lw[0][i] = mux(bg[u], tg[LUT_W + i], lw[0][i]);
+                    }
+                } else {
+                    const uint32_t btab = bslice + tab_b[u];
+                    const uint32_t cmi[1][4] = {{cm[u][0], cm[u][1], cm[u][2], cm[u][3]}};
+                    lut<1>(lw, cmi, btab);
+                    if constexpr (BIG) {
+                        const v4u gb = lds_q(btab + LUT_W * 4);
+                        lw[0][0] = mux(bg[u], gb.x, lw[0][0]);
+                        lw[0][1] = mux(bg[u], gb.y, lw[0][1]);
+                        lw[0][2] = mux(bg[u], gb.z, lw[0][2]);
+                        lw[0][3] = mux(bg[u], gb.w, lw[0][3]);
+                    }
+                }
+            }
+            // C->V of the first KEEP edges stay in registers for the V->C pass, the others are read
+            // again (the register budget of three 9-wave workgroups per CU)
+            constexpr int KEEP = BS_KEEP < DV ? BS_KEEP : DV;
+            uint32_t mn[KEEP > 0 ? KEEP : 1], mb[KEEP > 0 ? KEEP : 1][4];
+            uint32_t S[SB];
+#pragma unroll
+            for (int i = 0; i < SB; ++i) S[i] = 0u;
+            const int dwu = dw[u];
+            if (!first) {
+#pragma unroll
+                for (int f = 0; f < DV; ++f) {
+                    if (f < dwu) {
+                        uint32_t M[4], n, b[4];
+                        read_slot(n, M, vaddr(f));
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) b[i] = M[i] ^ n;
+                        if (f == 0) set_b<SB>(S, b, n);
+                        else add_b<SB>(S, b, n);
+                        if (f < KEEP) {
+                            mn[f < KEEP ? f : 0] = n;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) mb[f < KEEP ? f : 0][i] = b[i];
+                        }
+                    }
+                }
+                // APP_t = Q(ch) + S: the sign (hard decision) from the carry chain alone, the full
+                // sum only in the last iteration (APP > 0 for the loss counter)
+                uint32_t hd, nz = 0u;
+                const uint32_t c_s = cs[u];
+                if (last) {
+                    uint32_t A[SB];
+#pragma unroll
+                    for (int i = 0; i < SB; ++i) A[i] = S[i];
+                    const uint32_t cb[4] = {cm[u][0] ^ c_s, cm[u][1] ^ c_s, cm[u][2] ^ c_s, cm[u][3] ^ c_s};
+                    add_b<SB>(A, cb, c_s);
+                    hd = ~A[SB - 1];
+#pragma unroll
+                    for (int i = 0; i < SB; ++i) nz |= A[i];
+                } else {
+                    uint32_t c = c_s;
+#pragma unroll
+                    for (int i = 0; i < SB - 1; ++i) c = B3(T_MAJ, S[i], i < 4 ? (cm[u][i] ^ c_s) : c_s, c);
+                    hd = B3(T_XNOR3, S[SB - 1], c_s, c);
+                }
+                if (UCN && !last && ucn && v >= 0) lds_put((uint32_t)(4 * v), hd);   // HD[v] (Main_Functions.py:184-188)
+                hd &= valid;                                     // APP >= 0 -> hard decision 1
+                if (ABL(8)) hd = 0u;
+                if (counted) {
+                    wr |= hd;
+                    if (last) {
+                        apos |= hd & nz;
+                        nb += (uint32_t)__popc(hd);
+                    }
+                }
+            }
+            if (last) continue;
+            // Tv = clamp(Q(beta ch) + S): the table gives |Q(beta ch)|, the channel the sign
+            uint32_t lb[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lb[i] = lw[0][i] ^ cs[u];
+            add_b<SB>(S, lb, cs[u]);
+            uint32_t Tv[6];
+            clamp6<SB>(Tv, S);
+            const int dwm = dwmin[u];
+            if (first) {
+                // UCN at t = 0: the hard decision of x~ = Q(beta_0 ch) (Main_Functions.py:181-182)
+                if (UCN && ucn && v >= 0) lds_put((uint32_t)(4 * v), ~Tv[5]);
+                uint32_t x[7], X[4];
+#pragma unroll
+                for (int i = 0; i < 7; ++i) x[i] = Tv[i < 6 ? i : 5];
+                abs_sat(X, x);
+#pragma unroll
+                for (int f = 0; f < DV; ++f)
+                    if (f < dwu && (f < dwm || vaddr(f) != a.off_zero)) write_slot(vaddr(f), x[6], X);
+            } else {
+#pragma unroll
+                for (int f = 0; f < DV; ++f) {
+                    if (f < dwu) {
+                        if (ABL(4)) continue;
+                        uint32_t x[7], X[4], n, b[4];
+                        if (f < KEEP) {
+                            n = mn[f < KEEP ? f : 0];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) b[i] = mb[f < KEEP ? f : 0][i];
+                        } else {
+                            uint32_t M[4];
+                            read_slot(n, M, vaddr(f));
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) b[i] = M[i] ^ n;
+                        }
+                        sub_tv(x, Tv, b, n);
+                        abs_sat(X, x);
+                        if (f < dwm || vaddr(f) != a.off_zero) write_slot(vaddr(f), x[6], X);
+                    }
+                }
+            }
+        }
+        if (!first) {
+            if (!ABL(8)) wr = wave_or(wr);
+            if (last) {
+                apos = wave_or(apos);
+                nb = wave_add(nb);
+            }
+            if (lane == 0) {
+                if (wr) atomicOr(&RED[0], wr);
+                if (last) {
+                    if (apos) atomicOr(&RED[2], apos);
+                    if (nb) atomicAdd(&RED[3], nb);
+                }
+            }
+        }
+    };
+
+    vn_phase(true, false, a.off_blut, 0);
+    // check groups: chunk k of 64 check lanes; lane LPC c + j of it (check c = row i, index h)
+    // takes edges k = LPC m + j, at slots first_i + j A_i + m z + h (a.row_lay); edges past the
+    // degree read the all-ones PAD slot and are not written; idle lanes (c >= n_checks) read PAD
+    // only.  (Lane j of a check's group evaluates alpha-table output bits OB j .. OB j + OB - 1:
+    // 16 words per bit, at 64 B per bit.)
+    const int cj = lane % LPC;
+    int gchunk[CPL], gdeg[CPL];
+    uint32_t gbase[CPL], gtab[CPL], ghd[CPL][UCN ? HDW : 1];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+        gchunk[c] = (CPL == 1) ? wave : __builtin_amdgcn_readfirstlane(a.cn_chunk[wave * CPL + c]);
+        const int ql = max(gchunk[c], 0) * 64 + lane;
+        const int cc = ql / LPC;
+        const int ci = min(cc / a.z, a.n_checks / a.z - 1);
+        gdeg[c] = (cc < a.n_checks) ? a.row_ptr[ci + 1] - a.row_ptr[ci] : 0;
+        gbase[c] = a.off_slots + (uint32_t)((a.row_lay[2 * ci] + cj * a.row_lay[2 * ci + 1] + (cc - ci * a.z)) * SLOT_B);
+        gtab[c] = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * OB * 64);
+        if constexpr (UCN) {
+#pragma unroll
+            for (int p = 0; p < HDW; ++p) ghd[c][p] = (ucn && gchunk[c] >= 0) ? a.cn_hd[(size_t)ql * HDW + p] : 0u;
+        }
+    }
+    const uint32_t cstride = (uint32_t)(a.z * SLOT_B);
+    const uint32_t tabu = (uint32_t)(a.arows * LUT_W * 4);        // alpha' tables after the alpha ones
+    __syncthreads();
+
+    for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
+        if (tid == 0 && t > 0) {            // fold iteration t-1's frame flags
+            RED[1] &= RED[0];
+            RED[0] = 0u;
+        }
+        const int nx = (t + 1) & 1;
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) asm volatile("" : "+s"(dw[u]), "+s"(dwmin[u]));   // compared per use, not hoisted as masks
+        asm volatile("" : "+s"(cn_dmin));
+        // next iteration's tables (their slots were last read two phases ago)
+        if (t + 1 < a.T) {
+            for (int w = tid; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
+            if (a.bcols > 1)
+                for (int w = tid; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
+        }
+        // ======== check nodes ===================================================================
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const bool active = (CPL == 1) ? (tid < a.cn_lanes) : (gchunk[c] >= 0);
+            if (!active || ABL(1)) continue;
+            uint32_t cbase = gbase[c];
+            asm volatile("" : "+v"(cbase));
+            const int cdeg = gdeg[c];
+            // slot m of the lane: always a real edge while LPC m + LPC - 1 < cn_dmin
+            auto real = [&](int m) __attribute__((always_inline)) -> bool {
+                return LPC * m + LPC - 1 < cn_dmin || LPC * m + cj < cdeg;
+            };
+            auto caddr = [&](int m) __attribute__((always_inline)) -> uint32_t {
+                return real(m) ? cbase + m * cstride : a.off_pad;
+            };
+            // pass 1: two minima of |V->C| and the parity of [V->C >= 0] over the lane's edges
+            // (padding edges: negative, magnitude 15), then merged across the lane group
+            // (the lane's EPL slots are read once, all loads issued before any use, and kept
+            // in registers for pass 2)
+            uint32_t Xs[EPL][4], ns[EPL];
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) read_slot(ns[m], Xs[m], caddr(m));
+            // UCN: syndrome of the previous hard decisions over the check (padding edges read a
+            // zero word): odd -> the check is unsatisfied, its messages weighted by alpha'
+            uint32_t syn = 0u;
+            if constexpr (UCN) {
+                if (ucn) {
+#pragma unroll
+                    for (int m = 0; m < EPL; ++m) {
+                        const uint32_t hw = ghd[c][m >> 1];
+                        syn ^= lds_w((m & 1) ? (hw >> 16) : (hw & 0xFFFFu));
+                    }
+                    syn ^= qperm<QP_X1>(syn);
+                    if (LPC == 4) syn ^= qperm<QP_X2>(syn);
+                }
+            }
+            uint32_t m1[4] = {Xs[0][0], Xs[0][1], Xs[0][2], Xs[0][3]}, m2[4] = {~0u, ~0u, ~0u, ~0u};
+            uint32_t par = ns[0];
+#pragma unroll
+            for (int m = 1; m < EPL; ++m) {
+                const uint32_t(&X)[4] = Xs[m];
+                const uint32_t l1 = lt4(X, m1), l2 = lt4(X, m2);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    m2[i] = mux(l1, m1[i], mux(l2, X[i], m2[i]));
+                    m1[i] = mux(l1, X[i], m1[i]);
+                }
+                par ^= ns[m];
+            }
+            par ^= qperm<QP_X1>(par);
+            merge_lanes<QP_X1>(m1, m2);
+            if (LPC == 4) {
+                par ^= qperm<QP_X2>(par);
+                merge_lanes<QP_X2>(m1, m2);
+            }
+            // message k is negative iff an even number of the OTHER edges have V->C >= 0
+            // (Main_Functions.py:251-254): par ^ n_k, par the parity of [V->C >= 0] over the
+            // LPC EPL slots (an even count, padding included)
+            // weighted, quantized minima: each lane evaluates OB output bits, the group shares them
+            uint32_t q1[4], q2[4];
+            {
+                const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
+                const uint32_t tab = gtab[c] + (uint32_t)((t & 1) * AL * 4);
+                uint32_t qb[OB][2];
+#pragma unroll
+                for (int b = 0; b < OB; ++b) {
+                    uint32_t o[2];
+                    lut_bit<2>(o, mm, tab + (uint32_t)(b * 64));
+                    if constexpr (UCN) {
+                        if (ucn) {                    // alpha' where the check is unsatisfied
+                            uint32_t ou[2];
+                            lut_bit<2>(ou, mm, tab + tabu + (uint32_t)(b * 64));
+                            o[0] = mux(syn, ou[0], o[0]);
+                            o[1] = mux(syn, ou[1], o[1]);
+                        }
+                    }
+                    qb[b][0] = o[0];
+                    qb[b][1] = o[1];
+                }
+                if (LPC == 4) {
+                    q1[0] = qperm<0x00>(qb[0][0]); q1[1] = qperm<0x55>(qb[0][0]);
+                    q1[2] = qperm<0xAA>(qb[0][0]); q1[3] = qperm<0xFF>(qb[0][0]);
+                    q2[0] = qperm<0x00>(qb[0][1]); q2[1] = qperm<0x55>(qb[0][1]);
+                    q2[2] = qperm<0xAA>(qb[0][1]); q2[3] = qperm<0xFF>(qb[0][1]);
+                } else {                // lane 0 of a pair holds bits 0, 1; lane 1 bits 2, 3
+                    q1[0] = qperm<0xA0>(qb[0][0]); q1[1] = qperm<0xA0>(qb[OB - 1][0]);
+                    q1[2] = qperm<0xF5>(qb[0][0]); q1[3] = qperm<0xF5>(qb[OB - 1][0]);
+                    q2[0] = qperm<0xA0>(qb[0][1]); q2[1] = qperm<0xA0>(qb[OB - 1][1]);
+                    q2[2] = qperm<0xF5>(qb[0][1]); q2[3] = qperm<0xF5>(qb[OB - 1][1]);
+                }
+            }
+            // pass 2: an edge whose |V->C| equals the minimum gets the weighted second minimum
+            // (if it is not the only one, the two minima are equal), the others the minimum
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) {
+                if (real(m)) {
+                    const uint32_t addr = cbase + m * cstride;
+                    const uint32_t(&X)[4] = Xs[m];
+                    const uint32_t n = ns[m];
+                    uint32_t Mg[4];
+                    uint32_t ne = X[0] ^ m1[0];
+#pragma unroll
+                    for (int i = 1; i < 4; ++i) ne = B3(T_ORXOR, ne, X[i], m1[i]);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) Mg[i] = mux(ne, q1[i], q2[i]);
+                    write_slot(addr, par ^ n, Mg);
+                }
+            }
+        }
+        __syncthreads();
+        // ======== variable nodes ================================================================
+        const uint32_t bslice = a.off_blut + (uint32_t)(nx * BL * 4);
+        if (t == a.T - 1) vn_phase(false, true, bslice, t + 1);
+        else vn_phase(false, false, bslice, t + 1);
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const uint32_t wl = RED[0] & valid;
+        const uint32_t all = RED[1] & RED[0] & valid;
+        const uint32_t ap = RED[2] & valid;
+        if (a.counters) {
+            unsigned long long* cc = reinterpret_cast<unsigned long long*>(a.counters);
+            const unsigned long long c0 = RED[3], c1 = __popc(wl), c2 = __popc(all),
+                                     c3 = 2ull * __popc(ap) + __popc(wl & ~ap);
+            if (c0) atomicAdd(cc + 0, c0);
+            if (c1) atomicAdd(cc + 1, c1);
+            if (c2) atomicAdd(cc + 2, c2);
+            if (c3) atomicAdd(cc + 3, c3);
+        }
+        RED[5] = all;
+        RED[6] = wl;
+    }
+    if (a.flags) {
+        __syncthreads();
+        if (tid < nvalid)
+            a.flags[b0 + tid] = (uint8_t)(((RED[5] >> tid) & 1) | (((RED[6] >> tid) & 1) << 1));
+    }
+}
+
+template <int I>
+int launch_bs(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
+    constexpr BsInst k = kBsInst[I];
+    auto* fn = &k_bs<k.D, k.DV, k.LPC, k.VPL, k.CPL, k.UCN, k.BIG, k.PK, k.WPE>;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)BS_LDS_MAX);
+        attr = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(nblocks), dim3(64 * nw), lds, s, a);
+    return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+}
+
+// per-instance translation units (ldpc_bs_inst.hip, -DBS_INST=i)
+template <int I>
+int bs_launch(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s);
+
+}  // namespace bs
+}  // namespace ldpc

@@ -38,10 +38,11 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
 int fused5_cw(const DevGraph& g, int T);
 
 // bit-sliced (ldpc_bs.hip): 32 codewords per word, counters / flags only, QMS q = 5 / -5
-bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w);
-const char* bs_kernel_name(const DevGraph& g);
+// (clip: clip_LLR, the LLR of shortened bits)
+bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip);
+const char* bs_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip);
 int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
-              int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s);
+              bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s);
 void fused_free(FusedWorkspace& ws);
 
 }  // namespace ldpc

@@ -48,16 +48,16 @@ bool fused_supported(const DevGraph& g, int mode, int T, float clip_llr) {
 }
 
 // counters-only decodes (throughput mode) run the bit-sliced kernel when it applies
-static bool use_bs(const DevGraph& g, int mode, int T, bool ucn, bool per_edge_w) {
+static bool use_bs(const DevGraph& g, int mode, int T, bool ucn, bool per_edge_w, float clip) {
     const int cw = fused5_cw(g, T);
-    return cw > 0 && cw <= 32 && bs_supported(g, mode, ucn, per_edge_w);
+    return cw > 0 && cw <= 32 && bs_supported(g, mode, ucn, per_edge_w, clip);
 }
 
 // the kernel a counters-only decode runs (the throughput / roofline report)
 const char* fused_kernel_name(const DevGraph& g, int mode, int T, float clip_llr, bool ucn,
                               bool per_edge_w) {
     if (!fused_supported(g, mode, T, clip_llr)) return "";
-    if (use_bs(g, mode, T, ucn, per_edge_w)) return bs_kernel_name(g);
+    if (use_bs(g, mode, T, ucn, per_edge_w, clip_llr)) return bs_kernel_name(g, mode, ucn, per_edge_w, clip_llr);
     return fused5_shape_name(g, T);
 }
 
@@ -74,7 +74,7 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
     // counters-only decodes the bit-sliced kernel serves read their LLRs: with an in-kernel
     // channel requested, the caller (ldpc_decode_awgn) generates them into HBM first — the
     // channel kernel plus the bit-sliced decode beat the v5 kernel's in-prologue channel
-    if (b.awgn && !want_bits && !b.app_out && use_bs(g, mode, b.T, ucn, per_edge_w != 0))
+    if (b.awgn && !want_bits && !b.app_out && use_bs(g, mode, b.T, ucn, per_edge_w != 0, b.clip))
         return LDPC_ERR_UNSUPPORTED;
     const float step = mode_step(mode);
     const int cu = clip_units(mode, b.clip);
@@ -95,7 +95,7 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
             return LDPC_ERR_HIP;
         hd_out = ws.hd;
     }
-    if (!want_bits && !b.app_out && !b.awgn && use_bs(g, mode, b.T, ucn, per_edge_w != 0)) {
+    if (!want_bits && !b.app_out && !b.awgn && use_bs(g, mode, b.T, ucn, per_edge_w != 0, b.clip)) {
         // bit-sliced kernel; packs whose LLRs are off the quantizer grid go to the v5 kernel
         const int64_t npk = (b.B + 31) / 32;
         if (npk > ws.bs_bad_n) {
@@ -109,8 +109,12 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
             }
             ws.bs_bad_n = n;
         }
-        int st = bs_decode(g, b, ws, llr, mode, counters, flags, ws.bs_bad, s);
+        int st = bs_decode(g, b, ws, llr, mode, ucn, counters, flags, ws.bs_bad, s);
         if (st != LDPC_OK) return st;
+        // test hook: LDPC_BS_FIXUP=0 skips the v5 fixup, so a test can tell that a batch was
+        // decoded by the bit-sliced kernel alone (flagged packs then contribute nothing)
+        static const bool fixup = !(getenv("LDPC_BS_FIXUP") && atoi(getenv("LDPC_BS_FIXUP")) == 0);
+        if (!fixup) return LDPC_OK;
         return fused5_decode(g, b, ws, llr, mode_qmax(mode), step, cu, per_edge_w != 0, nullptr,
                              counters, flags, s, ws.bs_bad);
     }
