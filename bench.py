@@ -177,6 +177,9 @@ def main():
     ap.add_argument("--snr", type=float, default=None, help="default: the config's SNR")
     ap.add_argument("--iters", type=int, default=None, help="default: the config's T")
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--decoding-type", type=int, default=2, choices=[1, 2, 3],
+                    help="1 MS fp32, 2 QMS (default), 3 MS without the zero nudge")
+    ap.add_argument("--q-bit", type=int, default=5, choices=[6, 5, -5, 4, 3])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--all-kernels", action="store_true",
                     help="also time the non-default kernel and report it under 'kernels'")
@@ -238,7 +241,8 @@ def main():
     B = args.batch
 
     def run(kernel, e2e=False):
-        dec = NMSDecoder(proto, z, W, 2, 5, device=dev, kernel=kernel, B_max=B)
+        dec = NMSDecoder(proto, z, W, args.decoding_type, args.q_bit, device=dev, kernel=kernel,
+                         B_max=B)
         llr = dec.awgn(B, sigma, seed=1076, offset=rank * B, punct=punct, short=short)  # in HBM
         counters = torch.zeros(4, dtype=torch.int64, device=dev)
         name = dec.kernel_info(T)[1]
@@ -338,6 +342,7 @@ def main():
     pdesc = "".join([f", puncture {punct[0]}-{punct[1]}" if punct[0] else "",
                      f", shorten {short[0]}-{short[1]}" if short[0] else ""])
     sh = ",".join(str(x) for x in cfg["sharing"])
+    mdesc = {1: "MS fp32", 3: "MS fp32 (no nudge)"}.get(args.decoding_type, f"QMS q{args.q_bit}")
     out = {
         "metric": f"decoded codewords/sec, {cfg['label']}, {T} NMS iters",
         "value": round(value, 1),
@@ -349,9 +354,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if primary["name"] == "flood" else "i32",
-        "data": f"synthetic (on-GPU Philox AWGN, all-zero codeword, {snr} dB, QMS q=5 LLRs)",
-        "config": {"workload": f"{args.config}: {cfg['graph']} QMS q5 T={T} sharing [{sh}] "
+        "dtype": "i32" if primary["name"].startswith(("bsl", "fused5")) else "f32",
+        "data": f"synthetic (on-GPU Philox AWGN, all-zero codeword, {snr} dB, {mdesc} LLRs)",
+        "config": {"workload": f"{args.config}: {cfg['graph']} {mdesc} T={T} sharing [{sh}] "
                                f"{wdesc}{pdesc}, B={B} codewords/GPU/step @ {snr} dB",
                    "batch_per_gpu": B, "iterations": T, "kernel": primary["name"],
                    "parallelism": f"dp{world}"},
@@ -365,7 +370,8 @@ def main():
                            "ms_per_step": round(1e3 * e2e["elapsed"] / args.steps, 3)}
     if extra:
         out["kernels"] = extra
-    if world == 1 and rank == 0 and not args.no_cpu_baseline and args.config == "C2":
+    if (world == 1 and rank == 0 and not args.no_cpu_baseline and args.config == "C2"
+            and args.decoding_type == 2 and args.q_bit == 5):
         out["cpu_baseline"] = cpu_baseline(proto, g, W, cp, T=T)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -386,7 +386,9 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
     if (mode < 0) return LDPC_ERR_ARG;
     const bool ucn = g->d_alpha_ucn != nullptr;
     int kern = p->kernel;
-    const bool fok = fused_supported(g->dev, mode, p->T, p->clip_llr);
+    // the float modes' fused kernel (ffl) serves counters-only decodes; it is the one reported
+    const bool fl = ffl_mode(mode) && ffl_supported(g->dev, mode, ucn, g->per_edge_w != 0);
+    const bool fok = fl || fused_supported(g->dev, mode, p->T, p->clip_llr);
     if (kern == LDPC_KERNEL_AUTO) kern = fok ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
     if (kern == LDPC_KERNEL_FUSED && !fok) return LDPC_ERR_UNSUPPORTED;
     if (kern != LDPC_KERNEL_FLOOD && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_ARG;
@@ -405,7 +407,8 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
         nm = "flood";
     } else {
         bytes = fused_bytes_per_cw(g->dev, p->T);
-        nm = fused_kernel_name(g->dev, mode, p->T, p->clip_llr, ucn, g->per_edge_w != 0);
+        nm = fl ? ffl_kernel_name(g->dev, ucn, g->per_edge_w != 0)
+                : fused_kernel_name(g->dev, mode, p->T, p->clip_llr, ucn, g->per_edge_w != 0);
     }
     if (bytes_per_cw) *bytes_per_cw = bytes;
     if (name && name_len > 0) {
@@ -429,12 +432,17 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     DeviceGuard dg(g->device);
     const bool ucn = g->d_alpha_ucn != nullptr;
 
+    const bool want_bits = out.hard_bits || out.synd_bits;
     int kern = p->kernel;
-    const bool fok = fused_supported(g->dev, mode, p->T, p->clip_llr);
+    // float modes: the ffl kernel serves counters-only decodes of LLRs in HBM (AUTO takes flood
+    // for APP / bit exports; an in-kernel channel is generated first by the caller)
+    const bool fl = ffl_mode(mode);
+    const bool fok = fl ? (!want_bits && !out.app_all && ffl_supported(g->dev, mode, ucn, g->per_edge_w != 0))
+                        : fused_supported(g->dev, mode, p->T, p->clip_llr);
     if (kern == LDPC_KERNEL_AUTO) kern = fok ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
     if (kern != LDPC_KERNEL_FLOOD && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_ARG;
     if (kern == LDPC_KERNEL_FUSED && !fok) return LDPC_ERR_UNSUPPORTED;
-    if (gen && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_UNSUPPORTED;   // caller falls back
+    if (gen && (kern != LDPC_KERNEL_FUSED || fl)) return LDPC_ERR_UNSUPPORTED;   // caller falls back
 
     const int ntiles = (int)((B + TILE - 1) / TILE);
     const bool count = out.counters || out.frame_flags;
@@ -454,7 +462,6 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     b.anypos = c->anypos;
     b.biterr = c->biterr;
     b.awgn = gen;
-    const bool want_bits = out.hard_bits || out.synd_bits;
 
     if (count && kern == LDPC_KERNEL_FLOOD) {
         if (hipMemsetAsync(c->wrong, 0, (size_t)p->T * ntiles * 4 * sizeof(uint64_t), s) != hipSuccess ||
@@ -474,6 +481,9 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
         b.hd_all = want_bits ? 1 : 0;
         b.store_hd = (ucn || want_bits) ? 1 : 0;
         st = flood_decode(g->dev, b, llr_dev, mode, ucn, s);
+    } else if (fl) {
+        st = ffl_decode(g->dev, b, llr_dev, mode, ucn, g->per_edge_w != 0, out.counters,
+                        out.frame_flags, s);
     } else {
         st = fused_decode(g->dev, b, c->fused, llr_dev, mode, ucn, want_bits, c->ntiles_max,
                           c->T_max, g->per_edge_w, out.counters, out.frame_flags, s);

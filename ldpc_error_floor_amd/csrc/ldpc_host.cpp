@@ -62,7 +62,7 @@ int build_graph(const int32_t* proto, int32_t M, int32_t N, int32_t z, GraphTabl
         h.push_back(r0 * z + (pe - r0));
         h.push_back(g.row_ptr[(size_t)i + 1] - r0);
         h.push_back(g.pe_shift[(size_t)pe]);
-        h.push_back(0);
+        h.push_back(((i * z) << 6) | (pe - r0));      // first check of the row, position (ffl)
     }
     return LDPC_OK;
 }

@@ -51,7 +51,7 @@ struct GraphTables {
     std::vector<int32_t> col_ptr;    // [N+1]
     std::vector<int32_t> col_pe;     // [E] proto edges of each column, ascending row
     // the device image: row_ptr | pe_row | pe_col | pe_shift | col_ptr | col_pe | pad to 16 B |
-    // vn_edge [E] int4 {r0*z + (pe - r0), row degree, shift, 0} in column order
+    // vn_edge [E] int4 {r0*z + (pe - r0), row degree, shift, (i*z) << 6 | (pe - r0)} in column order
     std::vector<int32_t> device_block;
     size_t off_vn = 0;               // int32 offset of vn_edge inside device_block
 };

@@ -21,7 +21,7 @@ struct DevGraph {
     const int32_t* pe_shift;   // [E]  P[i,j] mod z
     const int32_t* col_ptr;    // [N+1]
     const int32_t* col_pe;     // [E]  proto edges of each column, ascending row
-    const int4* vn_edge;       // [E]  column order: {r0*z + (pe - r0), row degree, shift, 0}
+    const int4* vn_edge;       // [E]  column order: {r0*z + (pe - r0), row degree, shift, (i*z) << 6 | (pe - r0)}
     const int32_t* h_row_ptr;  // [M+1] host copy of row_ptr (kernel planning)
     // [M] row i may share check groups with row i-1 (equal degree and weights; set by
     // ldpc_weights_set): host copy for planning, device copy for the address tables

@@ -1,0 +1,73 @@
+"""The fused float-mode kernel (csrc/ldpc_ffl.hip: min-sum fp32, min-sum without the nudge,
+QMS q = 6) that serves counters-only decodes (GPU only).  Its arithmetic is the flood kernel's
+operation for operation, so counters and per-frame flags must equal flood's bit for bit (flood's
+APP is pinned to the reference fixtures in test_gpu_parity.py): wman with trained [3,0,3] and
+UCN [3,3,3] weights, 5G BG2 with puncture / shortening, ragged batches."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+DATA = os.path.join(ROOT, "ldpc_error_floor_amd", "data")
+
+
+def _dec(device, cfg, dt, q, T=None, ucn=False):
+    import bench
+    from ldpc_error_floor_amd.code import TannerGraph, load_base_graph
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    from ldpc_error_floor_amd.weights import expand_weights, read_weight_file
+    c = bench.CONFIGS[cfg]
+    if cfg == "C2" and ucn:
+        proto = load_base_graph(os.path.join(DATA, "BaseGraph", c["graph"] + ".txt"))
+        g = TannerGraph(proto, c["z"])
+        wf = read_weight_file(os.path.join(DATA, c["weights"]))
+        W = expand_weights((3, 3, 3), dict(wf.blocks), T or 20, g)
+        cp = bench.load_problem(T=T, config=cfg)[3]
+    else:
+        proto, g, W, cp = bench.load_problem(T=T, config=cfg)
+    dec = NMSDecoder(proto, c["z"], W, dt, q, device=device)
+    dec.punct = c.get("punct", (0, 0))
+    dec.short = c.get("short", (0, 0))
+    return dec, cp, c
+
+
+@pytest.mark.parametrize("cfg,dt,q,ucn,B,snr", [
+    ("C2", 1, 5, False, 3001, 2.0), ("C2", 3, 5, False, 777, 2.0), ("C2", 2, 6, False, 3001, 2.0),
+    ("C2", 1, 5, True, 2049, 2.25), ("C4", 1, 5, True, 1000, 1.25), ("C4", 3, 5, True, 257, 1.25),
+    ("C2", 1, 5, False, 40000, 2.5)])
+def test_ffl_equals_flood(cuda_device, cfg, dt, q, ucn, B, snr):
+    dec, cp, c = _dec(cuda_device, cfg, dt, q, ucn=ucn)
+    name = dec.kernel_info()[1]
+    assert name.startswith("ffl["), name
+    llr = dec.awgn(B, float(cp.sigma(snr)), seed=13, offset=5)
+    out = {}
+    for k in ("flood", "fused"):
+        r = dec.decode(llr, app=False, counters=True, flags=True, kernel=k)
+        out[k] = (r.counters.cpu().numpy(), r.flags.cpu().numpy())
+    assert np.array_equal(out["fused"][0], out["flood"][0]), (out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
+    assert 0 < out["fused"][0][1] < B
+
+
+def test_ffl_app_export_stays_on_flood(cuda_device):
+    """An APP / bit export in a float mode runs flood under AUTO; FUSED refuses it."""
+    dec, cp, c = _dec(cuda_device, "C2", 1, 5)
+    llr = dec.awgn(64, float(cp.sigma(2.0)), seed=1)
+    r = dec.decode(llr, app=True, counters=True)
+    f = dec.decode(llr, app=False, counters=True)
+    assert np.array_equal(r.counters.cpu().numpy(), f.counters.cpu().numpy())
+    with pytest.raises(RuntimeError):
+        dec.decode(llr, app=True, kernel="fused")
+
+
+def test_ffl_decode_awgn_matches_channel_then_decode(cuda_device):
+    dec, cp, c = _dec(cuda_device, "C4", 1, 5)
+    sigma = float(cp.sigma(1.25))
+    a = dec.decode_awgn(2000, sigma, seed=3, offset=11, counters=True, flags=True)
+    llr = dec.awgn(2000, sigma, seed=3, offset=11)
+    b = dec.decode(llr, app=False, counters=True, flags=True, kernel="flood")
+    assert np.array_equal(a.counters.cpu().numpy(), b.counters.cpu().numpy())
+    assert np.array_equal(a.flags.cpu().numpy(), b.flags.cpu().numpy())

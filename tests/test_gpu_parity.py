@@ -28,6 +28,11 @@ def _decoder(c, kernel, device):
     return dec
 
 
+def _float_mode(c):
+    """MS, MS without nudge and QMS q = 6: the fused path is the counters-only ffl kernel."""
+    return c["dt"] in (1, 3) or (c["dt"] == 2 and c["q"] == 6)
+
+
 def test_extension_is_native(cuda_device):
     from ldpc_error_floor_amd import _native
     mod = _native.load()
@@ -41,6 +46,15 @@ def test_decoder_matches_reference(name, kernel, cuda_device):
     from ldpc_error_floor_amd.decoder import unpack_bits
     c = load_case(name)
     dec = _decoder(c, kernel, cuda_device)
+    if kernel == "fused" and _float_mode(c):
+        # the float modes' fused kernel (ffl) decodes counters and frame flags only: they equal
+        # the flood kernel's bit for bit (whose APP the flood case checks against the fixture)
+        assert dec.kernel_info()[1].startswith("ffl["), dec.kernel_info()
+        full = _decoder(c, "flood", cuda_device).decode(c["llr"], app=True, counters=True, flags=True)
+        res = dec.decode(c["llr"], app=False, counters=True, flags=True)
+        assert np.array_equal(res.counters.cpu().numpy(), full.counters.cpu().numpy())
+        assert np.array_equal(res.flags.cpu().numpy(), full.flags.cpu().numpy())
+        return
     res = dec.decode(c["llr"], app=True, hard=True, synd=True, counters=True, flags=True)
     app = res.app.cpu().numpy()
     ref = c["app"]
@@ -100,7 +114,9 @@ def test_counters_only_decode_matches_reference(name, kernel, cuda_device):
     c = load_case(name)
     dec = _decoder(c, kernel, cuda_device)
     res = dec.decode(c["llr"], app=False, counters=True, flags=True)
-    full = dec.decode(c["llr"], app=True, counters=True, flags=True)
+    # (the float modes' fused kernel exports no APP: the full decode is flood's)
+    full_dec = _decoder(c, "flood", cuda_device) if kernel == "fused" and _float_mode(c) else dec
+    full = full_dec.decode(c["llr"], app=True, counters=True, flags=True)
     assert np.array_equal(res.counters.cpu().numpy(), full.counters.cpu().numpy())
     assert np.array_equal(res.flags.cpu().numpy(), full.flags.cpu().numpy())
     if c["exact"]:
