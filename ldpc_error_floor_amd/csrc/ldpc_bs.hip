@@ -84,7 +84,7 @@ struct BsPlan {
 // one m, slots first + j A + h: with first_i = first_{i-1} + z (mod 32) the checks stay
 // consecutive mod 32 across a row boundary, and A_i is the smallest stride >= the j = 0 block
 // whose multiples j A_i (j < LPC) are at least 32 / LPC apart mod 32.
-static std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* nslot) {
+std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* nslot) {
     std::vector<int32_t> lay((size_t)2 * h.M, 0);
     const int sep = 32 / LPC;
     auto ok = [&](int A) {
@@ -191,13 +191,13 @@ BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float cli
 using namespace bs;
 
 bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip) {
-    return bs_plan(g, mode, ucn, per_edge_w, clip).ok;
+    return bs_plan(g, mode, ucn, per_edge_w, clip).ok || bsc_supported(g, mode, ucn, per_edge_w, clip);
 }
 
 const char* bs_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip) {
     static thread_local char buf[64];
     const BsPlan p = bs_plan(g, mode, ucn, per_edge_w, clip);
-    if (!p.ok) return "";
+    if (!p.ok) return bsc_kernel_name(g, mode, ucn, per_edge_w, clip);
     const BsInst& k = kBsInst[p.inst];
     if (k.VPL == 1 && k.CPL == 1)
         snprintf(buf, sizeof(buf), "bsl[p32,w%d,d%d,v%d,l%d%s]", p.nw, k.D, k.DV, k.LPC, p.ucn ? ",ucn" : "");
@@ -210,7 +210,8 @@ const char* bs_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_
 // Deal `n` chunks (costs `cost`) to nw waves with at most `cap` chunks per wave, balancing the
 // four SIMDs (wave w runs on SIMD w mod 4): heaviest chunk first, to the least-loaded SIMD that
 // has a wave with room, on that SIMD's wave with the fewest chunks.  slot[w][c] = chunk or -1.
-static std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap) {
+namespace bs {
+std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap) {
     const int n = (int)cost.size();
     std::vector<int> order(n), slot((size_t)nw * cap, -1), used(nw, 0), load(4, 0);
     for (int c = 0; c < n; ++c) order[c] = c;
@@ -229,6 +230,30 @@ static std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int ca
     }
     return slot;
 }
+
+// the per-decode weight tables of both bit-sliced kernels (k_bs_tables)
+int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, float cu,
+                   bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s) {
+    const size_t na = (size_t)b.T * ar * LUT_W, nb = (size_t)b.T * bcols * BLUT_W;
+    const size_t bytes = (na + nb) * 4;
+    if (bytes > ws.bs_lut_bytes) {
+        if (ws.bs_lut) (void)hipFree(ws.bs_lut);
+        ws.bs_lut = nullptr;
+        ws.bs_lut_bytes = 0;
+        if (hipMalloc(&ws.bs_lut, bytes) != hipSuccess) { (void)hipGetLastError(); return LDPC_ERR_OOM; }
+        ws.bs_lut_bytes = bytes;
+    }
+    *alut = reinterpret_cast<uint32_t*>(ws.bs_lut);
+    *blut = *alut + na;
+    const int ntab = b.T * (ar + bcols);
+    // without UCN weights the alpha' slots (UCN instances) repeat the alpha tables (unused)
+    const float* au = (ucn && b.alpha_ucn) ? b.alpha_ucn : b.alpha;
+    hipLaunchKernelGGL(k_bs_tables, dim3((unsigned)((ntab + 127) / 128)), dim3(128), 0, s, b.alpha, au,
+                       b.beta, g.row_ptr, b.T, g.E, g.N, arows, ar, bcols, step, 1.0f / step, cu,
+                       *alut, *blut);
+    return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+}
+}  // namespace bs
 
 // graph tables, built once per context on the host (ws.bs_graph)
 static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& ws, hipStream_t s) {
@@ -356,7 +381,7 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
 int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
               bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s) {
     const BsPlan p = bs_plan(g, mode, ucn, false, b.clip);
-    if (!p.ok) return LDPC_ERR_UNSUPPORTED;
+    if (!p.ok) return bsc_decode(g, b, ws, llr, mode, ucn, counters, flags, bad, s);
     if (ws.bs_graph && ws.bs_graph_inst != p.inst) {
         (void)hipFree(ws.bs_graph);
         ws.bs_graph = nullptr;
@@ -366,24 +391,9 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     const BsInst& k = kBsInst[p.inst];
     const float step = mode_step_bs(mode);
     const int ar = (k.UCN ? 2 : 1) * p.arows;
-    const size_t na = (size_t)b.T * ar * LUT_W, nb = (size_t)b.T * p.bcols * BLUT_W;
-    const size_t bytes = (na + nb) * 4;
-    if (bytes > ws.bs_lut_bytes) {
-        if (ws.bs_lut) (void)hipFree(ws.bs_lut);
-        ws.bs_lut = nullptr;
-        ws.bs_lut_bytes = 0;
-        if (hipMalloc(&ws.bs_lut, bytes) != hipSuccess) { (void)hipGetLastError(); return LDPC_ERR_OOM; }
-        ws.bs_lut_bytes = bytes;
-    }
-    uint32_t* alut = reinterpret_cast<uint32_t*>(ws.bs_lut);
-    uint32_t* blut = alut + na;
-    const int ntab = b.T * (ar + p.bcols);
-    // without UCN weights the alpha' slots (UCN instances) repeat the alpha tables (unused)
-    const float* au = (ucn && b.alpha_ucn) ? b.alpha_ucn : b.alpha;
-    hipLaunchKernelGGL(k_bs_tables, dim3((unsigned)((ntab + 127) / 128)), dim3(128), 0, s, b.alpha, au,
-                       b.beta, g.row_ptr, b.T, g.E, g.N, p.arows, ar, p.bcols, step, 1.0f / step,
-                       p.cu, alut, blut);
-    if (hipGetLastError() != hipSuccess) return LDPC_ERR_HIP;
+    uint32_t *alut = nullptr, *blut = nullptr;
+    st = bs_make_tables(b, g, p.arows, ar, p.bcols, step, p.cu, ucn, ws, &alut, &blut, s);
+    if (st != LDPC_OK) return st;
     const int DV = k.DV;
     const int VNW = (k.PK ? (DV + 1) / 2 : DV) + 1;
     const uint32_t* gt = reinterpret_cast<const uint32_t*>(ws.bs_graph);

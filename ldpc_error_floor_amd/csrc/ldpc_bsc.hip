@@ -1,0 +1,695 @@
+// ldpc_bsc.hip — bit-sliced fused QMS decoder with COMPRESSED check messages ("bsc"), for the
+// graphs whose one-slot-per-edge state (ldpc_bs_kernel.h: 20 B per lifted edge and pack) does
+// not fit the 160 KB of LDS — 5G NR BG1 n2112 (C5: 8,784 edges = 176 KB).
+//
+// Same arithmetic and semantics as the bsl kernel (32 codewords per 32-bit word, one pack per
+// workgroup, Main_Functions.py:157-335 in units of the q-bit grid) with a different state
+// split (LDS per pack, BG1: 151 KB):
+//   TV[v][6]      Tv = clamp(Q(beta ch) + S, [-32, 31]) per variable (6 two's-complement planes)
+//   REC[c][8]     the check's two possible C->V magnitudes: q1 (every edge whose |V->C| is not
+//                 the minimum) and q2 (those that are), 4 planes each
+//   SGN[e], ARG[e] per edge: the C->V sign (parity ^ own V->C sign) and [|V->C| == minimum]
+// so the check phase recomputes V->C = clamp(Tv - C->V_old, +-15) from Tv and its own previous
+// message (instead of the variable phase writing it per edge), and the variable phase reads
+// each edge's C->V as (SGN, ARG ? q2 : q1) from the check's record.  The check side keeps the
+// bsl structure (LPC lanes per check, quad DPP merges, alpha table by mux tree); the variable
+// side needs no per-edge write-back.  Variable lanes hold several variables (VPL) and check
+// lanes several 64-lane chunks (CPL), one 16-wave workgroup per CU.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "ldpc_bs_kernel.h"
+
+namespace ldpc {
+namespace bs {
+
+// instances: D = check-degree bound, DVH / DVL = variable-degree bound of a lane's first /
+// other variables, LPC lanes per check, VPL variables and CPL check chunks per lane
+struct BscInst { int D, DVH, DVL, LPC, VPL, CPL; int WPE; };
+constexpr BscInst kBscInst[] = {
+    {20, 10, 5, 4, 3, 3, 4},          // 5G BG1 (C5): degree 19 rows, degree 10 / 8 columns
+};
+
+struct BscArgs {
+    const float* llr;
+    int64_t B;
+    int n_vars, n_checks, T, target_bits, cn_dmin, z;
+    float inv, cu;
+    int beta_id;                 // every beta is 1: Q(beta ch) = ch, no table
+    const int32_t* row_ptr;
+    const int32_t* row_lay;      // [M][2] slot layout (as bsl): first slot, j-block stride
+    const uint32_t* vn_tab;      // [VPL][64 nw][DVH + 1]: per edge slot | check << 16, variable
+    const int32_t* vn_wdeg;      // [VPL][nw][2]
+    const int32_t* cn_chunk;     // [nw][CPL]
+    const uint32_t* cn_var;      // [chunks * 64][CVW] variables of the lane's edges (16-bit packed)
+    const uint32_t* alut;        // [T][arows][LUT_W]
+    const uint32_t* blut;        // [T][bcols][BLUT_W]
+    int arows, bcols;
+    int64_t* counters;
+    uint8_t* flags;
+    uint32_t* bad;
+    uint32_t off_a, off_rec, off_tv, off_red, off_alut, off_blut;   // SGN at LDS byte 0
+};
+
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) v2u LdsD;
+__device__ __forceinline__ v2u lds_d(uint32_t addr) { return *reinterpret_cast<const LdsD*>(addr); }
+__device__ __forceinline__ void lds_dput(uint32_t addr, uint32_t x, uint32_t y) {
+    v2u v;
+    v.x = x;
+    v.y = y;
+    *reinterpret_cast<LdsD*>(addr) = v;
+}
+
+template <int D, int DVH, int DVL, int LPC, int VPL, int CPL, int WPE>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_bsc(BscArgs a) {
+    constexpr int SB = (DVH * QMAX + QMAX <= 127) ? 8 : 9;
+    constexpr int EPL = (D + LPC - 1) / LPC;
+    constexpr int OB = 4 / LPC;
+    constexpr int VNW = DVH + 1;
+    constexpr int CVW = (EPL + 1) / 2;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();          // LDS-absolute addresses
+    const int tid = threadIdx.x;
+    const int NT = blockDim.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwv = NT >> 6;
+    const int nv = a.n_vars;
+    const int64_t b0 = (int64_t)blockIdx.x * PACK;
+    const int nvalid = (int)min<int64_t>(PACK, a.B - b0);
+    const uint32_t valid = (nvalid >= 32) ? 0xFFFFFFFFu : ((1u << nvalid) - 1u);
+    uint32_t* RED = reinterpret_cast<uint32_t*>(smem + a.off_red);
+    const int AL = a.arows * LUT_W, BL = a.bcols * BLUT_W;
+    uint32_t* ALUT = reinterpret_cast<uint32_t*>(smem + a.off_alut);
+    uint32_t* BLUT = reinterpret_cast<uint32_t*>(smem + a.off_blut);
+
+    // ---- per-lane variables ------------------------------------------------------------------
+    uint32_t va[VPL][DVH];
+    int vv[VPL], dw[VPL], dwmin[VPL];
+    uint32_t tab_b[VPL];
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+        const int dvu = u == 0 ? DVH : DVL;
+        const uint32_t* vt = a.vn_tab + ((size_t)u * NT + tid) * VNW;
+#pragma unroll
+        for (int p = 0; p < DVH; ++p) va[u][p] = (p < dvu) ? vt[p] : 0u;
+        vv[u] = (int)vt[DVH];
+        dw[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave)]);
+        dwmin[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave) + 1]);
+        tab_b[u] = (a.bcols > 1 && vv[u] >= 0) ? (uint32_t)((vv[u] / (nv / a.bcols)) * BLUT_W * 4) : 0u;
+    }
+    (void)dwmin;
+
+    // ---- channel planes (as bsl: shortened bits = +-cu decoded here, other off-grid packs
+    // flagged for the v5 fixup) --------------------------------------------------------------
+    if (tid == 0) RED[7] = 0u;
+    __syncthreads();
+    uint32_t cs[VPL], cm[VPL][4], bg[VPL];
+    int off = 0;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+        cs[u] = 0u;
+        bg[u] = 0u;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) cm[u][p] = 0u;
+        const int v = vv[u];
+        if (v >= 0) {
+            const float* src = a.llr + b0 * nv + v;
+            float xv[PACK];
+#pragma unroll
+            for (int r = 0; r < PACK; ++r) xv[r] = src[(int64_t)min(r, nvalid - 1) * nv];
+#pragma unroll
+            for (int r = 0; r < PACK; ++r) {
+                const float x = xv[r] * a.inv;
+                const float xr = rintf(x);
+                const bool big = fabsf(x) == a.cu;
+                off |= ((xr != x || fabsf(xr) > (float)QMAX) && !big) ? 1 : 0;
+                const int xi = (r < nvalid) ? (big ? (x < 0.f ? -QMAX : QMAX) : (int)xr) : 0;
+                const uint32_t m = (uint32_t)(xi < 0 ? -xi : xi);
+                cs[u] |= (xi < 0 ? 1u : 0u) << r;
+                bg[u] |= (big && r < nvalid ? 1u : 0u) << r;
+#pragma unroll
+                for (int p = 0; p < 4; ++p) cm[u][p] |= ((m >> p) & 1u) << r;
+            }
+        }
+    }
+    if (off) atomicOr(&RED[7], 1u);
+    __syncthreads();
+    if (RED[7]) {
+        if (tid == 0) a.bad[blockIdx.x] = 1u;
+        return;
+    }
+    if (tid == 0) a.bad[blockIdx.x] = 0u;
+    // the zero edge / zero record (padding edges of the variable lanes), counters, tables
+    if (tid < 8) reinterpret_cast<uint32_t*>(smem + a.off_rec)[(size_t)a.n_checks * 8 + tid] = 0u;
+    if (tid < 8) RED[tid] = (tid == 1) ? 0xFFFFFFFFu : 0u;
+    for (int w = tid; w < AL; w += NT) ALUT[w] = a.alut[w];
+    for (int w = tid; w < BL; w += NT) BLUT[w] = a.blut[w];
+    __syncthreads();
+
+    // ---- variable phase --------------------------------------------------------------------
+    //   S = sum of the C->V (SGN, ARG ? q2 : q1), APP_t = Q(ch) + S (hard decision, counters);
+    //   unless last, TV[v] = clamp(Q(beta_{t+1} ch) + S)
+    auto vn_phase = [&](const bool first, const bool last, const uint32_t bslice, const int tb)
+                        __attribute__((always_inline)) {
+        uint32_t wr = 0u, apos = 0u, nb = 0u;
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) {
+            const int dvu = u == 0 ? DVH : DVL;
+#pragma unroll
+            for (int p = 0; p < DVH; ++p)
+                if (p < dvu) asm volatile("" : "+v"(va[u][p]));
+            const int v = vv[u];
+            const bool counted = v >= 0 && v < a.target_bits;
+            uint32_t lw[1][4];
+            if (!last) {
+                if (a.beta_id) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) lw[0][i] = cm[u][i];
+                } else if (a.bcols == 1) {
+                    const ConstW* tg = (const ConstW*)(a.blut) + (size_t)tb * BLUT_W;
+                    lut_s(lw[0], cm[u], tg);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) lw[0][i] = mux(bg[u], tg[LUT_W + i], lw[0][i]);
+                } else {
+                    const uint32_t btab = bslice + tab_b[u];
+                    const uint32_t cmi[1][4] = {{cm[u][0], cm[u][1], cm[u][2], cm[u][3]}};
+                    lut<1>(lw, cmi, btab);
+                    const v4u gb = lds_q(btab + LUT_W * 4);
+                    lw[0][0] = mux(bg[u], gb.x, lw[0][0]);
+                    lw[0][1] = mux(bg[u], gb.y, lw[0][1]);
+                    lw[0][2] = mux(bg[u], gb.z, lw[0][2]);
+                    lw[0][3] = mux(bg[u], gb.w, lw[0][3]);
+                }
+            }
+            uint32_t S[SB];
+#pragma unroll
+            for (int i = 0; i < SB; ++i) S[i] = 0u;
+            const int dwu = dw[u];
+            if (!first) {
+#pragma unroll
+                for (int f = 0; f < DVH; ++f) {
+                    if (f < dvu && f < dwu) {
+                        const uint32_t wd = va[u][f];
+                        const uint32_t sa = (wd & 0xFFFFu) << 2;
+                        const uint32_t ra = a.off_rec + ((wd >> 16) << 5);
+                        const uint32_t n = lds_w(sa), am = lds_w(sa + a.off_a);
+                        const v4u q1 = lds_q(ra), q2 = lds_q(ra + 16);
+                        uint32_t b[4];
+                        b[0] = mux(am, q2.x, q1.x) ^ n;
+                        b[1] = mux(am, q2.y, q1.y) ^ n;
+                        b[2] = mux(am, q2.z, q1.z) ^ n;
+                        b[3] = mux(am, q2.w, q1.w) ^ n;
+                        if (f == 0) set_b<SB>(S, b, n);
+                        else add_b<SB>(S, b, n);
+                    }
+                }
+                uint32_t hd, nz = 0u;
+                const uint32_t c_s = cs[u];
+                if (last) {
+                    uint32_t A[SB];
+#pragma unroll
+                    for (int i = 0; i < SB; ++i) A[i] = S[i];
+                    const uint32_t cb[4] = {cm[u][0] ^ c_s, cm[u][1] ^ c_s, cm[u][2] ^ c_s, cm[u][3] ^ c_s};
+                    add_b<SB>(A, cb, c_s);
+                    hd = ~A[SB - 1];
+#pragma unroll
+                    for (int i = 0; i < SB; ++i) nz |= A[i];
+                } else {
+                    uint32_t c = c_s;
+#pragma unroll
+                    for (int i = 0; i < SB - 1; ++i) c = B3(T_MAJ, S[i], i < 4 ? (cm[u][i] ^ c_s) : c_s, c);
+                    hd = B3(T_XNOR3, S[SB - 1], c_s, c);
+                }
+                hd &= valid;
+                if (counted) {
+                    wr |= hd;
+                    if (last) {
+                        apos |= hd & nz;
+                        nb += (uint32_t)__popc(hd);
+                    }
+                }
+            }
+            if (last || v < 0) continue;
+            uint32_t lb[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lb[i] = lw[0][i] ^ cs[u];
+            add_b<SB>(S, lb, cs[u]);
+            uint32_t Tv[6];
+            clamp6<SB>(Tv, S);
+            const uint32_t ta = a.off_tv + 24u * (uint32_t)v;
+            lds_dput(ta, Tv[0], Tv[1]);
+            lds_dput(ta + 8, Tv[2], Tv[3]);
+            lds_dput(ta + 16, Tv[4], Tv[5]);
+        }
+        if (!first) {
+            wr = wave_or(wr);
+            if (last) {
+                apos = wave_or(apos);
+                nb = wave_add(nb);
+            }
+            if (lane == 0) {
+                if (wr) atomicOr(&RED[0], wr);
+                if (last) {
+                    if (apos) atomicOr(&RED[2], apos);
+                    if (nb) atomicAdd(&RED[3], nb);
+                }
+            }
+        }
+    };
+
+    vn_phase(true, false, a.off_blut, 0);
+    // check groups (as bsl): lane LPC c + j of a chunk takes edges k = LPC m + j of check c
+    const int cj = lane % LPC;
+    int gchunk[CPL], gdeg[CPL];
+    uint32_t gslot[CPL], grec[CPL], gtab[CPL], gvar[CPL][CVW];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+        gchunk[c] = __builtin_amdgcn_readfirstlane(a.cn_chunk[wave * CPL + c]);
+        const int ql = max(gchunk[c], 0) * 64 + lane;
+        const int cc = ql / LPC;
+        const int ci = min(cc / a.z, a.n_checks / a.z - 1);
+        gdeg[c] = (cc < a.n_checks) ? a.row_ptr[ci + 1] - a.row_ptr[ci] : 0;
+        gslot[c] = (uint32_t)(4 * (a.row_lay[2 * ci] + cj * a.row_lay[2 * ci + 1] + (cc - ci * a.z)));
+        grec[c] = a.off_rec + 32u * (uint32_t)min(cc, a.n_checks - 1);
+        gtab[c] = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * OB * 64);
+#pragma unroll
+        for (int p = 0; p < CVW; ++p) gvar[c][p] = gchunk[c] >= 0 ? a.cn_var[(size_t)ql * CVW + p] : 0u;
+    }
+    const uint32_t sstride = (uint32_t)(4 * a.z);
+    int cn_dmin = a.cn_dmin;
+    __syncthreads();
+
+    for (int t = 0; t < a.T; ++t) {
+        if (tid == 0 && t > 0) {
+            RED[1] &= RED[0];
+            RED[0] = 0u;
+        }
+        const int nx = (t + 1) & 1;
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) asm volatile("" : "+s"(dw[u]));
+        asm volatile("" : "+s"(cn_dmin));
+        if (t + 1 < a.T) {
+            for (int w = tid; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
+            if (a.bcols > 1)
+                for (int w = tid; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
+        }
+        // ======== check nodes ===================================================================
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            if (gchunk[c] < 0) continue;
+            const int cdeg = gdeg[c];
+            uint32_t sbase = gslot[c];
+            asm volatile("" : "+v"(sbase));
+            auto real = [&](int m) __attribute__((always_inline)) -> bool {
+                return LPC * m + LPC - 1 < cn_dmin || LPC * m + cj < cdeg;
+            };
+            // V->C = clamp(Tv - C->V_old, +-15) of the lane's edges (padding: negative, 15)
+            v4u q1o = {0u, 0u, 0u, 0u}, q2o = {0u, 0u, 0u, 0u};
+            if (t > 0) {
+                q1o = lds_q(grec[c]);
+                q2o = lds_q(grec[c] + 16);
+            }
+            uint32_t Xs[EPL][4], ns[EPL];
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) {
+                const uint32_t vw = gvar[c][m >> 1];
+                const uint32_t vi = (m & 1) ? (vw >> 16) : (vw & 0xFFFFu);
+                const uint32_t ta = a.off_tv + 24u * vi;
+                const v2u t01 = lds_d(ta), t23 = lds_d(ta + 8), t45 = lds_d(ta + 16);
+                const uint32_t Tv[6] = {t01.x, t01.y, t23.x, t23.y, t45.x, t45.y};
+                uint32_t x[7];
+                if (t == 0) {
+#pragma unroll
+                    for (int i = 0; i < 7; ++i) x[i] = Tv[i < 6 ? i : 5];
+                } else {
+                    const uint32_t sa = sbase + m * sstride;
+                    const uint32_t so = lds_w(sa), ao = lds_w(sa + a.off_a);
+                    uint32_t bo[4];
+                    bo[0] = mux(ao, q2o.x, q1o.x) ^ so;
+                    bo[1] = mux(ao, q2o.y, q1o.y) ^ so;
+                    bo[2] = mux(ao, q2o.z, q1o.z) ^ so;
+                    bo[3] = mux(ao, q2o.w, q1o.w) ^ so;
+                    sub_tv(x, Tv, bo, so);
+                }
+                abs_sat(Xs[m], x);
+                ns[m] = x[6];
+                if (!(LPC * m + LPC - 1 < cn_dmin) && !real(m)) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) Xs[m][i] = ~0u;
+                    ns[m] = ~0u;
+                }
+            }
+            uint32_t m1[4] = {Xs[0][0], Xs[0][1], Xs[0][2], Xs[0][3]}, m2[4] = {~0u, ~0u, ~0u, ~0u};
+            uint32_t par = ns[0];
+#pragma unroll
+            for (int m = 1; m < EPL; ++m) {
+                const uint32_t(&X)[4] = Xs[m];
+                const uint32_t l1 = lt4(X, m1), l2 = lt4(X, m2);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    m2[i] = mux(l1, m1[i], mux(l2, X[i], m2[i]));
+                    m1[i] = mux(l1, X[i], m1[i]);
+                }
+                par ^= ns[m];
+            }
+            par ^= qperm<QP_X1>(par);
+            merge_lanes<QP_X1>(m1, m2);
+            if (LPC == 4) {
+                par ^= qperm<QP_X2>(par);
+                merge_lanes<QP_X2>(m1, m2);
+            }
+            // weighted, quantized minima (Main_Functions.py:266-316): bit OB j.. of the table per lane
+            uint32_t qb[OB][2];
+            {
+                const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
+                const uint32_t tab = gtab[c] + (uint32_t)((t & 1) * AL * 4);
+#pragma unroll
+                for (int b = 0; b < OB; ++b) {
+                    uint32_t o[2];
+                    lut_bit<2>(o, mm, tab + (uint32_t)(b * 64));
+                    qb[b][0] = o[0];
+                    qb[b][1] = o[1];
+                }
+            }
+            // the record: lane j writes planes OB j .. of q1 and q2 (the whole group has read the
+            // old record above: same wave, LDS operations in program order)
+#pragma unroll
+            for (int b = 0; b < OB; ++b) {
+                lds_put(grec[c] + 4u * (uint32_t)(OB * cj + b), qb[b][0]);
+                lds_put(grec[c] + 16u + 4u * (uint32_t)(OB * cj + b), qb[b][1]);
+            }
+            // per edge: the C->V sign (par ^ own V->C sign, :251-254) and [|V->C| == min]
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) {
+                if (real(m)) {
+                    const uint32_t sa = sbase + m * sstride;
+                    const uint32_t(&X)[4] = Xs[m];
+                    uint32_t ne = X[0] ^ m1[0];
+#pragma unroll
+                    for (int i = 1; i < 4; ++i) ne = B3(T_ORXOR, ne, X[i], m1[i]);
+                    lds_put(sa, par ^ ns[m]);
+                    lds_put(sa + a.off_a, ~ne);
+                }
+            }
+        }
+        __syncthreads();
+        // ======== variable nodes ================================================================
+        const uint32_t bslice = a.off_blut + (uint32_t)(nx * BL * 4);
+        if (t == a.T - 1) vn_phase(false, true, bslice, t + 1);
+        else vn_phase(false, false, bslice, t + 1);
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const uint32_t wl = RED[0] & valid;
+        const uint32_t all = RED[1] & RED[0] & valid;
+        const uint32_t ap = RED[2] & valid;
+        if (a.counters) {
+            unsigned long long* cc = reinterpret_cast<unsigned long long*>(a.counters);
+            const unsigned long long c0 = RED[3], c1 = __popc(wl), c2 = __popc(all),
+                                     c3 = 2ull * __popc(ap) + __popc(wl & ~ap);
+            if (c0) atomicAdd(cc + 0, c0);
+            if (c1) atomicAdd(cc + 1, c1);
+            if (c2) atomicAdd(cc + 2, c2);
+            if (c3) atomicAdd(cc + 3, c3);
+        }
+        RED[5] = all;
+        RED[6] = wl;
+    }
+    if (a.flags) {
+        __syncthreads();
+        if (tid < nvalid)
+            a.flags[b0 + tid] = (uint8_t)(((RED[5] >> tid) & 1) | (((RED[6] >> tid) & 1) << 1));
+    }
+}
+
+}  // namespace bs
+}  // namespace ldpc
+
+// ---- host: planning, graph tables, launch -------------------------------------------------
+namespace ldpc {
+namespace bs {
+
+std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* nslot);
+std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap);
+int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, float cu,
+                   bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s);
+
+constexpr int kBscNInst = sizeof(kBscInst) / sizeof(kBscInst[0]);
+constexpr int BSC_NW = 16;
+constexpr int BSC_TAG = 100;     // ws.bs_graph_inst of the bsc tables: BSC_TAG + instance
+
+struct BscPlan {
+    bool ok = false;
+    int inst = -1, cn_lanes = 0, arows = 1, bcols = 1, cn_dmin = 0;
+    float cu = -1.f;
+    size_t nslot = 0;
+    uint32_t off_a = 0, off_rec = 0, off_tv = 0, off_red = 0, off_alut = 0, off_blut = 0;
+    size_t lds = 0;
+    std::vector<int32_t> lay;
+    std::vector<int> vorder, vslot;      // variables by degree; chunk of each (wave, u) place
+};
+
+static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip) {
+    BscPlan p;
+    const char* e = getenv("LDPC_BS");
+    if (e && atoi(e) == 0) return p;
+    if (mode != MODE_Q5 && mode != MODE_QM5) return p;
+    if (ucn || per_edge_w || !g.host || !g.w_beta_nonneg) return p;
+    const host::GraphTables& h = *g.host;
+    int min_cdeg = 1 << 30;
+    for (int i = 0; i < h.M; ++i) min_cdeg = std::min(min_cdeg, h.row_ptr[i + 1] - h.row_ptr[i]);
+    if (min_cdeg < 2) return p;
+    const int nv = g.n_vars, nc = g.n_checks, z = h.z;
+    for (int i = 0; i < kBscNInst; ++i) {
+        const BscInst& k = kBscInst[i];
+        if (h.max_cdeg > k.D || h.max_vdeg > k.DVH) continue;
+        BscPlan q;
+        q.inst = i;
+        q.cn_lanes = 64 * ((k.LPC * nc + 63) / 64);
+        const int vch = (nv + 63) / 64, cch = q.cn_lanes / 64;
+        if (vch > k.VPL * BSC_NW || cch > k.CPL * BSC_NW) continue;
+        if (nv > 65535 || nc >= 65535) continue;
+        // variables by descending degree in 64-chunks, dealt to (wave, u) places (the first
+        // chunk of each wave, u = 0, takes the heaviest: only there may a degree exceed DVL)
+        q.vorder.resize(nv);
+        for (int v = 0; v < nv; ++v) q.vorder[v] = v;
+        auto vdeg = [&](int v) { const int j = v / z; return h.col_ptr[j + 1] - h.col_ptr[j]; };
+        std::stable_sort(q.vorder.begin(), q.vorder.end(), [&](int x, int y) { return vdeg(x) > vdeg(y); });
+        std::vector<int> cost(vch);
+        for (int ch = 0; ch < vch; ++ch) cost[ch] = 3 + vdeg(q.vorder[64 * ch]);
+        q.vslot = deal_chunks(cost, BSC_NW, k.VPL);
+        bool fits = true;
+        for (int w = 0; w < BSC_NW; ++w)
+            for (int u = 1; u < k.VPL; ++u) {
+                const int ch = q.vslot[(size_t)w * k.VPL + u];
+                if (ch >= 0 && vdeg(q.vorder[64 * ch]) > k.DVL) fits = false;
+            }
+        if (!fits) continue;
+        q.arows = g.w_alpha_uniform ? 1 : h.M;
+        q.bcols = g.w_beta_uniform ? 1 : h.N;
+        q.cn_dmin = (q.cn_lanes == k.LPC * nc) ? min_cdeg : 0;
+        const float cu = clip / ((mode == MODE_Q5) ? 0.5f : 1.0f);
+        q.cu = cu > (float)QMAX ? cu : -1.f;
+        q.lay = slot_layout(h, k.LPC, &q.nslot);
+        // LDS: SGN [nslot + 1] | ARG [nslot + 1] | REC [nc + 1][8] | TV [nv][6] | RED | ALUT | BLUT
+        const size_t sgn = ((q.nslot + 1) * 4 + 127) & ~(size_t)127;
+        if (q.nslot + 1 > 65535) continue;
+        q.off_a = (uint32_t)sgn;
+        size_t o = 2 * sgn;
+        q.off_rec = (uint32_t)o;
+        o += (size_t)(nc + 1) * 32;
+        q.off_tv = (uint32_t)o;
+        o += (size_t)nv * 24;
+        o = (o + 15) & ~(size_t)15;
+        q.off_red = (uint32_t)o;
+        o += 64;
+        q.off_alut = (uint32_t)o;
+        o += (size_t)2 * q.arows * LUT_W * 4;
+        q.off_blut = (uint32_t)o;
+        o += (size_t)2 * q.bcols * BLUT_W * 4;
+        q.lds = (o + 15) & ~(size_t)15;
+        if (q.lds > BS_LDS_MAX) continue;
+        q.ok = true;
+        return q;
+    }
+    return p;
+}
+
+static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, hipStream_t s) {
+    if (ws.bs_graph && ws.bs_graph_inst == BSC_TAG + p.inst) return LDPC_OK;
+    if (ws.bs_graph) {
+        (void)hipFree(ws.bs_graph);
+        ws.bs_graph = nullptr;
+    }
+    const host::GraphTables& h = *g.host;
+    const BscInst& k = kBscInst[p.inst];
+    const int nv = g.n_vars, nc = g.n_checks, z = h.z, LPC = k.LPC;
+    const int VNW = k.DVH + 1, EPL = (k.D + LPC - 1) / LPC, CVW = (EPL + 1) / 2;
+    const int nl = 64 * BSC_NW;
+    auto slot_of = [&](int i, int kk, int hc) {
+        return (uint32_t)((size_t)p.lay[2 * i] + (size_t)(kk % LPC) * p.lay[2 * i + 1] + (size_t)(kk / LPC) * z + hc);
+    };
+    const uint32_t pad_word = (uint32_t)p.nslot | ((uint32_t)nc << 16);    // zero slot, zero record
+    std::vector<uint32_t> vn((size_t)k.VPL * nl * VNW, 0u);
+    std::vector<int32_t> wdeg((size_t)2 * k.VPL * BSC_NW, 0);
+    for (int u = 0; u < k.VPL; ++u)
+        for (int l = 0; l < nl; ++l) {
+            uint32_t* q = &vn[((size_t)u * nl + l) * VNW];
+            for (int f = 0; f < k.DVH; ++f) q[f] = pad_word;
+            q[k.DVH] = 0xFFFFFFFFu;
+        }
+    for (int w = 0; w < BSC_NW; ++w)
+        for (int u = 0; u < k.VPL; ++u) {
+            const int ch = p.vslot[(size_t)w * k.VPL + u];
+            int dmax = 0, dmin = ch < 0 ? 0 : 1 << 30;
+            for (int l = 0; ch >= 0 && l < 64; ++l) {
+                const int o = 64 * ch + l;
+                if (o >= nv) { dmin = 0; continue; }
+                uint32_t* q = &vn[((size_t)u * nl + 64 * w + l) * VNW];
+                const int v = p.vorder[o], j = v / z, hh = v - j * z;
+                const int c0 = h.col_ptr[j], dv = h.col_ptr[j + 1] - c0;
+                for (int f = 0; f < dv; ++f) {
+                    const int pe = h.col_pe[c0 + f], i = h.pe_row[pe];
+                    int hc = hh - h.pe_shift[pe];
+                    hc = hc < 0 ? hc + z : hc;
+                    q[f] = slot_of(i, pe - h.row_ptr[i], hc) | ((uint32_t)(i * z + hc) << 16);
+                }
+                q[k.DVH] = (uint32_t)v;
+                dmax = std::max(dmax, dv);
+                dmin = std::min(dmin, dv);
+            }
+            wdeg[2 * ((size_t)u * BSC_NW + w)] = dmax;
+            wdeg[2 * ((size_t)u * BSC_NW + w) + 1] = dmin;
+        }
+    const int cch = p.cn_lanes / 64;
+    std::vector<int32_t> cchunk((size_t)BSC_NW * k.CPL, -1);
+    {
+        const std::vector<int> cs = deal_chunks(std::vector<int>(cch, 1), BSC_NW, k.CPL);
+        for (size_t x = 0; x < cs.size(); ++x) cchunk[x] = cs[x];
+    }
+    std::vector<uint32_t> cvar((size_t)p.cn_lanes * CVW, 0u);
+    for (int ql = 0; ql < p.cn_lanes; ++ql) {
+        const int cc = ql / LPC, cj = ql % LPC;
+        if (cc >= nc) continue;
+        const int i = cc / z, hc = cc - i * z;
+        for (int m = 0; m < EPL; ++m) {
+            const int kk = LPC * m + cj;
+            if (kk >= h.row_ptr[i + 1] - h.row_ptr[i]) continue;
+            const int pe = h.row_ptr[i] + kk;
+            const uint32_t v = (uint32_t)(h.pe_col[pe] * z + (hc + h.pe_shift[pe]) % z);
+            cvar[(size_t)ql * CVW + (m >> 1)] |= v << (16 * (m & 1));
+        }
+    }
+    const size_t nwords = vn.size() + wdeg.size() + p.lay.size() + cchunk.size() + cvar.size();
+    void* d = nullptr;
+    if (hipMalloc(&d, nwords * 4) != hipSuccess) { (void)hipGetLastError(); return LDPC_ERR_OOM; }
+    uint32_t* dp = reinterpret_cast<uint32_t*>(d);
+    size_t at = 0;
+    bool ok = true;
+    auto up = [&](const void* src, size_t n) {
+        if (n) ok = ok && hipMemcpyAsync(dp + at, src, n * 4, hipMemcpyHostToDevice, s) == hipSuccess;
+        at += n;
+    };
+    up(vn.data(), vn.size());
+    up(wdeg.data(), wdeg.size());
+    up(p.lay.data(), p.lay.size());
+    up(cchunk.data(), cchunk.size());
+    up(cvar.data(), cvar.size());
+    if (!ok || hipStreamSynchronize(s) != hipSuccess) {
+        (void)hipFree(d);
+        return LDPC_ERR_HIP;
+    }
+    ws.bs_graph = d;
+    ws.bs_graph_inst = BSC_TAG + p.inst;
+    return LDPC_OK;
+}
+
+template <int I>
+static int bsc_launch(const BscArgs& a, int nblocks, size_t lds, hipStream_t s) {
+    constexpr BscInst k = kBscInst[I];
+    auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE>;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)BS_LDS_MAX);
+        attr = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(nblocks), dim3(64 * BSC_NW), lds, s, a);
+    return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+}
+
+}  // namespace bs
+
+using namespace bs;
+
+bool bsc_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip) {
+    return bsc_plan(g, mode, ucn, per_edge_w, clip).ok;
+}
+
+const char* bsc_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip) {
+    static thread_local char buf[64];
+    const BscPlan p = bsc_plan(g, mode, ucn, per_edge_w, clip);
+    if (!p.ok) return "";
+    const BscInst& k = kBscInst[p.inst];
+    snprintf(buf, sizeof(buf), "bsc[p32,w%d,d%d,v%d/%d,l%d,x%d/%d]", BSC_NW, k.D, k.DVH, k.DVL, k.LPC,
+             k.VPL, k.CPL);
+    return buf;
+}
+
+int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
+               bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s) {
+    const BscPlan p = bsc_plan(g, mode, ucn, false, b.clip);
+    if (!p.ok) return LDPC_ERR_UNSUPPORTED;
+    int st = bsc_tables(g, p, ws, s);
+    if (st != LDPC_OK) return st;
+    const BscInst& k = kBscInst[p.inst];
+    const float step = (mode == MODE_Q5) ? 0.5f : 1.0f;
+    uint32_t *alut = nullptr, *blut = nullptr;
+    st = bs_make_tables(b, g, p.arows, p.arows, p.bcols, step, p.cu, false, ws, &alut, &blut, s);
+    if (st != LDPC_OK) return st;
+    const uint32_t* gt = reinterpret_cast<const uint32_t*>(ws.bs_graph);
+    const int VNW = k.DVH + 1;
+    BscArgs a{};
+    a.llr = llr;
+    a.B = b.B;
+    a.n_vars = g.n_vars;
+    a.n_checks = g.n_checks;
+    a.T = b.T;
+    a.target_bits = b.target_bits;
+    a.cn_dmin = p.cn_dmin;
+    a.z = g.z;
+    a.inv = 1.0f / step;
+    a.cu = p.cu;
+    a.beta_id = g.w_beta_one ? 1 : 0;
+    a.row_ptr = g.row_ptr;
+    a.vn_tab = gt;
+    const size_t nvt = (size_t)k.VPL * 64 * BSC_NW * VNW;
+    a.vn_wdeg = reinterpret_cast<const int32_t*>(gt + nvt);
+    a.row_lay = a.vn_wdeg + 2 * (size_t)k.VPL * BSC_NW;
+    a.cn_chunk = a.row_lay + 2 * (size_t)g.M;
+    a.cn_var = reinterpret_cast<const uint32_t*>(a.cn_chunk + (size_t)BSC_NW * k.CPL);
+    a.alut = alut;
+    a.blut = blut;
+    a.arows = p.arows;
+    a.bcols = p.bcols;
+    a.counters = counters;
+    a.flags = flags;
+    a.bad = bad;
+    a.off_a = p.off_a;
+    a.off_rec = p.off_rec;
+    a.off_tv = p.off_tv;
+    a.off_red = p.off_red;
+    a.off_alut = p.off_alut;
+    a.off_blut = p.off_blut;
+    const int nblocks = (int)((b.B + PACK - 1) / PACK);
+    switch (p.inst) {
+        default: return bsc_launch<0>(a, nblocks, p.lds, s);
+    }
+}
+
+}  // namespace ldpc

@@ -43,6 +43,11 @@ bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float 
 const char* bs_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip);
 int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
               bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s);
+// compressed bit-sliced kernel (ldpc_bsc.hip): the graphs whose per-edge slots exceed the LDS
+bool bsc_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip);
+const char* bsc_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip);
+int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
+               bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s);
 void fused_free(FusedWorkspace& ws);
 
 // float-mode fused decoder (ldpc_ffl.hip): MS, MS without nudge, QMS q = 6; counters / flags

@@ -97,6 +97,7 @@ int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const f
     w.alpha_uniform = (!w.per_edge_w && !alpha_ucn) ? 1 : 0;
     w.beta_uniform = 1;
     w.beta_nonneg = 1;
+    w.beta_one = 1;
     for (int t = 0; t < T; ++t) {
         const float a0 = alpha[(size_t)t * g.E], b0 = beta[(size_t)t * g.N];
         for (int e = 1; e < g.E && w.alpha_uniform; ++e)
@@ -105,6 +106,7 @@ int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const f
             const float b = beta[(size_t)t * g.N + j];
             if (b != b0) w.beta_uniform = 0;
             if (!(b >= 0.f)) w.beta_nonneg = 0;
+            if (b != 1.f) w.beta_one = 0;
         }
     }
     return LDPC_OK;

@@ -66,10 +66,11 @@ int build_graph(const int32_t* proto, int32_t M, int32_t N, int32_t z, GraphTabl
 // row weights, the previous row's weights at every t).
 // alpha_uniform = one CN weight for every edge at each t (sharing type 3, no UCN weights);
 // beta_uniform = one VN weight for every column at each t; beta_nonneg = no beta below 0
-// (the bit-sliced kernel takes the sign of Q(beta ch) from the channel).
+// (the bit-sliced kernel takes the sign of Q(beta ch) from the channel); beta_one = every beta
+// is 1 (flat weights: Q(beta ch) = Q(ch)).
 struct WeightInfo {
     int per_edge_w = 0;
-    int alpha_uniform = 0, beta_uniform = 0, beta_nonneg = 0;
+    int alpha_uniform = 0, beta_uniform = 0, beta_nonneg = 0, beta_one = 0;
     std::vector<int32_t> row_merge;
 };
 int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const float* alpha_ucn,

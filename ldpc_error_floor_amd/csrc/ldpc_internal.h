@@ -29,7 +29,7 @@ struct DevGraph {
     const int32_t* row_merge;
     const host::GraphTables* host;   // host tables (ldpc_host.h)
     // weight properties of the current weights (host::WeightInfo, set by ldpc_weights_set)
-    int w_alpha_uniform, w_beta_uniform, w_beta_nonneg;
+    int w_alpha_uniform, w_beta_uniform, w_beta_nonneg, w_beta_one;
 };
 
 // Per-decode buffers and scalars.

@@ -60,7 +60,8 @@ static void check_tables(const std::vector<int32_t>& P, int M, int N, int z, con
     for (int k = 0; k < E; ++k) {
         const int32_t* q = g.device_block.data() + g.off_vn + 4 * (size_t)k;
         const int pe = g.col_pe[k], i = g.pe_row[pe], r0 = g.row_ptr[i];
-        CHECK(q[0] == r0 * z + (pe - r0) && q[1] == g.row_ptr[i + 1] - r0 && q[2] == g.pe_shift[pe] && q[3] == 0);
+        CHECK(q[0] == r0 * z + (pe - r0) && q[1] == g.row_ptr[i + 1] - r0 && q[2] == g.pe_shift[pe] &&
+              q[3] == (((i * z) << 6) | (pe - r0)));
     }
 }
 

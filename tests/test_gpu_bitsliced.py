@@ -123,3 +123,41 @@ def test_bitsliced_ucn_off_grid_fixup(cuda_device, lpc):
     out = _both(dec, llr)
     assert np.array_equal(out["fused"][0], out["flood"][0])
     assert np.array_equal(out["fused"][1], out["flood"][1])
+
+
+# ---- the compressed bit-sliced kernel (csrc/ldpc_bsc.hip): 5G BG1 (C5: flat [3,0,3], T=50,
+# puncture 1-144, shortening 1537-1584), whose per-edge slots do not fit the LDS --------------
+@pytest.mark.parametrize("T,B,snr", [(50, 3001, 2.0), (12, 40000, 1.75), (50, 33, 2.5)])
+def test_bitsliced_compressed_bg1(cuda_device, T, B, snr, monkeypatch):
+    dec, cp, c = _config(cuda_device, "C5", T)
+    name = dec.kernel_info()[1]
+    assert name.startswith("bsc["), name
+    llr = dec.awgn(B, float(cp.sigma(snr)), seed=21, offset=3)
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0]), (out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
+    if B > 1000:
+        assert 0 < out["fused"][0][1] < B
+    monkeypatch.setenv("LDPC_BS_FIXUP", "0")       # shortened bits decoded in the kernel itself
+    r = dec.decode(llr, app=False, counters=True, flags=True, kernel="fused")
+    assert np.array_equal(r.counters.cpu().numpy(), out["flood"][0])
+
+
+def test_bitsliced_compressed_trained_weights(cuda_device):
+    """Per-row alpha tables and a trained per-iteration beta (not the flat identity beta) on BG1
+    (per-column beta tables do not fit its LDS beside the compressed state: v5 serves those)."""
+    import bench
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    from ldpc_error_floor_amd.weights import expand_weights
+    proto, g, _, cp = bench.load_problem(T=10, config="C5")
+    rng = np.random.RandomState(4)
+    W = expand_weights((2, 0, 3), {0: rng.uniform(0.5, 1.0, (10, g.M)),
+                                   2: rng.uniform(0.7, 1.3, (10, 1))}, 10, g)
+    dec = NMSDecoder(proto, 72, W, 2, 5, device=cuda_device)
+    dec.punct, dec.short = (1, 144), (1537, 1584)
+    assert dec.kernel_info()[1].startswith("bsc["), dec.kernel_info()
+    llr = dec.awgn(2000, float(cp.sigma(2.0)), seed=8)
+    llr[5, 17] += 0.1                              # one pack off the grid (v5 fixup)
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
