@@ -1,5 +1,5 @@
 """Correctness at the benchmark's batch size (GPU only): B = 2^20 codewords in one launch for
-C2 (wman, T=20) and C5 (5G BG1 n2112, T=50: B * n_vars = 2.4e9 > 2^31, so every index into the
+C2 (wman, T=20, bit-sliced bsl kernel) and C5 (5G BG1 n2112, T=50, compressed bsc kernel: B * n_vars = 2.4e9 > 2^31, so every index into the
 LLR block must be 64-bit).  The fused and flood kernels (both parity-pinned on the reference
 fixtures) must agree frame by frame, and the first and last codewords of the batch, decoded on
 their own, must match the oracle and the big launch's per-frame flags."""
@@ -27,8 +27,8 @@ def test_full_batch_kernels_agree_and_match_oracle(cuda_device, config, lpc, mon
     snr = {"C2": 2.5, "C5": 2.5}[config]
     sigma = float(cp.sigma(snr))
     dec = NMSDecoder(proto, z, W, 2, 5, device=cuda_device, B_max=B)
-    # counters-only decodes: the bit-sliced kernel where it applies (C2), else fused v5
-    assert dec.kernel_info(T)[1].startswith(("bsl[", "fused5[")), dec.kernel_info(T)
+    # counters-only decodes: the bit-sliced kernels (bsl for C2, the compressed bsc for C5)
+    assert dec.kernel_info(T)[1].startswith({"C2": "bsl[", "C5": "bsc["}[config]), dec.kernel_info(T)
     llr = dec.awgn(B, sigma, seed=31, punct=punct, short=short)
     res = {}
     for k in ("fused", "flood"):
