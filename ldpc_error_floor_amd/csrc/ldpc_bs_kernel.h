@@ -635,9 +635,13 @@ k_bs(BsArgs a) {
         asm volatile("" : "+s"(cn_dmin));
         // next iteration's tables (their slots were last read two phases ago)
         if (t + 1 < a.T) {
-            for (int w = tid; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
+            // (the lane index made opaque per iteration: the copy addresses are recomputed here
+            // rather than hoisted out of the T loop into registers the loop body spills)
+            int tl = tid;
+            asm volatile("" : "+v"(tl));
+            for (int w = tl; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
             if (a.bcols > 1)
-                for (int w = tid; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
+                for (int w = tl; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
         }
         // ======== check nodes ===================================================================
 #pragma unroll

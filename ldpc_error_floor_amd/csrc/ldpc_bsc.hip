@@ -27,9 +27,11 @@ namespace bs {
 
 // instances: D = check-degree bound, DVH / DVL = variable-degree bound of a lane's first /
 // other variables, LPC lanes per check, VPL variables and CPL check chunks per lane
+// (a wman-sized instance — one variable and one check chunk per lane, 64 VGPRs — was measured
+// against bsl on C2: 61 spills, and the BG1 instance there ran 68 M cw/s against bsl's 176 M)
 struct BscInst { int D, DVH, DVL, LPC, VPL, CPL; int WPE; };
 constexpr BscInst kBscInst[] = {
-    {20, 10, 5, 4, 3, 3, 4},          // 5G BG1 (C5): degree 19 rows, degree 10 / 8 columns
+    {20, 10, 5, 4, 3, 3, 4},          // 5G BG1 (C5): degree 19 rows, degree 10 / 8 columns, 16 waves
 };
 
 struct BscArgs {
@@ -274,6 +276,7 @@ k_bsc(BscArgs a) {
         const int cc = ql / LPC;
         const int ci = min(cc / a.z, a.n_checks / a.z - 1);
         gdeg[c] = (cc < a.n_checks) ? a.row_ptr[ci + 1] - a.row_ptr[ci] : 0;
+        (void)nwv;
         gslot[c] = (uint32_t)(4 * (a.row_lay[2 * ci] + cj * a.row_lay[2 * ci + 1] + (cc - ci * a.z)));
         grec[c] = a.off_rec + 32u * (uint32_t)min(cc, a.n_checks - 1);
         gtab[c] = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * OB * 64);
@@ -294,9 +297,13 @@ k_bsc(BscArgs a) {
         for (int u = 0; u < VPL; ++u) asm volatile("" : "+s"(dw[u]));
         asm volatile("" : "+s"(cn_dmin));
         if (t + 1 < a.T) {
-            for (int w = tid; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
+            // (the lane index made opaque per iteration: the copy addresses are recomputed here
+            // rather than hoisted out of the T loop into registers the loop body spills)
+            int tl = tid;
+            asm volatile("" : "+v"(tl));
+            for (int w = tl; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
             if (a.bcols > 1)
-                for (int w = tid; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
+                for (int w = tl; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
         }
         // ======== check nodes ===================================================================
 #pragma unroll
@@ -445,7 +452,7 @@ constexpr int BSC_TAG = 100;     // ws.bs_graph_inst of the bsc tables: BSC_TAG 
 
 struct BscPlan {
     bool ok = false;
-    int inst = -1, cn_lanes = 0, arows = 1, bcols = 1, cn_dmin = 0;
+    int inst = -1, nw = BSC_NW, cn_lanes = 0, arows = 1, bcols = 1, cn_dmin = 0;
     float cu = -1.f;
     size_t nslot = 0;
     uint32_t off_a = 0, off_rec = 0, off_tv = 0, off_red = 0, off_alut = 0, off_blut = 0;
@@ -472,7 +479,8 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
         q.inst = i;
         q.cn_lanes = 64 * ((k.LPC * nc + 63) / 64);
         const int vch = (nv + 63) / 64, cch = q.cn_lanes / 64;
-        if (vch > k.VPL * BSC_NW || cch > k.CPL * BSC_NW) continue;
+        if (k.VPL == 1 && k.CPL == 1) q.nw = std::max(vch, cch);
+        if (q.nw > 16 || vch > k.VPL * q.nw || cch > k.CPL * q.nw) continue;
         if (nv > 65535 || nc >= 65535) continue;
         // variables by descending degree in 64-chunks, dealt to (wave, u) places (the first
         // chunk of each wave, u = 0, takes the heaviest: only there may a degree exceed DVL)
@@ -482,9 +490,9 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
         std::stable_sort(q.vorder.begin(), q.vorder.end(), [&](int x, int y) { return vdeg(x) > vdeg(y); });
         std::vector<int> cost(vch);
         for (int ch = 0; ch < vch; ++ch) cost[ch] = 3 + vdeg(q.vorder[64 * ch]);
-        q.vslot = deal_chunks(cost, BSC_NW, k.VPL);
+        q.vslot = deal_chunks(cost, q.nw, k.VPL);
         bool fits = true;
-        for (int w = 0; w < BSC_NW; ++w)
+        for (int w = 0; w < q.nw; ++w)
             for (int u = 1; u < k.VPL; ++u) {
                 const int ch = q.vslot[(size_t)w * k.VPL + u];
                 if (ch >= 0 && vdeg(q.vorder[64 * ch]) > k.DVL) fits = false;
@@ -530,20 +538,20 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     const BscInst& k = kBscInst[p.inst];
     const int nv = g.n_vars, nc = g.n_checks, z = h.z, LPC = k.LPC;
     const int VNW = k.DVH + 1, EPL = (k.D + LPC - 1) / LPC, CVW = (EPL + 1) / 2;
-    const int nl = 64 * BSC_NW;
+    const int NWp = p.nw, nl = 64 * NWp;
     auto slot_of = [&](int i, int kk, int hc) {
         return (uint32_t)((size_t)p.lay[2 * i] + (size_t)(kk % LPC) * p.lay[2 * i + 1] + (size_t)(kk / LPC) * z + hc);
     };
     const uint32_t pad_word = (uint32_t)p.nslot | ((uint32_t)nc << 16);    // zero slot, zero record
     std::vector<uint32_t> vn((size_t)k.VPL * nl * VNW, 0u);
-    std::vector<int32_t> wdeg((size_t)2 * k.VPL * BSC_NW, 0);
+    std::vector<int32_t> wdeg((size_t)2 * k.VPL * NWp, 0);
     for (int u = 0; u < k.VPL; ++u)
         for (int l = 0; l < nl; ++l) {
             uint32_t* q = &vn[((size_t)u * nl + l) * VNW];
             for (int f = 0; f < k.DVH; ++f) q[f] = pad_word;
             q[k.DVH] = 0xFFFFFFFFu;
         }
-    for (int w = 0; w < BSC_NW; ++w)
+    for (int w = 0; w < NWp; ++w)
         for (int u = 0; u < k.VPL; ++u) {
             const int ch = p.vslot[(size_t)w * k.VPL + u];
             int dmax = 0, dmin = ch < 0 ? 0 : 1 << 30;
@@ -563,13 +571,15 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
                 dmax = std::max(dmax, dv);
                 dmin = std::min(dmin, dv);
             }
-            wdeg[2 * ((size_t)u * BSC_NW + w)] = dmax;
-            wdeg[2 * ((size_t)u * BSC_NW + w) + 1] = dmin;
+            wdeg[2 * ((size_t)u * NWp + w)] = dmax;
+            wdeg[2 * ((size_t)u * NWp + w) + 1] = dmin;
         }
     const int cch = p.cn_lanes / 64;
-    std::vector<int32_t> cchunk((size_t)BSC_NW * k.CPL, -1);
-    {
-        const std::vector<int> cs = deal_chunks(std::vector<int>(cch, 1), BSC_NW, k.CPL);
+    std::vector<int32_t> cchunk((size_t)NWp * k.CPL, -1);
+    if (k.CPL == 1 && k.VPL == 1) {
+        for (int w = 0; w < NWp; ++w) cchunk[w] = w < cch ? w : -1;
+    } else {
+        const std::vector<int> cs = deal_chunks(std::vector<int>(cch, 1), NWp, k.CPL);
         for (size_t x = 0; x < cs.size(); ++x) cchunk[x] = cs[x];
     }
     std::vector<uint32_t> cvar((size_t)p.cn_lanes * CVW, 0u);
@@ -610,7 +620,7 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
 }
 
 template <int I>
-static int bsc_launch(const BscArgs& a, int nblocks, size_t lds, hipStream_t s) {
+static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     constexpr BscInst k = kBscInst[I];
     auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE>;
     static bool attr = false;
@@ -619,7 +629,7 @@ static int bsc_launch(const BscArgs& a, int nblocks, size_t lds, hipStream_t s) 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)BS_LDS_MAX);
         attr = true;
     }
-    hipLaunchKernelGGL(fn, dim3(nblocks), dim3(64 * BSC_NW), lds, s, a);
+    hipLaunchKernelGGL(fn, dim3(nblocks), dim3(64 * nw), lds, s, a);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 
@@ -636,7 +646,7 @@ const char* bsc_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge
     const BscPlan p = bsc_plan(g, mode, ucn, per_edge_w, clip);
     if (!p.ok) return "";
     const BscInst& k = kBscInst[p.inst];
-    snprintf(buf, sizeof(buf), "bsc[p32,w%d,d%d,v%d/%d,l%d,x%d/%d]", BSC_NW, k.D, k.DVH, k.DVL, k.LPC,
+    snprintf(buf, sizeof(buf), "bsc[p32,w%d,d%d,v%d/%d,l%d,x%d/%d]", p.nw, k.D, k.DVH, k.DVL, k.LPC,
              k.VPL, k.CPL);
     return buf;
 }
@@ -668,11 +678,11 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     a.beta_id = g.w_beta_one ? 1 : 0;
     a.row_ptr = g.row_ptr;
     a.vn_tab = gt;
-    const size_t nvt = (size_t)k.VPL * 64 * BSC_NW * VNW;
+    const size_t nvt = (size_t)k.VPL * 64 * p.nw * VNW;
     a.vn_wdeg = reinterpret_cast<const int32_t*>(gt + nvt);
-    a.row_lay = a.vn_wdeg + 2 * (size_t)k.VPL * BSC_NW;
+    a.row_lay = a.vn_wdeg + 2 * (size_t)k.VPL * p.nw;
     a.cn_chunk = a.row_lay + 2 * (size_t)g.M;
-    a.cn_var = reinterpret_cast<const uint32_t*>(a.cn_chunk + (size_t)BSC_NW * k.CPL);
+    a.cn_var = reinterpret_cast<const uint32_t*>(a.cn_chunk + (size_t)p.nw * k.CPL);
     a.alut = alut;
     a.blut = blut;
     a.arows = p.arows;
@@ -688,7 +698,7 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     a.off_blut = p.off_blut;
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
     switch (p.inst) {
-        default: return bsc_launch<0>(a, nblocks, p.lds, s);
+        default: return bsc_launch<0>(a, nblocks, p.nw, p.lds, s);
     }
 }
 
