@@ -97,6 +97,18 @@ static void validation_cases() {
     CHECK(host::analyze_weights(g, INT32_MAX, a.data(), nullptr, b.data(), wi) == LDPC_ERR_ARG);
     CHECK(host::analyze_weights(g, 3, a.data(), nullptr, b.data(), wi) == LDPC_OK);
     CHECK(wi.per_edge_w == 0 && (int)wi.row_merge.size() == g.M);
+    CHECK(wi.beta_one == 1 && wi.beta_id_mask == 7u);          // beta = 1: identity tables
+    // identity iff min(15, rint(15 beta)) == 15 and rint(m beta) == m below: 0.98 is (15 * 0.98
+    // = 14.7), 0.96 is not (rint(14.4) = 14), 1.04 is not (rint(12 * 1.04 = 12.48) = 12 but
+    // rint(13 * 1.04 = 13.52) = 14); one column off spoils the iteration
+    for (int j = 0; j < g.N; ++j) {
+        b[(size_t)0 * g.N + j] = 0.98f;
+        b[(size_t)1 * g.N + j] = 0.96f;
+        b[(size_t)2 * g.N + j] = j == 0 ? 1.04f : 1.0f;
+    }
+    CHECK(host::analyze_weights(g, 3, a.data(), nullptr, b.data(), wi) == LDPC_OK);
+    CHECK(wi.beta_one == 0 && wi.beta_id_mask == 1u);
+    std::fill(b.begin(), b.end(), 1.0f);
 
     // decode parameters
     ldpc_decode_params p{};
