@@ -409,6 +409,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.inv = 1.0f / step;
     a.cu = p.cu > 0.f ? p.cu : -1.f;
     a.ucn = p.ucn ? 1 : 0;
+    a.beta_id = (mode == MODE_Q5 || mode == MODE_QM5) ? g.w_beta_id_mask : 0;
     a.row_ptr = g.row_ptr;
     a.z = g.z;
     a.vn_tab = gt;

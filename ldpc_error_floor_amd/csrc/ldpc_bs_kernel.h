@@ -67,6 +67,7 @@ struct BsArgs {
     float inv;
     float cu;                    // |LLR| / step of a shortened bit (BIG instances), > QMAX
     int ucn;                     // UCN weights present (UCN instances)
+    uint64_t beta_id;            // bit t: iteration t's channel table is the identity (skipped)
     const int32_t* row_ptr;      // [M + 1] proto edges of each row (the check degrees)
     const int32_t* row_lay;      // [M][2] slot layout of each proto row: first slot, j-block stride
     int z;
@@ -238,14 +239,22 @@ __device__ __forceinline__ void lut(uint32_t (&o)[NI][4], const uint32_t (&in)[N
 // costs no LDS traffic; a leaf is a v_and + v_xor with SGPR operands (the 2-cycle VOP2 forms,
 // one SGPR per instruction) in place of one v_bitop3 — the same issue cycles
 typedef __attribute__((address_space(4))) const uint32_t ConstW;
+// (m & X) ^ Y with X, Y in SGPRs as two VOP2 instructions: left to itself the compiler fuses
+// them into a v_bitop3 (VOP3), which may read only one SGPR, and adds a v_mov of the other
+__device__ __forceinline__ uint32_t leaf_s(uint32_t m, uint32_t X, uint32_t Y) {
+    uint32_t t, l;
+    asm("v_and_b32 %0, %1, %2" : "=v"(t) : "s"(X), "v"(m));
+    asm("v_xor_b32 %0, %1, %2" : "=v"(l) : "s"(Y), "v"(t));
+    return l;
+}
 __device__ __forceinline__ void lut_s(uint32_t (&o)[4], const uint32_t (&a)[4], const ConstW* tab) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         uint32_t g[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t l0 = (a[0] & tab[j * 16 + 4 * q]) ^ tab[j * 16 + 4 * q + 1];
-            const uint32_t l1 = (a[0] & tab[j * 16 + 4 * q + 2]) ^ tab[j * 16 + 4 * q + 3];
+            const uint32_t l0 = leaf_s(a[0], tab[j * 16 + 4 * q], tab[j * 16 + 4 * q + 1]);
+            const uint32_t l1 = leaf_s(a[0], tab[j * 16 + 4 * q + 2], tab[j * 16 + 4 * q + 3]);
             g[q] = mux(a[1], l1, l0);
         }
         o[j] = mux(a[3], mux(a[2], g[3], g[2]), mux(a[2], g[1], g[0]));
@@ -461,7 +470,7 @@ k_bs(BsArgs a) {
             const bool counted = v >= 0 && v < a.target_bits;
             uint32_t lw[1][4];                   // |Q(beta_{t+1} ch)| (before the C->V: fewer live registers)
             if (!last) {
-                if (ABL(2)) {
+                if (ABL(2) || ((a.beta_id >> tb) & 1)) {   // identity table: |Q(beta ch)| = |ch|
 #pragma unroll
                     for (int i = 0; i < 4; ++i) lw[0][i] = cm[u][i];
                 } else if (a.bcols == 1) {          // one beta per iteration: table in SGPRs

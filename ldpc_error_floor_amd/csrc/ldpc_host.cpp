@@ -98,6 +98,17 @@ int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const f
     w.beta_uniform = 1;
     w.beta_nonneg = 1;
     w.beta_one = 1;
+    for (int t = 0; t < T && t < 64; ++t) {
+        bool id = true;
+        for (int j = 0; j < g.N && id; ++j) {
+            const float b = beta[(size_t)t * g.N + j];
+            for (int m = 0; m <= 15 && id; ++m) {
+                const float q = std::nearbyint((float)m * b);     // round half to even, fp32 product
+                id = std::min(15.f, std::fabs(q)) == (float)m && !(b < 0.f);
+            }
+        }
+        if (id) w.beta_id_mask |= (uint64_t)1 << t;
+    }
     for (int t = 0; t < T; ++t) {
         const float a0 = alpha[(size_t)t * g.E], b0 = beta[(size_t)t * g.N];
         for (int e = 1; e < g.E && w.alpha_uniform; ++e)

@@ -30,6 +30,7 @@ struct DevGraph {
     const host::GraphTables* host;   // host tables (ldpc_host.h)
     // weight properties of the current weights (host::WeightInfo, set by ldpc_weights_set)
     int w_alpha_uniform, w_beta_uniform, w_beta_nonneg, w_beta_one;
+    uint64_t w_beta_id_mask;     // iterations whose q5 channel table is the identity
 };
 
 // Per-decode buffers and scalars.
