@@ -8,18 +8,36 @@
 
 namespace ldpc {
 
+// one (codeword, element pair) per thread, grid-strided.  The index -> (codeword, pair) split is
+// a 32-bit division whenever the batch has fewer than 2^32 pairs (a 64-bit one is a long
+// emulated sequence), and an even row length stores the pair as one 8-byte write.
+template <bool WIDE>
 __global__ void __launch_bounds__(256) k_awgn(float* __restrict__ out, int64_t B, int n_vars,
-                                              AwgnParams a) {
+                                              AwgnParams a, int pairs8) {
     const int npairs = (n_vars + 1) / 2;
     const int64_t total = B * npairs;
+    const bool even = pairs8 != 0;
     for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
          id += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t b = id / npairs;
-        const int pr = (int)(id - b * npairs);
+        int64_t b;
+        int pr;
+        if (WIDE) {
+            b = id / npairs;
+            pr = (int)(id - b * npairs);
+        } else {
+            const uint32_t q = (uint32_t)id / (uint32_t)npairs;
+            b = q;
+            pr = (int)((uint32_t)id - q * (uint32_t)npairs);
+        }
         float l[2];
         awgn_pair(a, b, pr, l);
-        out[b * n_vars + 2 * pr] = l[0];
-        if (2 * pr + 1 < n_vars) out[b * n_vars + 2 * pr + 1] = l[1];
+        float* row = out + b * n_vars;
+        if (even) {
+            *reinterpret_cast<float2*>(row + 2 * pr) = make_float2(l[0], l[1]);
+        } else {
+            row[2 * pr] = l[0];
+            if (2 * pr + 1 < n_vars) row[2 * pr + 1] = l[1];
+        }
     }
 }
 
@@ -58,7 +76,12 @@ extern "C" int ldpc_channel_awgn(float* llr_dev, int64_t B, int32_t n_vars, doub
     const ldpc::AwgnParams a = ldpc::make_awgn(sigma, seed, offset, decoding_type, q_bit,
                                                punct_start, punct_end, short_start, short_end,
                                                clip_llr);
-    hipLaunchKernelGGL(ldpc::k_awgn, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                       llr_dev, B, (int)n_vars, a);
+    // 8-byte pair stores: even rows in an 8-byte aligned buffer
+    const int pairs8 = ((n_vars & 1) == 0 && (reinterpret_cast<uintptr_t>(llr_dev) & 7) == 0) ? 1 : 0;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (total + (int64_t)grid * 256 < ((int64_t)1 << 32))
+        hipLaunchKernelGGL(ldpc::k_awgn<false>, dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a, pairs8);
+    else
+        hipLaunchKernelGGL(ldpc::k_awgn<true>, dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a, pairs8);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
