@@ -65,7 +65,12 @@ __device__ __forceinline__ float awgn_quant(float x, int q_bit) {
     }
 }
 
-// LLRs of elements 2*pr and 2*pr+1 of codeword `b` (batch-relative) into l[0], l[1]
+// LLRs of elements 2*pr and 2*pr+1 of codeword `b` (batch-relative) into l[0], l[1].
+// QB: the quantizer, fixed at compile time (0 = none, i.e. a float mode; else the q_bit), or
+// AWGN_QRT to take decoding_type / q_bit from `a` at run time (the runtime switch compiles to
+// all five quantizers and selects)
+constexpr int AWGN_QRT = 99;
+template <int QB = AWGN_QRT>
 __device__ __forceinline__ void awgn_pair(const AwgnParams& a, int64_t b, int pr, float (&l)[2]) {
     const uint64_t gcw = (uint64_t)(a.offset + b);
     uint32_t c[4] = {(uint32_t)pr, (uint32_t)gcw, (uint32_t)(gcw >> 32), 0x4C445043u};
@@ -81,7 +86,11 @@ __device__ __forceinline__ void awgn_pair(const AwgnParams& a, int64_t b, int pr
     for (int h = 0; h < 2; ++h) {
         const int bit = 2 * pr + h + 1;                                  // 1-based like the reference
         float llr = (nz[h] * a.sigma - 1.0f) * a.inv;
-        if (a.decoding_type == LDPC_DEC_QMS) llr = awgn_quant(llr, a.q_bit);
+        if constexpr (QB == AWGN_QRT) {
+            if (a.decoding_type == LDPC_DEC_QMS) llr = awgn_quant(llr, a.q_bit);
+        } else if constexpr (QB != 0) {
+            llr = awgn_quant(llr, QB);
+        }
         if (a.ps > 0 && bit >= a.ps && bit <= a.pe) llr = (a.decoding_type == 0) ? 0.001f : 0.0f;
         if (a.ss > 0 && bit >= a.ss && bit <= a.se) llr = -a.clip;
         l[h] = llr;

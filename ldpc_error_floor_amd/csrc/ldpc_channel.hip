@@ -2,6 +2,7 @@
 // The generator itself (model, Philox stream, precision) is ldpc_awgn.h, shared with the
 // fused decoder's in-prologue channel.
 #include <algorithm>
+#include <type_traits>
 
 #include "ldpc_awgn.h"
 #include "ldpc_internal.h"
@@ -11,7 +12,7 @@ namespace ldpc {
 // one (codeword, element pair) per thread, grid-strided.  The index -> (codeword, pair) split is
 // a 32-bit division whenever the batch has fewer than 2^32 pairs (a 64-bit one is a long
 // emulated sequence), and an even row length stores the pair as one 8-byte write.
-template <bool WIDE>
+template <bool WIDE, int QB>
 __global__ void __launch_bounds__(256) k_awgn(float* __restrict__ out, int64_t B, int n_vars,
                                               AwgnParams a, int pairs8) {
     const int npairs = (n_vars + 1) / 2;
@@ -30,7 +31,7 @@ __global__ void __launch_bounds__(256) k_awgn(float* __restrict__ out, int64_t B
             pr = (int)((uint32_t)id - q * (uint32_t)npairs);
         }
         float l[2];
-        awgn_pair(a, b, pr, l);
+        awgn_pair<QB>(a, b, pr, l);
         float* row = out + b * n_vars;
         if (even) {
             *reinterpret_cast<float2*>(row + 2 * pr) = make_float2(l[0], l[1]);
@@ -79,9 +80,20 @@ extern "C" int ldpc_channel_awgn(float* llr_dev, int64_t B, int32_t n_vars, doub
     // 8-byte pair stores: even rows in an 8-byte aligned buffer
     const int pairs8 = ((n_vars & 1) == 0 && (reinterpret_cast<uintptr_t>(llr_dev) & 7) == 0) ? 1 : 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (total + (int64_t)grid * 256 < ((int64_t)1 << 32))
-        hipLaunchKernelGGL(ldpc::k_awgn<false>, dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a, pairs8);
-    else
-        hipLaunchKernelGGL(ldpc::k_awgn<true>, dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a, pairs8);
+    const bool wide = total + (int64_t)grid * 256 >= ((int64_t)1 << 32);
+    const int qb = decoding_type == LDPC_DEC_QMS ? q_bit : 0;
+    auto go = [&](auto qc) {
+        constexpr int Q = decltype(qc)::value;
+        if (wide) hipLaunchKernelGGL((ldpc::k_awgn<true, Q>), dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a, pairs8);
+        else hipLaunchKernelGGL((ldpc::k_awgn<false, Q>), dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a, pairs8);
+    };
+    switch (qb) {       // one build per quantizer (check_channel has validated q_bit)
+        case 6: go(std::integral_constant<int, 6>{}); break;
+        case 5: go(std::integral_constant<int, 5>{}); break;
+        case -5: go(std::integral_constant<int, -5>{}); break;
+        case 4: go(std::integral_constant<int, 4>{}); break;
+        case 3: go(std::integral_constant<int, 3>{}); break;
+        default: go(std::integral_constant<int, 0>{}); break;
+    }
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }

@@ -71,3 +71,19 @@ def test_ffl_decode_awgn_matches_channel_then_decode(cuda_device):
     b = dec.decode(llr, app=False, counters=True, flags=True, kernel="flood")
     assert np.array_equal(a.counters.cpu().numpy(), b.counters.cpu().numpy())
     assert np.array_equal(a.flags.cpu().numpy(), b.flags.cpu().numpy())
+
+
+def test_ffl_refuses_per_edge_weights(cuda_device):
+    """Per-edge CN weights (sharing 1) have no compressed record: AUTO decodes them with flood."""
+    import bench
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    from ldpc_error_floor_amd.weights import expand_weights
+    proto, g, _, cp = bench.load_problem(T=8, config="C2")
+    rng = np.random.RandomState(2)
+    W = expand_weights((1, 0, 3), {0: rng.uniform(0.5, 1.0, (8, g.E)), 2: np.ones((8, 1))}, 8, g)
+    dec = NMSDecoder(proto, 24, W, 1, 5, device=cuda_device)
+    assert dec.kernel_info()[1] == "flood", dec.kernel_info()
+    llr = dec.awgn(500, float(cp.sigma(2.0)), seed=4)
+    a = dec.decode(llr, app=False, counters=True)
+    b = dec.decode(llr, app=False, counters=True, kernel="flood")
+    assert np.array_equal(a.counters.cpu().numpy(), b.counters.cpu().numpy())

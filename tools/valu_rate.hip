@@ -66,6 +66,19 @@ __global__ void __launch_bounds__(256) k_mix(uint32_t* out, uint32_t seed, unsig
                 asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
             } else if (MIX == 17) {    // DPP row_shr (VOP2 + DPP word)
                 asm volatile("v_add_u32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 18) {    // 32 x 32 -> 64 multiply-add (Philox round product)
+                uint64_t x = ((uint64_t)b[j] << 32) | a[j];
+                uint64_t cy;
+                asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(x), "=s"(cy) : "v"(b[j]), "v"(c[j]));
+                a[j] = (uint32_t)x ^ (uint32_t)(x >> 32);
+            } else if (MIX == 19) {    // v_mul_hi_u32
+                asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 20) {    // v_mul_lo_u32
+                asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 21) {    // v_bitop3_b32 (VOP3, any 3-input boolean function)
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+            } else if (MIX == 22) {    // v_log_f32 (transcendental)
+                asm volatile("v_log_f32 %0, %0" : "+v"(a[j]));
             }
         }
     }
@@ -128,6 +141,11 @@ int main() {
         run<15>("v_cndmask_b32 vcc", 1, w, ncu, clk, d);
         run<16>("v_add3_u32", 1, w, ncu, clk, d);
         run<17>("v_add_u32_dpp", 1, w, ncu, clk, d);
+        run<18>("v_mad_u64_u32 (+1 xor)", 2, w, ncu, clk, d);
+        run<19>("v_mul_hi_u32", 1, w, ncu, clk, d);
+        run<20>("v_mul_lo_u32", 1, w, ncu, clk, d);
+        run<21>("v_bitop3_b32", 1, w, ncu, clk, d);
+        run<22>("v_log_f32", 1, w, ncu, clk, d);
     }
     hipFree(d);
     return 0;
