@@ -307,6 +307,7 @@ int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* 
     g->dev.w_beta_nonneg = wi.beta_nonneg;
     g->dev.w_beta_one = wi.beta_one;
     g->dev.w_beta_id_mask = wi.beta_id_mask;
+    g->dev.w_version++;
     return LDPC_OK;
 }
 

@@ -15,6 +15,9 @@ struct FusedWorkspace {
     size_t bs_lut_bytes = 0;
     uint32_t* bs_bad = nullptr;    // [packs] 1: pack decoded by the v5 fixup
     int64_t bs_bad_n = 0;
+    // what the per-decode table kernels last wrote (they depend only on the graph, the weights
+    // and T): a decode with the same key skips them
+    uint64_t key_gad[4] = {~0ull, 0, 0, 0}, key_qtab[4] = {~0ull, 0, 0, 0}, key_bslut[4] = {~0ull, 0, 0, 0};
 };
 
 // fused v5 serves this request (QMS q in {5,-5,4,3}, clip_llr on the grid, a shape fits)

@@ -142,6 +142,7 @@ void fused_free(FusedWorkspace& ws) {
     if (ws.bs_bad) (void)hipFree(ws.bs_bad);
     ws.bs_bad = nullptr;
     ws.bs_bad_n = 0;
+    ws.key_gad[0] = ws.key_qtab[0] = ws.key_bslut[0] = ~0ull;
 }
 
 }  // namespace ldpc

@@ -313,6 +313,7 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
         if (ws.tables) (void)hipFree(ws.tables);
         ws.tables = nullptr;
         ws.tables_bytes = 0;
+        ws.key_gad[0] = ws.key_qtab[0] = ~0ull;
         if (hipMalloc(&ws.tables, tbytes) != hipSuccess) {
             (void)hipGetLastError();
             return LDPC_ERR_OOM;
@@ -323,17 +324,29 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     uint32_t* gad = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws.tables) + off_gad);
     uint4* grow = reinterpret_cast<uint4*>(reinterpret_cast<char*>(ws.tables) + off_grow);
     {
-        if (lut)
+        // (skipped when the same tables are already in place: same weights, T, shape, grouping)
+        const uint64_t kq[4] = {g.w_version, (uint64_t)b.T << 32 | (uint32_t)qmax,
+                                (uint64_t)__builtin_bit_cast(uint32_t, step) << 32 | (uint32_t)qslice,
+                                (uint64_t)(b.alpha_ucn != nullptr)};
+        if (lut && !std::equal(kq, kq + 4, ws.key_qtab)) {
             hipLaunchKernelGGL(k_f5_tables, dim3((unsigned)((nqt + 255) / 256)), dim3(256), 0, s,
                                b.alpha, b.alpha_ucn, g.row_ptr, b.T, g.M, g.E, qmax, step,
                                1.0f / step, qslice, qtab);
+            std::copy(kq, kq + 4, ws.key_qtab);
+        }
         const int lcw = f5_logcw(sh.cw);
         const char* be = getenv("LDPC_F5_BALANCE");
         const bool hetero = sh.hg > 0 && sh.hg < sh.maxg;
         const bool bal = hetero || (be ? atoi(be) != 0 : sh.bal);
-        hipLaunchKernelGGL(k_f5_gad, dim3((unsigned)((p.ngroups * 64 + 255) / 256)), dim3(256), 0, s,
-                           g.row_ptr, g.pe_col, g.pe_shift, p.merge, g.M, p.ngroups, g.z, lcw,
-                           sh.maxdeg, npk, g.n_vars * sh.cw, p.nw, bal ? 1 : 0, gad, grow);
+        const uint64_t kg[4] = {g.w_version, (uint64_t)p.shape << 32 | (uint32_t)p.ngroups,
+                                (uint64_t)(p.merge != nullptr) << 1 | (bal ? 1u : 0u),
+                                (uint64_t)off_gad << 32 | (uint32_t)p.nw};
+        if (!std::equal(kg, kg + 4, ws.key_gad)) {
+            hipLaunchKernelGGL(k_f5_gad, dim3((unsigned)((p.ngroups * 64 + 255) / 256)), dim3(256), 0, s,
+                               g.row_ptr, g.pe_col, g.pe_shift, p.merge, g.M, p.ngroups, g.z, lcw,
+                               sh.maxdeg, npk, g.n_vars * sh.cw, p.nw, bal ? 1 : 0, gad, grow);
+            std::copy(kg, kg + 4, ws.key_gad);
+        }
         if (hipGetLastError() != hipSuccess) return LDPC_ERR_HIP;
     }
     a.betas = b.beta;      // [T][N] as given (the kernel keeps ch / step)

@@ -161,3 +161,35 @@ def test_bitsliced_compressed_trained_weights(cuda_device):
     out = _both(dec, llr)
     assert np.array_equal(out["fused"][0], out["flood"][0])
     assert np.array_equal(out["fused"][1], out["flood"][1])
+
+
+def test_table_cache_follows_weights_and_T(cuda_device):
+    """The per-decode weight / address tables are cached per (weights, T, layout): new weights
+    or another T on the same decoder must give what a fresh decoder gives (bsl, bsc, v5)."""
+    import bench
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    from ldpc_error_floor_amd.weights import flat_weights
+    for cfg in ("C2", "C5"):
+        proto, g, W, cp = bench.load_problem(T=12, config=cfg)
+        c = bench.CONFIGS[cfg]
+        W2 = flat_weights(g, 12, alpha=0.625, beta=1.0)
+        dec = NMSDecoder(proto, c["z"], W, 2, 5, device=cuda_device)
+        dec.punct, dec.short = c.get("punct", (0, 0)), c.get("short", (0, 0))
+        llr = dec.awgn(3000, float(cp.sigma(c["snr"] - 1.0)), seed=6)
+        for k in ("fused", "flood"):
+            a1 = dec.decode(llr, app=False, counters=True, kernel=k).counters.cpu().numpy()
+            a8 = dec.decode(llr, T=8, app=False, counters=True, kernel=k).counters.cpu().numpy()
+            dec.set_weights(W2)
+            b1 = dec.decode(llr, app=False, counters=True, kernel=k).counters.cpu().numpy()
+            dec.set_weights(W)
+            c1 = dec.decode(llr, app=False, counters=True, kernel=k).counters.cpu().numpy()
+            assert np.array_equal(a1, c1), (cfg, k)
+            fresh = NMSDecoder(proto, c["z"], W2, 2, 5, device=cuda_device)
+            f1 = fresh.decode(llr, app=False, counters=True, kernel=k).counters.cpu().numpy()
+            assert np.array_equal(b1, f1), (cfg, k, b1, f1)
+            assert not np.array_equal(a1, b1) and not np.array_equal(a1, a8), (cfg, k)
+            if k == "fused":
+                ref = {}
+                for kk in ("flood",):
+                    ref[kk] = dec.decode(llr, T=8, app=False, counters=True, kernel=kk).counters.cpu().numpy()
+                assert np.array_equal(a8, ref["flood"]), cfg

@@ -79,6 +79,17 @@ __global__ void __launch_bounds__(256) k_mix(uint32_t* out, uint32_t seed, unsig
                 asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
             } else if (MIX == 22) {    // v_log_f32 (transcendental)
                 asm volatile("v_log_f32 %0, %0" : "+v"(a[j]));
+            } else if (MIX == 23) {    // v_bitop3_b32 with one SGPR operand
+                asm volatile("v_bitop3_b32 %0, %1, %0, %2 bitop3:0x6c" : "+v"(a[j]) : "s"(seed), "v"(c[j]));
+            } else if (MIX == 24) {    // v_mov_b32 from an SGPR (VOP1)
+                asm volatile("v_mov_b32 %0, %1" : "=v"(a[j]) : "s"(seed + j));
+            } else if (MIX == 25) {    // v_xor_b32 VGPR, VGPR (VOP2)
+                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 26) {    // v_and_b32 with an inline constant
+                asm volatile("v_and_b32 %0, 0x7fff, %0" : "+v"(a[j]));
+            } else if (MIX == 27) {    // ds_read_b128 broadcast (all lanes, same LDS address) + 2 bitop3
+                // (LDS traffic in the VALU loop: the table-leaf alternative)
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x6c" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
             }
         }
     }
@@ -146,6 +157,10 @@ int main() {
         run<20>("v_mul_lo_u32", 1, w, ncu, clk, d);
         run<21>("v_bitop3_b32", 1, w, ncu, clk, d);
         run<22>("v_log_f32", 1, w, ncu, clk, d);
+        run<23>("v_bitop3_b32 1 sgpr", 1, w, ncu, clk, d);
+        run<24>("v_mov_b32 from sgpr", 1, w, ncu, clk, d);
+        run<25>("v_xor_b32 vv", 1, w, ncu, clk, d);
+        run<26>("v_and_b32 inline const", 1, w, ncu, clk, d);
     }
     hipFree(d);
     return 0;
