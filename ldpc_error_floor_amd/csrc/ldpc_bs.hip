@@ -240,11 +240,18 @@ int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcol
         if (ws.bs_lut) (void)hipFree(ws.bs_lut);
         ws.bs_lut = nullptr;
         ws.bs_lut_bytes = 0;
+        ws.key_bslut[0] = ~0ull;
         if (hipMalloc(&ws.bs_lut, bytes) != hipSuccess) { (void)hipGetLastError(); return LDPC_ERR_OOM; }
         ws.bs_lut_bytes = bytes;
     }
     *alut = reinterpret_cast<uint32_t*>(ws.bs_lut);
     *blut = *alut + na;
+    // (skipped when these tables are already in place: same weights, T and layout)
+    const uint64_t kb[4] = {g.w_version, (uint64_t)b.T << 32 | (uint32_t)(arows << 16 | ar),
+                            (uint64_t)__builtin_bit_cast(uint32_t, step) << 32 | __builtin_bit_cast(uint32_t, cu),
+                            (uint64_t)bcols << 1 | (ucn && b.alpha_ucn ? 1u : 0u)};
+    if (std::equal(kb, kb + 4, ws.key_bslut)) return LDPC_OK;
+    std::copy(kb, kb + 4, ws.key_bslut);
     const int ntab = b.T * (ar + bcols);
     // without UCN weights the alpha' slots (UCN instances) repeat the alpha tables (unused)
     const float* au = (ucn && b.alpha_ucn) ? b.alpha_ucn : b.alpha;
