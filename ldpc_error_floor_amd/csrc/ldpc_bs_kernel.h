@@ -239,8 +239,9 @@ __device__ __forceinline__ void lut(uint32_t (&o)[NI][4], const uint32_t (&in)[N
 // costs no LDS traffic; a leaf is a v_and + v_xor with SGPR operands (the 2-cycle VOP2 forms,
 // one SGPR per instruction) in place of one v_bitop3 — the same issue cycles
 typedef __attribute__((address_space(4))) const uint32_t ConstW;
-// (m & X) ^ Y with X, Y in SGPRs as two VOP2 instructions: left to itself the compiler fuses
-// them into a v_bitop3 (VOP3), which may read only one SGPR, and adds a v_mov of the other
+// (m & X) ^ Y with X, Y in SGPRs as two VOP2 instructions (the compiler's own form is a v_mov
+// of one SGPR plus a v_bitop3 reading the other: the same issue cost, every VALU op with an
+// SGPR operand takes ~4.2 cycles against 2.4 for VGPR-only ones; tools/valu_rate.hip)
 __device__ __forceinline__ uint32_t leaf_s(uint32_t m, uint32_t X, uint32_t Y) {
     uint32_t t, l;
     asm("v_and_b32 %0, %1, %2" : "=v"(t) : "s"(X), "v"(m));
