@@ -193,3 +193,20 @@ def test_table_cache_follows_weights_and_T(cuda_device):
                 for kk in ("flood",):
                     ref[kk] = dec.decode(llr, T=8, app=False, counters=True, kernel=kk).counters.cpu().numpy()
                 assert np.array_equal(a8, ref["flood"]), cfg
+
+
+@pytest.mark.parametrize("cfg", ["C3", "C4", "C5"])
+def test_bitsliced_q_minus5_large_graphs(cuda_device, cfg):
+    """q = -5 (grid step 1: shortened bits are +-20 grid units) on the UCN / multi-lane bsl
+    instances and on bsc."""
+    import bench
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    proto, g, W, cp = bench.load_problem(T=10, config=cfg)
+    c = bench.CONFIGS[cfg]
+    dec = NMSDecoder(proto, c["z"], W, 2, -5, device=cuda_device)
+    dec.punct, dec.short = c.get("punct", (0, 0)), c.get("short", (0, 0))
+    assert dec.kernel_info()[1].startswith(("bsl[", "bsc[")), dec.kernel_info()
+    llr = dec.awgn(2500, float(cp.sigma(c["snr"] - 0.5)), seed=12)
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0]), (cfg, out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
