@@ -55,8 +55,9 @@ constexpr BsInst kBsInst[] = {
     {16, 8, 4, 1, 1, false, false, true, 8},
     {15, 6, 2, 1, 1, false, false, true, 8},     // LDPC_BS_LPC=2 A/B
     {24, 4, 4, 1, 1, true, true, true, 6},       // 802.11n (C3): degree 22, UCN
-    {10, 8, 4, 2, 3, true, true, false, 4},      // 5G BG2 (C4): 1,280 variables, 640 checks
-    {10, 8, 2, 2, 2, true, true, false, 4},      // LDPC_BS_LPC=2 A/B
+    {10, 8, 2, 2, 2, true, true, false, 4},      // 5G BG2 (C4): 1,280 variables, 640 checks;
+                                                 // 18.2 ms vs 21.2 for LPC 4 (CPL 3), same box
+    {10, 8, 4, 2, 3, true, true, false, 4},      // LDPC_BS_LPC=4 A/B
 };
 constexpr int kBsNInst = sizeof(kBsInst) / sizeof(kBsInst[0]);
 

@@ -32,6 +32,7 @@ namespace bs {
 struct BscInst { int D, DVH, DVL, LPC, VPL, CPL; int WPE; };
 constexpr BscInst kBscInst[] = {
     {20, 10, 5, 4, 3, 3, 4},          // 5G BG1 (C5): degree 19 rows, degree 10 / 8 columns, 16 waves
+    {20, 10, 5, 2, 3, 2, 4},          // the same with 2 lanes per check (LDPC_BS_LPC A/B)
 };
 
 struct BscArgs {
@@ -384,11 +385,14 @@ k_bsc(BscArgs a) {
                 }
             }
             // the record: lane j writes planes OB j .. of q1 and q2 (the whole group has read the
-            // old record above: same wave, LDS operations in program order)
+            // old record above: same wave, LDS operations in program order); idle lanes past
+            // the last check (degree 0) share its clamped record address and must not write
+            if (cdeg > 0) {
 #pragma unroll
-            for (int b = 0; b < OB; ++b) {
-                lds_put(grec[c] + 4u * (uint32_t)(OB * cj + b), qb[b][0]);
-                lds_put(grec[c] + 16u + 4u * (uint32_t)(OB * cj + b), qb[b][1]);
+                for (int b = 0; b < OB; ++b) {
+                    lds_put(grec[c] + 4u * (uint32_t)(OB * cj + b), qb[b][0]);
+                    lds_put(grec[c] + 16u + 4u * (uint32_t)(OB * cj + b), qb[b][1]);
+                }
             }
             // per edge: the C->V sign (par ^ own V->C sign, :251-254) and [|V->C| == min]
 #pragma unroll
@@ -472,9 +476,12 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
     for (int i = 0; i < h.M; ++i) min_cdeg = std::min(min_cdeg, h.row_ptr[i + 1] - h.row_ptr[i]);
     if (min_cdeg < 2) return p;
     const int nv = g.n_vars, nc = g.n_checks, z = h.z;
+    const char* el = getenv("LDPC_BS_LPC");          // A/B: force 2 or 4 lanes per check
+    const int want_lpc = el ? atoi(el) : 0;
     for (int i = 0; i < kBscNInst; ++i) {
         const BscInst& k = kBscInst[i];
         if (h.max_cdeg > k.D || h.max_vdeg > k.DVH) continue;
+        if (want_lpc != 0 && want_lpc != k.LPC) continue;
         BscPlan q;
         q.inst = i;
         q.cn_lanes = 64 * ((k.LPC * nc + 63) / 64);
@@ -698,6 +705,7 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     a.off_blut = p.off_blut;
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
     switch (p.inst) {
+        case 1: return bsc_launch<1>(a, nblocks, p.nw, p.lds, s);
         default: return bsc_launch<0>(a, nblocks, p.nw, p.lds, s);
     }
 }

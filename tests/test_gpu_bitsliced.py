@@ -210,3 +210,23 @@ def test_bitsliced_q_minus5_large_graphs(cuda_device, cfg):
     out = _both(dec, llr)
     assert np.array_equal(out["fused"][0], out["flood"][0]), (cfg, out["fused"][0], out["flood"][0])
     assert np.array_equal(out["fused"][1], out["flood"][1])
+
+
+@pytest.mark.parametrize("lpc_c", ["4", "2"])
+def test_bitsliced_compressed_idle_check_lanes(cuda_device, lpc_c, monkeypatch):
+    """bsc with a last check chunk that is only partly used (BG1 lifted by z = 60: 600 checks,
+    4 x 600 lanes = 37.5 chunks), where the idle lanes share the last check's record address."""
+    import bench
+    from ldpc_error_floor_amd.code import TannerGraph
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    from ldpc_error_floor_amd.weights import flat_weights
+    monkeypatch.setenv("LDPC_BS_LPC", lpc_c)
+    proto = bench.load_problem(T=10, config="C5")[0]
+    g = TannerGraph(proto, 60)
+    dec = NMSDecoder(proto, 60, flat_weights(g, 10, alpha=0.75, beta=1.0), 2, 5, device=cuda_device)
+    assert dec.kernel_info()[1].startswith("bsc[") and f",l{lpc_c}," in dec.kernel_info()[1], dec.kernel_info()
+    from ldpc_error_floor_amd.code import CodeParams
+    llr = dec.awgn(3000, float(CodeParams(proto, 60).sigma(3.0)), seed=17)
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0]), (out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
