@@ -177,8 +177,8 @@ def main():
     ap.add_argument("--snr", type=float, default=None, help="default: the config's SNR")
     ap.add_argument("--iters", type=int, default=None, help="default: the config's T")
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
-    ap.add_argument("--decoding-type", type=int, default=2, choices=[1, 2, 3],
-                    help="1 MS fp32, 2 QMS (default), 3 MS without the zero nudge")
+    ap.add_argument("--decoding-type", type=int, default=2, choices=[0, 1, 2, 3],
+                    help="0 sum-product, 1 MS fp32, 2 QMS (default), 3 MS without the zero nudge")
     ap.add_argument("--q-bit", type=int, default=5, choices=[6, 5, -5, 4, 3])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--all-kernels", action="store_true",
@@ -342,7 +342,7 @@ def main():
     pdesc = "".join([f", puncture {punct[0]}-{punct[1]}" if punct[0] else "",
                      f", shorten {short[0]}-{short[1]}" if short[0] else ""])
     sh = ",".join(str(x) for x in cfg["sharing"])
-    mdesc = {1: "MS fp32", 3: "MS fp32 (no nudge)"}.get(args.decoding_type, f"QMS q{args.q_bit}")
+    mdesc = {0: "sum-product fp32", 1: "MS fp32", 3: "MS fp32 (no nudge)"}.get(args.decoding_type, f"QMS q{args.q_bit}")
     out = {
         "metric": f"decoded codewords/sec, {cfg['label']}, {T} NMS iters",
         "value": round(value, 1),

@@ -342,6 +342,12 @@ int ldpc_ctx_destroy(ldpc_ctx* c) {
 static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
                        const ldpc_decode_outputs* o, void* stream, const AwgnParams* gen);
 
+// LDPC_KERNEL_AUTO takes the fused kernel when it serves the request, except for sum-product:
+// its check update is bound by the tanh / atanh / divide VALU work, which flood's four codewords
+// per lane amortize better (wman T=20: flood 3.98 M against 3.64 M codewords/s for the fused
+// kernel, one box), so the fused SP kernel runs only when asked for
+static bool auto_fused(int mode) { return mode != MODE_SP; }
+
 int ldpc_decode(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
                 const ldpc_decode_outputs* o, void* stream) {
     if (!llr_dev) return LDPC_ERR_ARG;
@@ -392,7 +398,7 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
     // the float modes' fused kernel (ffl) serves counters-only decodes; it is the one reported
     const bool fl = ffl_mode(mode) && ffl_supported(g->dev, mode, ucn, g->per_edge_w != 0);
     const bool fok = fl || fused_supported(g->dev, mode, p->T, p->clip_llr);
-    if (kern == LDPC_KERNEL_AUTO) kern = fok ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
+    if (kern == LDPC_KERNEL_AUTO) kern = (fok && auto_fused(mode)) ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
     if (kern == LDPC_KERNEL_FUSED && !fok) return LDPC_ERR_UNSUPPORTED;
     if (kern != LDPC_KERNEL_FLOOD && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_ARG;
     const int64_t nv = (int64_t)g->h.N * g->h.z, ne = (int64_t)g->h.E * g->h.z;
@@ -410,7 +416,7 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
         nm = "flood";
     } else {
         bytes = fused_bytes_per_cw(g->dev, p->T);
-        nm = fl ? ffl_kernel_name(g->dev, ucn, g->per_edge_w != 0)
+        nm = fl ? ffl_kernel_name(g->dev, mode, ucn, g->per_edge_w != 0)
                 : fused_kernel_name(g->dev, mode, p->T, p->clip_llr, ucn, g->per_edge_w != 0);
     }
     if (bytes_per_cw) *bytes_per_cw = bytes;
@@ -442,7 +448,7 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     const bool fl = ffl_mode(mode);
     const bool fok = fl ? (!want_bits && !out.app_all && ffl_supported(g->dev, mode, ucn, g->per_edge_w != 0))
                         : fused_supported(g->dev, mode, p->T, p->clip_llr);
-    if (kern == LDPC_KERNEL_AUTO) kern = fok ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
+    if (kern == LDPC_KERNEL_AUTO) kern = (fok && auto_fused(mode)) ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
     if (kern != LDPC_KERNEL_FLOOD && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_ARG;
     if (kern == LDPC_KERNEL_FUSED && !fok) return LDPC_ERR_UNSUPPORTED;
     if (gen && (kern != LDPC_KERNEL_FUSED || fl)) return LDPC_ERR_UNSUPPORTED;   // caller falls back

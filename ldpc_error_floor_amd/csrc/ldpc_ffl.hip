@@ -67,6 +67,33 @@ __device__ __forceinline__ uint32_t fold(uint64_t m) {
     return CW == 32 ? r : (r & ((1u << CW) - 1u));
 }
 
+// frame flags / counters of the block from the LDS reductions (RED[0]: some bit wrong at the
+// last iteration, RED[1]: wrong at every earlier one, RED[2]: some app > 0, RED[3]: bit errors)
+__device__ __forceinline__ void block_finish(const FflArgs& a, uint32_t* RED, int tid, int64_t b0,
+                                             int nvalid, uint32_t valid) {
+    if (tid == 0) {
+        const uint32_t wl = RED[0] & valid;
+        const uint32_t all = RED[1] & RED[0] & valid;
+        const uint32_t ap = RED[2] & valid;
+        if (a.counters) {
+            unsigned long long* cc = reinterpret_cast<unsigned long long*>(a.counters);
+            const unsigned long long c0 = RED[3], c1 = __popc(wl), c2 = __popc(all),
+                                     c3 = 2ull * __popc(ap) + __popc(wl & ~ap);
+            if (c0) atomicAdd(cc + 0, c0);
+            if (c1) atomicAdd(cc + 1, c1);
+            if (c2) atomicAdd(cc + 2, c2);
+            if (c3) atomicAdd(cc + 3, c3);
+        }
+        RED[5] = all;
+        RED[6] = wl;
+    }
+    if (a.flags) {
+        __syncthreads();
+        if (tid < nvalid)
+            a.flags[b0 + tid] = (uint8_t)(((RED[5] >> tid) & 1) | (((RED[6] >> tid) & 1) << 1));
+    }
+}
+
 template <int MODE, int CW, bool UCN>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(8)))
 k_ffl(FflArgs a) {
@@ -262,27 +289,178 @@ k_ffl(FflArgs a) {
         }
         __syncthreads();
     }
-    if (tid == 0) {
-        const uint32_t wl = RED[0] & valid;
-        const uint32_t all = RED[1] & RED[0] & valid;
-        const uint32_t ap = RED[2] & valid;
-        if (a.counters) {
-            unsigned long long* cc = reinterpret_cast<unsigned long long*>(a.counters);
-            const unsigned long long c0 = RED[3], c1 = __popc(wl), c2 = __popc(all),
-                                     c3 = 2ull * __popc(ap) + __popc(wl & ~ap);
-            if (c0) atomicAdd(cc + 0, c0);
-            if (c1) atomicAdd(cc + 1, c1);
-            if (c2) atomicAdd(cc + 2, c2);
-            if (c3) atomicAdd(cc + 3, c3);
+    block_finish(a, RED, tid, b0, nvalid, valid);
+}
+
+// ---- sum-product (decoding_type 0): flood's cn_update_sp / k_vn_update on LDS ---------------
+// The sum-product messages do not compress (every edge's C->V differs), so the state is flood's
+// own: C2V[(pe z + h)][w] per edge (proto edge pe in row order, check h of the row: a wave's
+// consecutive checks are consecutive words) and TV[v][w]; pass 1 parks t_k = tanh(-x_k/2) in
+// the edge's slot after reading the old message there, pass 2 overwrites it with the new one.
+// LDS per codeword: 4 (N z + E z) [+ 4 N z] bytes.  Per-edge weights are read as flood reads them.
+template <int CW, bool UCN>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(8)))
+k_ffs(FflArgs a) {
+    constexpr int G = 64 / CW;
+    constexpr float SP_EPS = 1.0f - 1e-7f;               // as flood (Main_Functions.py:243)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* TV = reinterpret_cast<float*>(smem + a.off_tv);
+    float* C2V = reinterpret_cast<float*>(smem + a.off_rec);
+    uint32_t* HD = reinterpret_cast<uint32_t*>(smem + a.off_hd);
+    uint32_t* RED = reinterpret_cast<uint32_t*>(smem + a.off_red);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = uni(tid >> 6);
+    const int g = lane / CW, w = lane % CW;
+    const int z = a.z, hq = a.hq, nv = a.n_vars;
+    const int64_t b0 = (int64_t)blockIdx.x * CW;
+    const int nvalid = (int)min<int64_t>(CW, a.B - b0);
+    const bool wvalid = w < nvalid;
+    const uint32_t valid = (nvalid >= 32) ? 0xFFFFFFFFu : ((1u << nvalid) - 1u);
+    const int nvt = a.N * hq, nct = a.M * hq;
+
+    float ch[KVMAX];
+#pragma unroll
+    for (int kk = 0; kk < KVMAX; ++kk) {
+        ch[kk] = 0.f;
+        const int q = wave + kk * NW;
+        if (q < nvt) {
+            const int j = q / hq, h = (q - j * hq) * G + g;
+            if (h < z && wvalid) ch[kk] = a.llr[(b0 + w) * nv + j * z + h];
         }
-        RED[5] = all;
-        RED[6] = wl;
     }
-    if (a.flags) {
+#pragma unroll
+    for (int kk = 0; kk < KVMAX; ++kk) {
+        const int q = wave + kk * NW;
+        if (q < nvt) {
+            const int j = q / hq, h = (q - j * hq) * G + g;
+            if (h < z) {
+                const int v = j * z + h;
+                const float lw = ch[kk] * a.beta[j];
+                TV[v * CW + w] = lw;
+                if (UCN) HD[v * CW + w] = lw >= 0.f ? 1u : 0u;
+            }
+        }
+    }
+    if (tid < 8) RED[tid] = (tid == 1) ? 0xFFFFFFFFu : 0u;
+    __syncthreads();
+
+    for (int t = 0; t < a.T; ++t) {
+        if (tid == 0 && t > 0) {
+            RED[1] &= RED[0];
+            RED[0] = 0u;
+        }
+        // ======== check nodes (flood's cn_update_sp) =========================================
+        for (int q = wave; q < nct; q += NW) {
+            const int i = uni(q / hq);
+            const int h = (q - i * hq) * G + g;
+            const bool act = h < z;
+            const int hh = act ? h : z - 1;
+            const int r0 = a.row_ptr[i], deg = a.row_ptr[i + 1] - r0;
+            float P = 1.f, L = 0.f;
+            uint32_t syn = 0u;
+            for (int k0 = 0; k0 < deg; k0 += 4) {
+                float tv[4], cv[4];
+                uint32_t hdv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (k0 + u < deg) {
+                        const int pe = r0 + k0 + u;
+                        const int s = hh + a.pe_shift[pe];
+                        const int v = a.pe_col[pe] * z + (s >= z ? s - z : s);
+                        tv[u] = TV[v * CW + w];
+                        cv[u] = (t > 0) ? C2V[(pe * z + hh) * CW + w] : 0.f;
+                        if (UCN) hdv[u] = HD[v * CW + w];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (k0 + u < deg) {
+                        const float x = fminf(fmaxf(tv[u] - cv[u], -a.clip), a.clip);      // :227
+                        float y = tanhf(-0.5f * x);
+                        y = (fabsf(y) > 0.f) ? y : 1.f;                                   // :240
+                        P *= y;
+                        L += logf(fabsf(y));
+                        if (act) C2V[((r0 + k0 + u) * z + hh) * CW + w] = y;
+                        if (UCN) syn ^= hdv[u];
+                    }
+                }
+            }
+            const float* at = a.alpha + (size_t)t * a.E + r0;
+            const float* au = UCN ? a.alpha_ucn + (size_t)t * a.E + r0 : nullptr;
+            const bool big = fabsf(P) >= 1.17549435e-38f;
+            for (int k = 0; k < deg; ++k) {
+                const int slot = ((r0 + k) * z + hh) * CW + w;
+                const float y = act ? C2V[slot] : 1.f;
+                float others;
+                if (big) {
+                    others = P / y;
+                } else {                                   // product underflowed: log domain
+                    const bool neg = (P < 0.f) != (y < 0.f);
+                    const float m = expf(L - logf(fabsf(y)));
+                    others = neg ? -m : m;
+                }
+                others = fminf(fmaxf(others, -SP_EPS), SP_EPS);                         // :243
+                const float o = -2.0f * atanhf(others);                                // :244
+                const float wt = (UCN && (syn & 1u)) ? au[k] : at[k];
+                float x = fabsf(o) * wt;
+                x = (x > 0.f) ? x : 0.f;                                               // :308
+                x = fminf(fmaxf(x, -a.clip), a.clip);                                  // :313
+                if (act) C2V[slot] = (o > 0.f) ? x : ((o < 0.f) ? -x : 0.f);           // :316
+            }
+        }
         __syncthreads();
-        if (tid < nvalid)
-            a.flags[b0 + tid] = (uint8_t)(((RED[5] >> tid) & 1) | (((RED[6] >> tid) & 1) << 1));
+        // ======== variable nodes (flood's k_vn_update) ========================================
+        const bool last = (t == a.T - 1);
+        uint32_t wr = 0u, apos = 0u, nb = 0u;
+#pragma unroll
+        for (int kk = 0; kk < KVMAX; ++kk) {
+            const int q = wave + kk * NW;
+            if (q >= nvt) continue;
+            const int j = uni(q / hq);
+            const int h = (q - j * hq) * G + g;
+            const bool act = h < z;
+            const int hh = act ? h : z - 1;
+            const int e0 = a.col_ptr[j], e1 = a.col_ptr[j + 1];
+            float S = 0.f;
+            for (int e = e0; e < e1; e += 4) {
+                float cv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (e + u < e1) {
+                        const int pe = a.col_pe[e + u];
+                        int hc = hh - a.pe_shift[pe];
+                        hc = hc < 0 ? hc + z : hc;
+                        cv[u] = C2V[(pe * z + hc) * CW + w];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (e + u < e1) S += cv[u];
+            }
+            const int v = j * z + hh;
+            const float app = fminf(fmaxf(ch[kk] + S, -a.clip), a.clip);
+            const bool counted = act && wvalid && v < a.target_bits;
+            const bool hd = app >= 0.f;
+            wr |= fold<CW>(__ballot(counted && hd));
+            if (last) {
+                apos |= fold<CW>(__ballot(counted && app > 0.f));
+                nb += (uint32_t)__popcll(__ballot(counted && hd));
+            } else if (act) {
+                const float beta = a.beta[(size_t)(t + 1) * a.N + j];
+                TV[v * CW + w] = ch[kk] * beta + S;
+                if (UCN) HD[v * CW + w] = hd ? 1u : 0u;
+            }
+        }
+        if (lane == 0) {
+            if (wr) atomicOr(&RED[0], wr);
+            if (last) {
+                if (apos) atomicOr(&RED[2], apos);
+                if (nb) atomicAdd(&RED[3], nb);
+            }
+        }
+        __syncthreads();
     }
+    block_finish(a, RED, tid, b0, nvalid, valid);
 }
 
 struct FflPlan {
@@ -292,14 +470,20 @@ struct FflPlan {
     size_t lds = 0;
 };
 
-static FflPlan plan(const DevGraph& g, bool ucn, bool per_edge_w) {
+// min-sum modes: CW 16 (else 4) with the compressed records, one weight per row; sum-product:
+// CW 8 (else 4, 2) with per-edge messages, any weights
+static FflPlan plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
     FflPlan p;
     const char* e = getenv("LDPC_FFL");
     if (e && atoi(e) == 0) return p;
-    if (per_edge_w || !g.host || g.max_cdeg > 32) return p;
+    const bool sp = (mode == MODE_SP);
+    if (!g.host || (!sp && (per_edge_w || g.max_cdeg > 32))) return p;
     const host::GraphTables& h = *g.host;
-    const int cws[2] = {16, 4};
-    for (int cw : cws) {
+    // (sum-product: CW 8 first — no idle check lanes when 8 | z; 3.64 M against 3.34 M cw/s at
+    // CW 4 on wman, one box)
+    const int cws_ms[3] = {16, 4, 0}, cws_sp[3] = {8, 4, 2};
+    for (int cw : sp ? cws_sp : cws_ms) {
+        if (cw == 0) break;
         const int G = 64 / cw;
         const int hq = (h.z + G - 1) / G;
         if ((h.N * hq + NW - 1) / NW > KVMAX) continue;
@@ -307,7 +491,7 @@ static FflPlan plan(const DevGraph& g, bool ucn, bool per_edge_w) {
         p.off_tv = 0;
         o += (size_t)g.n_vars * cw * 4;
         p.off_rec = (uint32_t)o;
-        o += (size_t)4 * g.n_checks * cw * 4;
+        o += sp ? (size_t)g.n_edges * cw * 4 : (size_t)4 * g.n_checks * cw * 4;
         p.off_hd = (uint32_t)o;
         if (ucn) o += (size_t)g.n_vars * cw * 4;
         p.off_red = (uint32_t)o;
@@ -320,6 +504,18 @@ static FflPlan plan(const DevGraph& g, bool ucn, bool per_edge_w) {
         return p;
     }
     return FflPlan{};
+}
+
+template <int CW, bool UCN>
+static int launch_sp(const FflArgs& a, int nblocks, size_t lds, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ffs<CW, UCN>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_ffs<CW, UCN>), dim3(nblocks), dim3(64 * NW), lds, s, a);
+    return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 
 template <int MODE, int CW, bool UCN>
@@ -342,22 +538,25 @@ static int launch_mode(const FflArgs& a, int cw, bool ucn, int nblocks, size_t l
 
 }  // namespace ffl
 
-bool ffl_mode(int mode) { return mode == MODE_MS || mode == MODE_MSNN || mode == MODE_Q6; }
-
-bool ffl_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
-    return ffl_mode(mode) && ffl::plan(g, ucn, per_edge_w).ok;
+bool ffl_mode(int mode) {
+    return mode == MODE_MS || mode == MODE_MSNN || mode == MODE_Q6 || mode == MODE_SP;
 }
 
-const char* ffl_kernel_name(const DevGraph& g, bool ucn, bool per_edge_w) {
+bool ffl_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
+    return ffl_mode(mode) && ffl::plan(g, mode, ucn, per_edge_w).ok;
+}
+
+const char* ffl_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w) {
     static thread_local char buf[48];
-    const ffl::FflPlan p = ffl::plan(g, ucn, per_edge_w);
-    snprintf(buf, sizeof(buf), "ffl[cw%d,w%d%s]", p.cw, ffl::NW, ucn ? ",ucn" : "");
+    const ffl::FflPlan p = ffl::plan(g, mode, ucn, per_edge_w);
+    snprintf(buf, sizeof(buf), "ffl[%scw%d,w%d%s]", mode == MODE_SP ? "sp," : "", p.cw, ffl::NW,
+             ucn ? ",ucn" : "");
     return buf;
 }
 
 int ffl_decode(const DevGraph& g, const Bufs& b, const float* llr, int mode, bool ucn, bool per_edge_w,
                int64_t* counters, uint8_t* flags, hipStream_t s) {
-    const ffl::FflPlan p = ffl::plan(g, ucn, per_edge_w);
+    const ffl::FflPlan p = ffl::plan(g, mode, ucn, per_edge_w);
     if (!p.ok || !ffl_mode(mode)) return LDPC_ERR_UNSUPPORTED;
     ffl::FflArgs a{};
     a.llr = llr;
@@ -392,6 +591,10 @@ int ffl_decode(const DevGraph& g, const Bufs& b, const float* llr, int mode, boo
     switch (mode) {
         case MODE_MS: return ffl::launch_mode<MODE_MS>(a, p.cw, ucn, nblocks, p.lds, s);
         case MODE_MSNN: return ffl::launch_mode<MODE_MSNN>(a, p.cw, ucn, nblocks, p.lds, s);
+        case MODE_SP:
+            if (p.cw == 8) return ucn ? ffl::launch_sp<8, true>(a, nblocks, p.lds, s) : ffl::launch_sp<8, false>(a, nblocks, p.lds, s);
+            if (p.cw == 4) return ucn ? ffl::launch_sp<4, true>(a, nblocks, p.lds, s) : ffl::launch_sp<4, false>(a, nblocks, p.lds, s);
+            return ucn ? ffl::launch_sp<2, true>(a, nblocks, p.lds, s) : ffl::launch_sp<2, false>(a, nblocks, p.lds, s);
         default: return ffl::launch_mode<MODE_Q6>(a, p.cw, ucn, nblocks, p.lds, s);
     }
 }

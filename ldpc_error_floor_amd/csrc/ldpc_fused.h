@@ -53,11 +53,11 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
                bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s);
 void fused_free(FusedWorkspace& ws);
 
-// float-mode fused decoder (ldpc_ffl.hip): MS, MS without nudge, QMS q = 6; counters / flags
+// float-mode fused decoder (ldpc_ffl.hip): MS, MS without nudge, QMS q = 6, sum-product; counters / flags
 // only, row-uniform CN weights
 bool ffl_mode(int mode);
 bool ffl_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w);
-const char* ffl_kernel_name(const DevGraph& g, bool ucn, bool per_edge_w);
+const char* ffl_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w);
 int ffl_decode(const DevGraph& g, const Bufs& b, const float* llr, int mode, bool ucn, bool per_edge_w,
                int64_t* counters, uint8_t* flags, hipStream_t s);
 

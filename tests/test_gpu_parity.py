@@ -29,8 +29,9 @@ def _decoder(c, kernel, device):
 
 
 def _float_mode(c):
-    """MS, MS without nudge and QMS q = 6: the fused path is the counters-only ffl kernel."""
-    return c["dt"] in (1, 3) or (c["dt"] == 2 and c["q"] == 6)
+    """Sum-product, MS, MS without nudge and QMS q = 6: the fused path is the counters-only ffl
+    kernel."""
+    return c["dt"] in (0, 1, 3) or (c["dt"] == 2 and c["q"] == 6)
 
 
 def test_extension_is_native(cuda_device):
