@@ -231,6 +231,25 @@ std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap) {
     return slot;
 }
 
+// dealing cost of each 64-lane check chunk (LPC lanes per check): the chunk's edge positions
+// that hold a real edge for some lane (the kernels skip the rest wave-uniformly) plus the
+// per-check work that does not depend on the degree
+std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch) {
+    std::vector<int> cost(cch, 2);
+    const int nc = h.M * h.z;
+    for (int ch = 0; ch < cch; ++ch) {
+        int dmax = 0;
+        for (int l = 0; l < 64; ++l) {
+            const int cc = (64 * ch + l) / LPC;
+            if (cc >= nc) break;
+            const int i = cc / h.z;
+            dmax = std::max(dmax, h.row_ptr[i + 1] - h.row_ptr[i]);
+        }
+        cost[ch] += (dmax + LPC - 1) / LPC;
+    }
+    return cost;
+}
+
 // the per-decode weight tables of both bit-sliced kernels (k_bs_tables)
 int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, float cu,
                    bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s) {
@@ -336,7 +355,7 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
     if (k.CPL == 1 && k.VPL == 1) {
         for (int w = 0; w < p.nw; ++w) cchunk[w] = w < cch ? w : -1;
     } else {
-        const std::vector<int> cs = deal_chunks(std::vector<int>(cch, 1), p.nw, k.CPL);
+        const std::vector<int> cs = deal_chunks(check_chunk_cost(h, LPC, cch), p.nw, k.CPL);
         for (size_t x = 0; x < cs.size(); ++x) cchunk[x] = cs[x];
     }
     // UCN: per check lane, the LDS byte addresses (16-bit, packed) of its edges' hard decisions

@@ -356,6 +356,7 @@ k_bs(BsArgs a) {
     static_assert(LPC == 2 || LPC == 4, "lanes per check");
     constexpr int SB = (DV * QMAX + QMAX <= 127) ? 8 : 9;     // planes of S and of lw + S
     constexpr int EPL = (D + LPC - 1) / LPC;                     // edge slots per check lane
+    constexpr bool SKIPM = CPL > 1;                              // chunk-wide padding skipped
     constexpr int OB = 4 / LPC;                                  // alpha-table output bits per lane
     constexpr int VNA = PK ? (DV + 1) / 2 : DV;                  // address words per variable
     constexpr int VNW = VNA + 1;
@@ -615,7 +616,7 @@ k_bs(BsArgs a) {
     // only.  (Lane j of a check's group evaluates alpha-table output bits OB j .. OB j + OB - 1:
     // 16 words per bit, at 64 B per bit.)
     const int cj = lane % LPC;
-    int gchunk[CPL], gdeg[CPL];
+    int gchunk[CPL], gdeg[CPL], gm[CPL];
     uint32_t gbase[CPL], gtab[CPL], ghd[CPL][UCN ? HDW : 1];
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
@@ -624,6 +625,12 @@ k_bs(BsArgs a) {
         const int cc = ql / LPC;
         const int ci = min(cc / a.z, a.n_checks / a.z - 1);
         gdeg[c] = (cc < a.n_checks) ? a.row_ptr[ci + 1] - a.row_ptr[ci] : 0;
+        // edge positions m holding a real edge for some lane of the chunk (wave-uniform): the
+        // positions past them are padding for every lane and skipped (LPC, an even count, lanes
+        // of each group skip together, so the group's [V->C >= 0] parity is unchanged)
+        // (the instances with several check chunks per lane: 5G-type graphs, whose rows differ
+        // in degree; the one-chunk instances serve near-regular rows and keep their registers)
+        gm[c] = SKIPM ? (int)__popc(wave_or((1u << ((gdeg[c] + LPC - 1) / LPC)) - 1u)) : EPL;
         gbase[c] = a.off_slots + (uint32_t)((a.row_lay[2 * ci] + cj * a.row_lay[2 * ci + 1] + (cc - ci * a.z)) * SLOT_B);
         gtab[c] = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * OB * 64);
         if constexpr (UCN) {
@@ -662,6 +669,8 @@ k_bs(BsArgs a) {
             uint32_t cbase = gbase[c];
             asm volatile("" : "+v"(cbase));
             const int cdeg = gdeg[c];
+            int gmc = gm[c];
+            asm volatile("" : "+s"(gmc));
             // slot m of the lane: always a real edge while LPC m + LPC - 1 < cn_dmin
             auto real = [&](int m) __attribute__((always_inline)) -> bool {
                 return LPC * m + LPC - 1 < cn_dmin || LPC * m + cj < cdeg;
@@ -675,7 +684,15 @@ k_bs(BsArgs a) {
             // in registers for pass 2)
             uint32_t Xs[EPL][4], ns[EPL];
 #pragma unroll
-            for (int m = 0; m < EPL; ++m) read_slot(ns[m], Xs[m], caddr(m));
+            for (int m = 0; m < EPL; ++m) {
+                if (SKIPM && m >= gmc) {             // padding for the whole chunk
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) Xs[m][i] = ~0u;
+                    ns[m] = ~0u;
+                } else {
+                    read_slot(ns[m], Xs[m], caddr(m));
+                }
+            }
             // UCN: syndrome of the previous hard decisions over the check (padding edges read a
             // zero word): odd -> the check is unsatisfied, its messages weighted by alpha'
             uint32_t syn = 0u;
@@ -683,6 +700,7 @@ k_bs(BsArgs a) {
                 if (ucn) {
 #pragma unroll
                     for (int m = 0; m < EPL; ++m) {
+                        if (SKIPM && m >= gmc) continue;
                         const uint32_t hw = ghd[c][m >> 1];
                         syn ^= lds_w((m & 1) ? (hw >> 16) : (hw & 0xFFFFu));
                     }
@@ -694,6 +712,7 @@ k_bs(BsArgs a) {
             uint32_t par = ns[0];
 #pragma unroll
             for (int m = 1; m < EPL; ++m) {
+                if (SKIPM && m >= gmc) continue;
                 const uint32_t(&X)[4] = Xs[m];
                 const uint32_t l1 = lt4(X, m1), l2 = lt4(X, m2);
 #pragma unroll

@@ -268,7 +268,7 @@ k_bsc(BscArgs a) {
     vn_phase(true, false, a.off_blut, 0);
     // check groups (as bsl): lane LPC c + j of a chunk takes edges k = LPC m + j of check c
     const int cj = lane % LPC;
-    int gchunk[CPL], gdeg[CPL];
+    int gchunk[CPL], gdeg[CPL], gm[CPL];
     uint32_t gslot[CPL], grec[CPL], gtab[CPL], gvar[CPL][CVW];
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
@@ -277,6 +277,10 @@ k_bsc(BscArgs a) {
         const int cc = ql / LPC;
         const int ci = min(cc / a.z, a.n_checks / a.z - 1);
         gdeg[c] = (cc < a.n_checks) ? a.row_ptr[ci + 1] - a.row_ptr[ci] : 0;
+        // edge positions m holding a real edge for some lane of the chunk (wave-uniform): the
+        // positions past them are padding for every lane and skipped (LPC, an even count, lanes
+        // of each group skip together, so the group's [V->C >= 0] parity is unchanged)
+        gm[c] = __popc(wave_or((1u << ((gdeg[c] + LPC - 1) / LPC)) - 1u));
         (void)nwv;
         gslot[c] = (uint32_t)(4 * (a.row_lay[2 * ci] + cj * a.row_lay[2 * ci + 1] + (cc - ci * a.z)));
         grec[c] = a.off_rec + 32u * (uint32_t)min(cc, a.n_checks - 1);
@@ -311,6 +315,8 @@ k_bsc(BscArgs a) {
         for (int c = 0; c < CPL; ++c) {
             if (gchunk[c] < 0) continue;
             const int cdeg = gdeg[c];
+            int gmc = gm[c];
+            asm volatile("" : "+s"(gmc));
             uint32_t sbase = gslot[c];
             asm volatile("" : "+v"(sbase));
             auto real = [&](int m) __attribute__((always_inline)) -> bool {
@@ -325,6 +331,12 @@ k_bsc(BscArgs a) {
             uint32_t Xs[EPL][4], ns[EPL];
 #pragma unroll
             for (int m = 0; m < EPL; ++m) {
+                if (m >= gmc) {                      // padding for the whole chunk
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) Xs[m][i] = ~0u;
+                    ns[m] = ~0u;
+                    continue;
+                }
                 const uint32_t vw = gvar[c][m >> 1];
                 const uint32_t vi = (m & 1) ? (vw >> 16) : (vw & 0xFFFFu);
                 const uint32_t ta = a.off_tv + 24u * vi;
@@ -356,6 +368,7 @@ k_bsc(BscArgs a) {
             uint32_t par = ns[0];
 #pragma unroll
             for (int m = 1; m < EPL; ++m) {
+                if (m >= gmc) continue;
                 const uint32_t(&X)[4] = Xs[m];
                 const uint32_t l1 = lt4(X, m1), l2 = lt4(X, m2);
 #pragma unroll
@@ -447,6 +460,7 @@ namespace bs {
 
 std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* nslot);
 std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap);
+std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch);
 int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, float cu,
                    bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s);
 
@@ -586,7 +600,7 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     if (k.CPL == 1 && k.VPL == 1) {
         for (int w = 0; w < NWp; ++w) cchunk[w] = w < cch ? w : -1;
     } else {
-        const std::vector<int> cs = deal_chunks(std::vector<int>(cch, 1), NWp, k.CPL);
+        const std::vector<int> cs = deal_chunks(check_chunk_cost(h, LPC, cch), NWp, k.CPL);
         for (size_t x = 0; x < cs.size(); ++x) cchunk[x] = cs[x];
     }
     std::vector<uint32_t> cvar((size_t)p.cn_lanes * CVW, 0u);
