@@ -17,14 +17,15 @@ namespace bs {
 // per-decode tables: 16-entry g(m) tables as mux-tree leaves, [t][table][bit j][pair p] {X, Y}
 // with Y = bit j of g(2p) (as a 0 / ~0 word) and X = Y ^ (bit j of g(2p + 1)):
 // level 1 of the tree is (m0 & X) ^ Y.
-//   alpha: g(m) = Q(relu(fl32(m step * alpha_{t,row}))) (Main_Functions.py:266-316), m = min(|V->C|);
+//   alpha: g(m) = Q(relu(fl32(min(m, qmax) step * alpha_{t,row}))) (Main_Functions.py:266-316),
+//          m = min(|V->C|) saturated at 15 (see bs_qmax);
 //          with UCN the alpha' tables (rows arows .. 2 arows - 1) follow the alpha ones
 //   beta:  g(m) = Q(fl32(m * beta_{t,col})) in grid units (lw = Q(beta ch), :164-177; beta >= 0),
 //          then 4 words: the planes of |Q(fl32(cu * beta))| for a shortened bit (|ch| = cu)
 __global__ void k_bs_tables(const float* __restrict__ alpha, const float* __restrict__ alpha_ucn,
                             const float* __restrict__ beta, const int32_t* __restrict__ row_ptr,
                             int T, int E, int N, int arows, int ar, int bcols, float step, float inv,
-                            float cu, uint32_t* alut, uint32_t* blut) {
+                            int qmax, float cu, uint32_t* alut, uint32_t* blut) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;    // one table per thread
     const int na = T * ar, nbt = T * bcols;
     if (f >= na + nbt) return;
@@ -35,18 +36,18 @@ __global__ void k_bs_tables(const float* __restrict__ alpha, const float* __rest
         const float* al = (r < arows) ? alpha : alpha_ucn;
         const int row = (r < arows) ? r : r - arows;
         const float w = al[(size_t)t * E + row_ptr[row]];
-        for (int m = 0; m < 16; ++m) g[m] = f5::q_mag5(m, w, step, inv, QMAX);
+        for (int m = 0; m < 16; ++m) g[m] = f5::q_mag5(min(m, qmax), w, step, inv, qmax);
         out = alut + (size_t)f * LUT_W;
     } else {
         const int f2 = f - na;
         const int t = f2 / bcols, col = f2 - t * bcols;
         const float b = beta[(size_t)t * N + col];
         for (int m = 0; m < 16; ++m) {
-            const int q = (int)__builtin_amdgcn_fmed3f(rintf((float)m * b), -(float)QMAX, (float)QMAX);
+            const int q = (int)__builtin_amdgcn_fmed3f(rintf((float)m * b), -(float)qmax, (float)qmax);
             g[m] = q < 0 ? -q : q;       // beta >= 0 (checked on the host)
         }
         out = blut + (size_t)f2 * BLUT_W;
-        const int qb = (int)__builtin_amdgcn_fmed3f(rintf(cu * b), -(float)QMAX, (float)QMAX);
+        const int qb = (int)__builtin_amdgcn_fmed3f(rintf(cu * b), -(float)qmax, (float)qmax);
         for (int j = 0; j < 4; ++j) out[LUT_W + j] = (((qb < 0 ? -qb : qb) >> j) & 1) ? ~0u : 0u;
     }
     for (int j = 0; j < 4; ++j)
@@ -110,7 +111,17 @@ std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* ns
     return lay;
 }
 
-static float mode_step_bs(int mode) { return (mode == MODE_Q5) ? 0.5f : 1.0f; }
+// The QMS grids both bit-sliced kernels decode: q = 5 (step 0.5), -5 (1), 4 (1), 3 (2), values
+// |m| <= qmax in grid units (Cal_MSA_Q, Print_Functions.py:12-25; Main_Functions.py:475-494).
+// Messages keep four magnitude planes saturated at 15 >= qmax: a V->C magnitude only reaches the
+// check's two minima and the [|V->C| = min] test, and the alpha tables are built on
+// min(m, qmax), so saturating at 15 instead of qmax leaves every C->V unchanged (the clamp
+// commutes with the order statistics, and whenever the minimum is >= qmax every edge gets
+// g(qmax)); APP and Tv are sums of C->V and the channel, which is checked against qmax.
+bool bs_mode(int mode) { return mode == MODE_Q5 || mode == MODE_QM5 || mode == MODE_Q4 || mode == MODE_Q3; }
+float bs_step(int mode) { return mode == MODE_Q5 ? 0.5f : mode == MODE_Q3 ? 2.0f : 1.0f; }
+int bs_qmax(int mode) { return mode == MODE_Q4 ? 7 : mode == MODE_Q3 ? 3 : QMAX; }
+static float mode_step_bs(int mode) { return bs_step(mode); }
 
 // the plan of one instance (ok = it serves the graph)
 static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_cdeg, int mode) {
@@ -137,7 +148,7 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     p.cn_dmin = (p.cn_lanes == k.LPC * nc) ? min_cdeg : 0;
     if (k.BIG) {
         const float cu = clip / mode_step_bs(mode);
-        if (cu > (float)QMAX) p.cu = cu;
+        if (cu > (float)bs_qmax(mode)) p.cu = cu;
     }
     size_t nslot = 0;
     p.lay = slot_layout(h, k.LPC, &nslot);
@@ -172,7 +183,7 @@ BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float cli
     if (e && atoi(e) == 0) return p;
     const char* el = getenv("LDPC_BS_LPC");          // A/B: force 2 or 4 lanes per check
     const int want_lpc = el ? atoi(el) : 0;
-    if (mode != MODE_Q5 && mode != MODE_QM5) return p;           // qmax 15: 4 magnitude planes
+    if (!bs_mode(mode)) return p;
     if (per_edge_w || !g.host || !g.w_beta_nonneg) return p;
     const host::GraphTables& h = *g.host;
     int min_cdeg = 1 << 30;
@@ -251,8 +262,8 @@ std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch) 
 }
 
 // the per-decode weight tables of both bit-sliced kernels (k_bs_tables)
-int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, float cu,
-                   bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s) {
+int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, int qmax,
+                   float cu, bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s) {
     const size_t na = (size_t)b.T * ar * LUT_W, nb = (size_t)b.T * bcols * BLUT_W;
     const size_t bytes = (na + nb) * 4;
     if (bytes > ws.bs_lut_bytes) {
@@ -268,15 +279,15 @@ int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcol
     // (skipped when these tables are already in place: same weights, T and layout)
     const uint64_t kb[4] = {g.w_version, (uint64_t)b.T << 32 | (uint32_t)(arows << 16 | ar),
                             (uint64_t)__builtin_bit_cast(uint32_t, step) << 32 | __builtin_bit_cast(uint32_t, cu),
-                            (uint64_t)bcols << 1 | (ucn && b.alpha_ucn ? 1u : 0u)};
+                            (uint64_t)qmax << 40 | (uint64_t)bcols << 1 | (ucn && b.alpha_ucn ? 1u : 0u)};
     if (std::equal(kb, kb + 4, ws.key_bslut)) return LDPC_OK;
     std::copy(kb, kb + 4, ws.key_bslut);
     const int ntab = b.T * (ar + bcols);
     // without UCN weights the alpha' slots (UCN instances) repeat the alpha tables (unused)
     const float* au = (ucn && b.alpha_ucn) ? b.alpha_ucn : b.alpha;
     hipLaunchKernelGGL(k_bs_tables, dim3((unsigned)((ntab + 127) / 128)), dim3(128), 0, s, b.alpha, au,
-                       b.beta, g.row_ptr, b.T, g.E, g.N, arows, ar, bcols, step, 1.0f / step, cu,
-                       *alut, *blut);
+                       b.beta, g.row_ptr, b.T, g.E, g.N, arows, ar, bcols, step, 1.0f / step, qmax,
+                       cu, *alut, *blut);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 }  // namespace bs
@@ -418,7 +429,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     const float step = mode_step_bs(mode);
     const int ar = (k.UCN ? 2 : 1) * p.arows;
     uint32_t *alut = nullptr, *blut = nullptr;
-    st = bs_make_tables(b, g, p.arows, ar, p.bcols, step, p.cu, ucn, ws, &alut, &blut, s);
+    st = bs_make_tables(b, g, p.arows, ar, p.bcols, step, bs_qmax(mode), p.cu, ucn, ws, &alut, &blut, s);
     if (st != LDPC_OK) return st;
     const int DV = k.DV;
     const int VNW = (k.PK ? (DV + 1) / 2 : DV) + 1;
@@ -434,8 +445,9 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.cn_dmin = p.cn_dmin;
     a.inv = 1.0f / step;
     a.cu = p.cu > 0.f ? p.cu : -1.f;
+    a.qmax = bs_qmax(mode);
     a.ucn = p.ucn ? 1 : 0;
-    a.beta_id = (mode == MODE_Q5 || mode == MODE_QM5) ? g.w_beta_id_mask : 0;
+    a.beta_id = g.w_beta_id_mask;        // (identity on m <= 15 implies it on m <= qmax)
     a.row_ptr = g.row_ptr;
     a.z = g.z;
     a.vn_tab = gt;

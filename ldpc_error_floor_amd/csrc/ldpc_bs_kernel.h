@@ -66,7 +66,8 @@ struct BsArgs {
     int64_t B;
     int n_vars, n_checks, T, target_bits, cn_lanes, cn_dmin;
     float inv;
-    float cu;                    // |LLR| / step of a shortened bit (BIG instances), > QMAX
+    float cu;                    // |LLR| / step of a shortened bit (BIG instances), > qmax
+    int qmax;                    // the grid's largest magnitude in grid units (15, 7 or 3)
     int ucn;                     // UCN weights present (UCN instances)
     uint64_t beta_id;            // bit t: iteration t's channel table is the identity (skipped)
     const int32_t* row_ptr;      // [M + 1] proto edges of each row (the check degrees)
@@ -423,9 +424,9 @@ k_bs(BsArgs a) {
             for (int r = 0; r < PACK; ++r) {
                 const float x = xv[r] * a.inv;
                 const float xr = rintf(x);
-                const bool big = BIG && fabsf(x) == a.cu;       // a shortened bit (a.cu > QMAX)
-                off |= ((xr != x || fabsf(xr) > (float)QMAX) && !big) ? 1 : 0;
-                const int xi = (r < nvalid) ? (big ? (x < 0.f ? -QMAX : QMAX) : (int)xr) : 0;
+                const bool big = BIG && fabsf(x) == a.cu;       // a shortened bit (a.cu > qmax)
+                off |= ((xr != x || fabsf(xr) > (float)a.qmax) && !big) ? 1 : 0;
+                const int xi = (r < nvalid) ? (big ? (x < 0.f ? -a.qmax : a.qmax) : (int)xr) : 0;
                 const uint32_t m = (uint32_t)(xi < 0 ? -xi : xi);
                 cs[u] |= (xi < 0 ? 1u : 0u) << r;
                 if (BIG) bg[u] |= (big && r < nvalid ? 1u : 0u) << r;

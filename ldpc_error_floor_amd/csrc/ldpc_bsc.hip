@@ -40,6 +40,7 @@ struct BscArgs {
     int64_t B;
     int n_vars, n_checks, T, target_bits, cn_dmin, z;
     float inv, cu;
+    int qmax;                    // the grid's largest magnitude in grid units (15, 7 or 3)
     int beta_id;                 // every beta is 1: Q(beta ch) = ch, no table
     const int32_t* row_ptr;
     const int32_t* row_lay;      // [M][2] slot layout (as bsl): first slot, j-block stride
@@ -130,8 +131,8 @@ k_bsc(BscArgs a) {
                 const float x = xv[r] * a.inv;
                 const float xr = rintf(x);
                 const bool big = fabsf(x) == a.cu;
-                off |= ((xr != x || fabsf(xr) > (float)QMAX) && !big) ? 1 : 0;
-                const int xi = (r < nvalid) ? (big ? (x < 0.f ? -QMAX : QMAX) : (int)xr) : 0;
+                off |= ((xr != x || fabsf(xr) > (float)a.qmax) && !big) ? 1 : 0;
+                const int xi = (r < nvalid) ? (big ? (x < 0.f ? -a.qmax : a.qmax) : (int)xr) : 0;
                 const uint32_t m = (uint32_t)(xi < 0 ? -xi : xi);
                 cs[u] |= (xi < 0 ? 1u : 0u) << r;
                 bg[u] |= (big && r < nvalid ? 1u : 0u) << r;
@@ -461,8 +462,11 @@ namespace bs {
 std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* nslot);
 std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap);
 std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch);
-int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, float cu,
-                   bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s);
+int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, int qmax,
+                   float cu, bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s);
+bool bs_mode(int mode);
+float bs_step(int mode);
+int bs_qmax(int mode);
 
 constexpr int kBscNInst = sizeof(kBscInst) / sizeof(kBscInst[0]);
 constexpr int BSC_NW = 16;
@@ -483,7 +487,7 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
     BscPlan p;
     const char* e = getenv("LDPC_BS");
     if (e && atoi(e) == 0) return p;
-    if (mode != MODE_Q5 && mode != MODE_QM5) return p;
+    if (!bs_mode(mode)) return p;
     if (ucn || per_edge_w || !g.host || !g.w_beta_nonneg) return p;
     const host::GraphTables& h = *g.host;
     int min_cdeg = 1 << 30;
@@ -522,8 +526,8 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
         q.arows = g.w_alpha_uniform ? 1 : h.M;
         q.bcols = g.w_beta_uniform ? 1 : h.N;
         q.cn_dmin = (q.cn_lanes == k.LPC * nc) ? min_cdeg : 0;
-        const float cu = clip / ((mode == MODE_Q5) ? 0.5f : 1.0f);
-        q.cu = cu > (float)QMAX ? cu : -1.f;
+        const float cu = clip / bs_step(mode);
+        q.cu = cu > (float)bs_qmax(mode) ? cu : -1.f;
         q.lay = slot_layout(h, k.LPC, &q.nslot);
         // LDS: SGN [nslot + 1] | ARG [nslot + 1] | REC [nc + 1][8] | TV [nv][6] | RED | ALUT | BLUT
         const size_t sgn = ((q.nslot + 1) * 4 + 127) & ~(size_t)127;
@@ -679,9 +683,9 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     int st = bsc_tables(g, p, ws, s);
     if (st != LDPC_OK) return st;
     const BscInst& k = kBscInst[p.inst];
-    const float step = (mode == MODE_Q5) ? 0.5f : 1.0f;
+    const float step = bs_step(mode);
     uint32_t *alut = nullptr, *blut = nullptr;
-    st = bs_make_tables(b, g, p.arows, p.arows, p.bcols, step, p.cu, false, ws, &alut, &blut, s);
+    st = bs_make_tables(b, g, p.arows, p.arows, p.bcols, step, bs_qmax(mode), p.cu, false, ws, &alut, &blut, s);
     if (st != LDPC_OK) return st;
     const uint32_t* gt = reinterpret_cast<const uint32_t*>(ws.bs_graph);
     const int VNW = k.DVH + 1;
@@ -696,6 +700,7 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     a.z = g.z;
     a.inv = 1.0f / step;
     a.cu = p.cu;
+    a.qmax = bs_qmax(mode);
     a.beta_id = g.w_beta_one ? 1 : 0;
     a.row_ptr = g.row_ptr;
     a.vn_tab = gt;

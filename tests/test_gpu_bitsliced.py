@@ -1,8 +1,8 @@
 """The bit-sliced fused kernel (csrc/ldpc_bs.hip: 32 codewords per 32-bit word) that serves
 counters-only QMS decodes (GPU only).  Its counters and per-frame flags must equal the flood
 kernel's (pinned to the reference fixtures) bit for bit: on ragged batches, with per-row /
-per-column weights, for q = 5 and q = -5, and with LLRs off the quantizer grid (those packs are
-decoded by the v5 kernel instead, so the result stays exact for any input)."""
+per-column weights, for q = 5, -5, 4 and 3, and with LLRs off the quantizer grid (those packs
+are decoded by the v5 kernel instead, so the result stays exact for any input)."""
 import os
 
 import numpy as np
@@ -230,3 +230,57 @@ def test_bitsliced_compressed_idle_check_lanes(cuda_device, lpc_c, monkeypatch):
     out = _both(dec, llr)
     assert np.array_equal(out["fused"][0], out["flood"][0]), (out["fused"][0], out["flood"][0])
     assert np.array_equal(out["fused"][1], out["flood"][1])
+
+
+# ---- q = 4 (integers, |v| <= 7) and q = 3 (even integers, |v| <= 6: 3 grid units of 2): the
+# messages keep four planes saturated at 15 and the alpha tables are built on min(m, qmax)
+# (ldpc_bs.hip, bs_qmax) --------------------------------------------------------------------
+@pytest.mark.parametrize("q", [4, 3])
+@pytest.mark.parametrize("sharing", [(3, 0, 3), (2, 0, 2)])
+def test_bitsliced_q4_q3_wman(cuda_device, q, sharing, lpc):
+    dec, cp = _wman(cuda_device, sharing=sharing, q=q, T=20 if sharing == (3, 0, 3) else 12)
+    assert dec.kernel_info()[1].startswith("bsl") and dec.kernel_info()[1].endswith(f",l{lpc}]"), \
+        dec.kernel_info()
+    for B, snr in ((3001, 2.0), (64, 3.0)):
+        llr = dec.awgn(B, float(cp.sigma(snr)), seed=21 + B, offset=5)
+        out = _both(dec, llr)
+        assert np.array_equal(out["fused"][0], out["flood"][0]), (q, out["fused"][0], out["flood"][0])
+        assert np.array_equal(out["fused"][1], out["flood"][1])
+    assert 0 < out["fused"][0][3] or B == 64
+
+
+@pytest.mark.parametrize("q", [4, 3])
+def test_bitsliced_q4_q3_off_grid(cuda_device, q):
+    """On the q = 4 / 3 grids a value of the q = 5 grid (0.5) or beyond qmax (9 > 7, 8 > 6) is
+    off the grid: its pack goes to the v5 fixup and the result stays exact."""
+    dec, cp = _wman(cuda_device, q=q)
+    llr = dec.awgn(3000, float(cp.sigma(2.0)), seed=4)
+    llr[40, 3] = 0.5
+    llr[1000, 7] = 9.0 if q == 4 else 8.0
+    llr[2999, 0] = -1.0 if q == 3 else 1.5
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
+
+
+@pytest.mark.parametrize("q", [4, 3])
+@pytest.mark.parametrize("cfg", ["C3", "C4", "C5"])
+def test_bitsliced_q4_q3_large_graphs(cuda_device, cfg, q, monkeypatch):
+    """The UCN / multi-lane bsl instances and bsc on q = 4 / 3: shortened bits are -clip_LLR =
+    -20 (20 / 10 grid units > qmax), decoded in place (the v5 fixup switched off gives the same)."""
+    import bench
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    proto, g, W, cp = bench.load_problem(T=12, config=cfg)
+    c = bench.CONFIGS[cfg]
+    dec = NMSDecoder(proto, c["z"], W, 2, q, device=cuda_device)
+    dec.punct, dec.short = c.get("punct", (0, 0)), c.get("short", (0, 0))
+    assert dec.kernel_info()[1].startswith(("bsl[", "bsc[")), dec.kernel_info()
+    llr = dec.awgn(2500, float(cp.sigma(c["snr"] - 0.5)), seed=13)
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0]), (cfg, q, out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
+    assert 0 < out["fused"][0][1] < 2500
+    if c.get("short", (0, 0))[0]:
+        monkeypatch.setenv("LDPC_BS_FIXUP", "0")
+        r = dec.decode(llr, app=False, counters=True, flags=True, kernel="fused")
+        assert np.array_equal(r.counters.cpu().numpy(), out["flood"][0])
