@@ -474,7 +474,8 @@ k_bs(BsArgs a) {
             const bool counted = v >= 0 && v < a.target_bits;
             uint32_t lw[1][4];                   // |Q(beta_{t+1} ch)| (before the C->V: fewer live registers)
             if (!last) {
-                if (ABL(2) || ((a.beta_id >> tb) & 1)) {   // identity table: |Q(beta ch)| = |ch|
+                // identity table: |Q(beta ch)| = |ch| (the mask covers iterations 0..63)
+                if (ABL(2) || (tb < 64 && ((a.beta_id >> tb) & 1))) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) lw[0][i] = cm[u][i];
                 } else if (a.bcols == 1) {          // one beta per iteration: table in SGPRs

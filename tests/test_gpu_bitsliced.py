@@ -284,3 +284,23 @@ def test_bitsliced_q4_q3_large_graphs(cuda_device, cfg, q, monkeypatch):
         monkeypatch.setenv("LDPC_BS_FIXUP", "0")
         r = dec.decode(llr, app=False, counters=True, flags=True, kernel="fused")
         assert np.array_equal(r.counters.cpu().numpy(), out["flood"][0])
+
+
+def test_bitsliced_more_than_64_iterations(cuda_device):
+    """T = 70 with a beta that is the identity on the grid in the first iterations only: the
+    identity-table mask covers iterations 0..63 and must not wrap onto later ones."""
+    from ldpc_error_floor_amd.code import CodeParams, TannerGraph, load_base_graph
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    from ldpc_error_floor_amd.weights import expand_weights
+    proto = load_base_graph(os.path.join(DATA, "BaseGraph", "wman_N0576_R34_z24.txt"))
+    g = TannerGraph(proto, 24)
+    T = 70
+    beta = np.where(np.arange(T) < 8, 1.0, 0.7)[:, None]    # identity at t < 8 only: a wrapped
+    #                                                         mask would skip t = 64..69's tables
+    W = expand_weights((3, 0, 3), {0: np.full((T, 1), 0.75), 2: beta}, T, g)
+    dec = NMSDecoder(proto, 24, W, 2, 5, device=cuda_device)
+    assert dec.kernel_info()[1].startswith("bsl"), dec.kernel_info()
+    llr = dec.awgn(2000, float(CodeParams(proto, 24).sigma(2.0)), seed=8)
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0]), (out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
