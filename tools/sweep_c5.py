@@ -10,6 +10,7 @@ no error in the scan).  Each stage checkpoints to ``<out>/ckpt_<stage>.json`` ev
 and resumes from it when rerun with the same arguments.  Writes ``<out>/sweep_c5.json``.
 
   python tools/sweep_c5.py --out gpurun_out/sweep_c5 [--scan 4194304] [--deep 1073741824]
+  python tools/sweep_c5.py --out gpurun_out/c5_deep --deep-snrs 15.0 --deep 10737418240
 """
 import argparse
 import json
@@ -29,6 +30,8 @@ def main():
     ap.add_argument("--deep", type=int, default=1 << 30)
     ap.add_argument("--deep-below", type=float, default=1e-3)
     ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--deep-snrs", default="",
+                    help="skip the scan: decode --deep codewords at each of these SNRs only")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -43,7 +46,7 @@ def main():
     dec = NMSDecoder(proto, cfg["z"], W, 2, 5, device=dev, B_max=a.batch)
     dec.punct, dec.short = cfg["punct"], cfg["short"]
     kernel = dec.kernel_info()[1]
-    snrs = [float(x) for x in a.snrs.split(",")]
+    snrs = [float(x) for x in (a.deep_snrs or a.snrs).split(",")]
     sig = [float(x) for x in cp.sigma(np.asarray(snrs))]
     last = [time.time()]
 
@@ -71,13 +74,16 @@ def main():
             print(f"{stage} {snrs[i]:.2f} dB: FER_last {fe}/{n} = {fe / n:.3e}", flush=True)
         return rows, dt
 
-    scan, t_scan = run("scan", list(range(len(snrs))), a.scan)
-    deep_idx = [i for i, r in enumerate(scan) if 0 < r["fer_last"] < a.deep_below]
-    zero = [i for i, r in enumerate(scan) if r["frame_err_last"] == 0]
-    if zero:
-        deep_idx.append(zero[0])
+    if a.deep_snrs:
+        scan, t_scan, deep_idx = [], 0.0, list(range(len(snrs)))
+    else:
+        scan, t_scan = run("scan", list(range(len(snrs))), a.scan)
+        deep_idx = [i for i, r in enumerate(scan) if 0 < r["fer_last"] < a.deep_below]
+        zero = [i for i, r in enumerate(scan) if r["frame_err_last"] == 0]
+        if zero:
+            deep_idx.append(zero[0])
     deep, t_deep = run("deep", sorted(set(deep_idx)), a.deep) if deep_idx else ([], 0.0)
-    n_total = a.scan * len(snrs) + a.deep * len(set(deep_idx))
+    n_total = a.scan * len(scan) + a.deep * len(set(deep_idx))
     out = {"workload": "C5: 5G_LDPC_R0.73_n_dec2304_n2112_k1536_z72_s1537_1584, QMS q5, T=50, "
                        "flat [3,0,3] alpha=0.75 beta=1, puncture 1-144, shorten 1537-1584, "
                        "on-GPU Philox AWGN (seed 1076 + 7919 x SNR index), all-zero codeword",
