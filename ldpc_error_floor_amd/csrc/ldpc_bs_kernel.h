@@ -328,6 +328,16 @@ __device__ __forceinline__ void merge2(uint32_t (&m1)[4], uint32_t (&m2)[4], con
 #pragma unroll
     for (int i = 0; i < 4; ++i) m2[i] = mux(l2, x[i], y[i]);
 }
+// lo = min(A, B), hi = max(A, B) (4-plane magnitudes)
+__device__ __forceinline__ void sort2(uint32_t (&lo)[4], uint32_t (&hi)[4], const uint32_t (&A)[4],
+                                      const uint32_t (&B)[4]) {
+    const uint32_t l = lt4(B, A);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        lo[i] = mux(l, B[i], A[i]);
+        hi[i] = mux(l, A[i], B[i]);
+    }
+}
 template <int CTRL>
 __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]) {
     uint32_t b1[4], b2[4];
@@ -712,6 +722,29 @@ k_bs(BsArgs a) {
             }
             uint32_t m1[4] = {Xs[0][0], Xs[0][1], Xs[0][2], Xs[0][3]}, m2[4] = {~0u, ~0u, ~0u, ~0u};
             uint32_t par = ns[0];
+            if constexpr (!SKIPM && EPL >= 2) {
+                // tournament: sort pairs (12 ops), merge sorted pairs (24) — 48 ops for four
+                // edges against 56 for the running two-minima update (only the two values matter)
+                sort2(m1, m2, Xs[0], Xs[1]);
+                par ^= ns[1];
+#pragma unroll
+                for (int m = 2; m + 1 < EPL; m += 2) {
+                    uint32_t b1[4], b2[4];
+                    sort2(b1, b2, Xs[m], Xs[m + 1]);
+                    merge2(m1, m2, b1, b2);
+                    par ^= ns[m] ^ ns[m + 1];
+                }
+                if constexpr (EPL & 1) {
+                    const uint32_t(&X)[4] = Xs[EPL - 1];
+                    const uint32_t l1 = lt4(X, m1), l2 = lt4(X, m2);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        m2[i] = mux(l1, m1[i], mux(l2, X[i], m2[i]));
+                        m1[i] = mux(l1, X[i], m1[i]);
+                    }
+                    par ^= ns[EPL - 1];
+                }
+            } else {
 #pragma unroll
             for (int m = 1; m < EPL; ++m) {
                 if (SKIPM && m >= gmc) continue;
@@ -723,6 +756,7 @@ k_bs(BsArgs a) {
                     m1[i] = mux(l1, X[i], m1[i]);
                 }
                 par ^= ns[m];
+            }
             }
             par ^= qperm<QP_X1>(par);
             merge_lanes<QP_X1>(m1, m2);

@@ -54,3 +54,28 @@ def test_full_batch_kernels_agree_and_match_oracle(cuda_device, config, lpc, mon
         assert np.array_equal(small.flags.cpu().numpy(), flags[lo:lo + n])
     del llr
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("q", [4, 3])
+def test_full_batch_q4_q3(cuda_device, q):
+    """q = 4 / 3 at B = 2^20 on the bit-sliced kernel (grid step 1 / 2, qmax 7 / 3): counters and
+    per-frame flags equal flood's, and the in-decoder channel gives the same."""
+    import torch
+    import bench
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    proto, g, W, cp = bench.load_problem(config="C2")
+    dec = NMSDecoder(proto, 24, W, 2, q, device=cuda_device, B_max=B)
+    assert dec.kernel_info()[1].startswith("bsl["), dec.kernel_info()
+    sigma = float(cp.sigma(2.5))
+    llr = dec.awgn(B, sigma, seed=37)
+    res = {}
+    for k in ("fused", "flood"):
+        r = dec.decode(llr, app=False, counters=True, flags=True, kernel=k)
+        res[k] = (r.counters.cpu().numpy(), r.flags.cpu().numpy())
+    assert np.array_equal(res["fused"][0], res["flood"][0])
+    assert np.array_equal(res["fused"][1], res["flood"][1])
+    assert 0 < res["fused"][0][1] < B
+    r = dec.decode_awgn(B, sigma, 37, counters=True, flags=True)
+    assert np.array_equal(r.counters.cpu().numpy(), res["fused"][0])
+    del llr
+    torch.cuda.empty_cache()
