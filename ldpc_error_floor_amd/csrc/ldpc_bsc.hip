@@ -365,19 +365,31 @@ k_bsc(BscArgs a) {
                     ns[m] = ~0u;
                 }
             }
-            uint32_t m1[4] = {Xs[0][0], Xs[0][1], Xs[0][2], Xs[0][3]}, m2[4] = {~0u, ~0u, ~0u, ~0u};
-            uint32_t par = ns[0];
+            // two minima by a tournament (sorted pairs merged, as bsl); positions past the chunk's
+            // bound hold the all-ones padding, so a pair that straddles it sorts correctly and its
+            // padding sign word, XORed by all LPC lanes of the group, leaves the parity unchanged
+            uint32_t m1[4], m2[4];
+            sort2(m1, m2, Xs[0], Xs[1]);
+            uint32_t par = ns[0] ^ ns[1];
 #pragma unroll
-            for (int m = 1; m < EPL; ++m) {
+            for (int m = 2; m + 1 < EPL; m += 2) {
                 if (m >= gmc) continue;
-                const uint32_t(&X)[4] = Xs[m];
-                const uint32_t l1 = lt4(X, m1), l2 = lt4(X, m2);
+                uint32_t b1[4], b2[4];
+                sort2(b1, b2, Xs[m], Xs[m + 1]);
+                merge2(m1, m2, b1, b2);
+                par ^= ns[m] ^ ns[m + 1];
+            }
+            if constexpr (EPL & 1) {
+                if (EPL - 1 < gmc) {
+                    const uint32_t(&X)[4] = Xs[EPL - 1];
+                    const uint32_t l1 = lt4(X, m1), l2 = lt4(X, m2);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    m2[i] = mux(l1, m1[i], mux(l2, X[i], m2[i]));
-                    m1[i] = mux(l1, X[i], m1[i]);
+                    for (int i = 0; i < 4; ++i) {
+                        m2[i] = mux(l1, m1[i], mux(l2, X[i], m2[i]));
+                        m1[i] = mux(l1, X[i], m1[i]);
+                    }
+                    par ^= ns[EPL - 1];
                 }
-                par ^= ns[m];
             }
             par ^= qperm<QP_X1>(par);
             merge_lanes<QP_X1>(m1, m2);
