@@ -15,6 +15,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--snr", type=float, default=None, help="default: the config's SNR")
     ap.add_argument("--config", default="C2", help="a bench.py SURVEY 8d workload (C2..C5)")
+    ap.add_argument("--decoding-type", type=int, default=2)
+    ap.add_argument("--q-bit", type=int, default=5)
     a = ap.parse_args()
     import torch
     import bench
@@ -22,7 +24,7 @@ def main():
     cfg = bench.CONFIGS[a.config]
     proto, g, W, cp = bench.load_problem(config=a.config)
     snr = cfg["snr"] if a.snr is None else a.snr
-    dec = NMSDecoder(proto, cfg["z"], W, 2, 5, kernel=a.kernel, B_max=a.batch)
+    dec = NMSDecoder(proto, cfg["z"], W, a.decoding_type, a.q_bit, kernel=a.kernel, B_max=a.batch)
     llr = dec.awgn(a.batch, float(cp.sigma(snr)), seed=1076, punct=cfg.get("punct", (0, 0)),
                    short=cfg.get("short", (0, 0)))
     cnt = torch.zeros(4, dtype=torch.int64, device=llr.device)

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 K=${K:-auto}; B=${B:-1048576}; TAG=${TAG:-p}; CFG=${CFG:-C2}
 OUT=gpurun_out/prof_${TAG}_${CFG}_${K}
 mkdir -p $OUT
-ARGS="--kernel $K --batch $B --reps 3 --config $CFG"
+ARGS="--kernel $K --batch $B --reps 3 --config $CFG ${PROF_EXTRA:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 tools/prof_decode.py $ARGS > $OUT/trace.log 2>&1 || { tail $OUT/trace.log; exit 1; }
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE" \
