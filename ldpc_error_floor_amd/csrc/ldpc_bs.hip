@@ -330,35 +330,52 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
             for (int f = 0; f < DV; ++f) put(q, f, p.off_zero);
             q[VNA] = 0xFFFFFFFFu;
         }
+    const char* eo = getenv("LDPC_BS_VORDER");       // A/B: 0 keeps the graph's edge order
+    const bool vorder = !(eo && atoi(eo) == 0);
+    int vcost_before = 0, vcost_after = 0;
+    std::vector<uint32_t> A((size_t)64 * DV);
+    std::vector<int> dl(64);
     for (int w = 0; w < p.nw; ++w)
         for (int u = 0; u < k.VPL; ++u) {
             const int ch = vslot[(size_t)w * k.VPL + u];
             int dmax = 0, dmin = 1 << 30;
             if (ch < 0) dmin = 0;
-            for (int l = 0; ch >= 0 && l < 64; ++l) {
-                uint32_t* q = &vn[((size_t)u * nl + 64 * w + l) * VNW];
+            if (ch < 0) continue;
+            std::fill(A.begin(), A.end(), p.off_zero);
+            std::fill(dl.begin(), dl.end(), 0);
+            for (int l = 0; l < 64; ++l) {
                 const int o = 64 * ch + l;
                 if (o >= nv) { dmin = 0; continue; }
                 const int v = order[o], j = v / z, hh = v - j * z;
                 const int c0 = h.col_ptr[j], dv = h.col_ptr[j + 1] - c0;
-                for (int pw = 0; pw < VNA; ++pw) q[pw] = 0u;
-                for (int f = 0; f < DV; ++f) {
-                    uint32_t addr = p.off_zero;
-                    if (f < dv) {
-                        const int pe = h.col_pe[c0 + f], i = h.pe_row[pe];
-                        int hc = hh - h.pe_shift[pe];
-                        hc = hc < 0 ? hc + z : hc;
-                        addr = slot_addr(i, pe - h.row_ptr[i], hc);
-                    }
-                    put(q, f, addr);
+                for (int f = 0; f < dv; ++f) {
+                    const int pe = h.col_pe[c0 + f], i = h.pe_row[pe];
+                    int hc = hh - h.pe_shift[pe];
+                    hc = hc < 0 ? hc + z : hc;
+                    A[(size_t)l * DV + f] = slot_addr(i, pe - h.row_ptr[i], hc);
                 }
-                q[VNA] = (uint32_t)v;
+                dl[l] = dv;
                 dmax = std::max(dmax, dv);
                 dmin = std::min(dmin, dv);
+            }
+            if (vorder) {
+                const std::pair<int, int> c = host::order_variable_edges(A, dl, DV, std::min(DV, dmax));
+                vcost_before += c.first;
+                vcost_after += c.second;
+            }
+            for (int l = 0; l < 64; ++l) {
+                const int o = 64 * ch + l;
+                if (o >= nv) continue;
+                uint32_t* q = &vn[((size_t)u * nl + 64 * w + l) * VNW];
+                for (int pw = 0; pw < VNA; ++pw) q[pw] = 0u;
+                for (int f = 0; f < DV; ++f) put(q, f, A[(size_t)l * DV + f]);
+                q[VNA] = (uint32_t)order[o];
             }
             wdeg[2 * ((size_t)u * p.nw + w)] = dmax;
             wdeg[2 * ((size_t)u * p.nw + w) + 1] = dmin;
         }
+    if (getenv("LDPC_BS_VORDER_LOG"))
+        fprintf(stderr, "bsl variable-phase bank cycles per slot word: %d -> %d\n", vcost_before, vcost_after);
     // check chunks (64 check lanes each) dealt to (wave, c) places; the small instances run
     // chunk w on wave w
     const int cch = p.cn_lanes / 64;

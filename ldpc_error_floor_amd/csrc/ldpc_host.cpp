@@ -152,5 +152,56 @@ int check_channel(int64_t B, int32_t n_vars, double sigma, int64_t offset, int32
     return LDPC_OK;
 }
 
+std::pair<int, int> order_variable_edges(std::vector<uint32_t>& A, const std::vector<int>& deg, int DV,
+                                         int rounds) {
+    // cost of round f of the half-wave at lane h0: the most distinct addresses on one bank (the
+    // cycles the access takes), and the sum of squared bank loads as the tie-break that lets the
+    // climb leave plateaus of equal maxima
+    auto round_cost = [&](int h0, int f) {
+        uint32_t seen[32];
+        int ns = 0, cnt[32] = {0}, mx = 0, sq = 0;
+        for (int l = h0; l < h0 + 32; ++l) {
+            const uint32_t ad = A[(size_t)l * DV + f];
+            bool dup = false;
+            for (int i = 0; i < ns && !dup; ++i) dup = seen[i] == ad;
+            if (dup) continue;
+            seen[ns++] = ad;
+            const int c = ++cnt[(ad >> 2) & 31];
+            mx = std::max(mx, c);
+            sq += 2 * c - 1;
+        }
+        return mx * 4096 + sq;
+    };
+    int before = 0, after = 0;
+    uint64_t rng = 0x9E3779B97F4A7C15ull;
+    for (int h0 = 0; h0 < 64; h0 += 32) {
+        std::vector<int> cost(rounds);
+        std::vector<int> movable;
+        for (int l = h0; l < h0 + 32; ++l)
+            if (deg[l] >= 2) movable.push_back(l);
+        for (int f = 0; f < rounds; ++f) {
+            cost[f] = round_cost(h0, f);
+            before += cost[f] / 4096;
+        }
+        for (int it = 0; it < 4000 && !movable.empty(); ++it) {
+            rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+            const int l = movable[(rng >> 33) % movable.size()];
+            const int f1 = (int)((rng >> 17) % (uint64_t)deg[l]);
+            int f2 = (int)((rng >> 45) % (uint64_t)(deg[l] - 1));
+            if (f2 >= f1) ++f2;
+            std::swap(A[(size_t)l * DV + f1], A[(size_t)l * DV + f2]);
+            const int c1 = round_cost(h0, f1), c2 = round_cost(h0, f2);
+            if (c1 + c2 <= cost[f1] + cost[f2]) {
+                cost[f1] = c1;
+                cost[f2] = c2;
+            } else {
+                std::swap(A[(size_t)l * DV + f1], A[(size_t)l * DV + f2]);
+            }
+        }
+        for (int f = 0; f < rounds; ++f) after += cost[f] / 4096;
+    }
+    return {before, after};
+}
+
 }  // namespace host
 }  // namespace ldpc

@@ -11,6 +11,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 #include "ldpc_nms.h"
@@ -89,6 +90,19 @@ int check_decode(const GraphTables& g, int64_t B, int64_t B_max, int32_t T_max, 
 int check_channel(int64_t B, int32_t n_vars, double sigma, int64_t offset, int32_t decoding_type,
                   int32_t q_bit, int32_t punct_start, int32_t punct_end, int32_t short_start,
                   int32_t short_end, float clip_llr);
+
+// Variable-phase edge order.  A variable lane reads (and rewrites) its slots in edge order f, one
+// LDS instruction per f for the whole wave; a half-wave (32 lanes) is served in one pass only
+// when its 32 dword addresses fall in distinct banks (dword mod 32; identical addresses
+// broadcast).  The slot layout is fixed by the check phase, but each lane may visit its own
+// edges in any order (S is a sum; the V->C write-back is per edge), so the order is chosen per
+// lane to minimise, over the rounds f, the largest number of distinct addresses sharing a bank:
+// a deterministic hill climb over swaps of two edges of one lane.  Real edges stay in positions
+// [0, degree) (the kernel treats positions below the wave's smallest degree as real).
+// A[l * DV + f]: byte address of lane l's edge f; deg[l]: its degree; rounds: the wave's largest
+// degree.  Returns the summed cost (cycles) before and after.
+std::pair<int, int> order_variable_edges(std::vector<uint32_t>& A, const std::vector<int>& deg, int DV,
+                                         int rounds);
 
 }  // namespace host
 }  // namespace ldpc

@@ -4,6 +4,7 @@
 //
 //   host_check selftest              argument-validation cases + randomized graphs / weights
 //   host_check tables FILE Z         the tables of a BaseGraph/*.txt proto as JSON on stdout
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -218,11 +219,74 @@ static int tables(const char* path, int z) {
     return failures ? 1 : 0;
 }
 
+
+// bit-sliced variable-phase edge order (order_variable_edges): every lane keeps its edges, real
+// edges stay in positions [0, degree), padding positions are untouched, the bank cost never rises,
+// and a half-wave of one cyclic column block plus a second block's lanes is made conflict-free
+static void vorder_cases(int rounds) {
+    uint64_t r = 12345;
+    auto rnd = [&](int n) { r = r * 6364136223846793005ull + 1442695040888963407ull; return (int)((r >> 33) % n); };
+    auto cost = [](const std::vector<uint32_t>& A, int DV, int nr) {
+        int c = 0;
+        for (int h0 = 0; h0 < 64; h0 += 32)
+            for (int f = 0; f < nr; ++f) {
+                std::vector<uint32_t> seen;
+                int cnt[32] = {0}, mx = 0;
+                for (int l = h0; l < h0 + 32; ++l) {
+                    const uint32_t a = A[(size_t)l * DV + f];
+                    if (std::find(seen.begin(), seen.end(), a) != seen.end()) continue;
+                    seen.push_back(a);
+                    mx = std::max(mx, ++cnt[(a >> 2) & 31]);
+                }
+                c += mx;
+            }
+        return c;
+    };
+    for (int it = 0; it < rounds; ++it) {
+        const int DV = 2 + rnd(7), nr = 1 + rnd(DV);
+        const uint32_t zero = 4u * 100000u;
+        std::vector<uint32_t> A((size_t)64 * DV, zero);
+        std::vector<int> deg(64, 0);
+        uint32_t next = 0;
+        for (int l = 0; l < 64; ++l) {
+            deg[l] = rnd(nr + 1);
+            for (int f = 0; f < deg[l]; ++f) { next += 1 + rnd(40); A[(size_t)l * DV + f] = 20u * next; }
+        }
+        const std::vector<uint32_t> A0 = A;
+        const int c0 = cost(A, DV, nr);
+        const std::pair<int, int> c = host::order_variable_edges(A, deg, DV, nr);
+        CHECK(c.first == c0 && c.second == cost(A, DV, nr) && c.second <= c.first);
+        for (int l = 0; l < 64; ++l) {
+            std::vector<uint32_t> a(A.begin() + (size_t)l * DV, A.begin() + (size_t)l * DV + deg[l]);
+            std::vector<uint32_t> b(A0.begin() + (size_t)l * DV, A0.begin() + (size_t)l * DV + deg[l]);
+            std::sort(a.begin(), a.end());
+            std::sort(b.begin(), b.end());
+            CHECK(a == b);
+            for (int f = deg[l]; f < DV; ++f) CHECK(A[(size_t)l * DV + f] == zero);
+        }
+    }
+    // lanes 0..23 of one column take banks 5l and 5(l + 8); lanes 24 + i of another column hold
+    // an edge on bank 5i and one on bank 5(24 + i), in the order that collides in both rounds
+    // (4 cycles); the reordered lanes 24..31 are conflict-free (2)
+    const int DV = 2;
+    std::vector<uint32_t> A((size_t)64 * DV, 4u * 100000u);
+    std::vector<int> deg(64, 0);
+    for (int l = 0; l < 32; ++l) {
+        deg[l] = 2;
+        const uint32_t i = (uint32_t)(l - 24);
+        A[(size_t)l * DV] = 20u * (l < 24 ? (uint32_t)l : 32u * 50u + i);
+        A[(size_t)l * DV + 1] = 20u * (l < 24 ? 32u * 70u + (uint32_t)l + 8u : 32u * 60u + 24u + i);
+    }
+    const std::pair<int, int> c = host::order_variable_edges(A, deg, DV, 2);
+    CHECK(c.first == 4 + 2 && c.second == 2 + 2);   // (the empty second half-wave: 1 per round)
+}
+
 int main(int argc, char** argv) {
     if (argc >= 4 && std::string(argv[1]) == "tables") return tables(argv[2], std::atoi(argv[3]));
     if (argc >= 2 && std::string(argv[1]) == "selftest") {
         validation_cases();
         fuzz(argc >= 3 ? std::atoi(argv[2]) : 3000);
+        vorder_cases(500);
         std::printf("host_check: %d failures\n", failures);
         return failures ? 1 : 0;
     }
