@@ -588,51 +588,10 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
             for (int f = 0; f < k.DVH; ++f) q[f] = pad_word;
             q[k.DVH] = 0xFFFFFFFFu;
         }
-    // variable-phase edge order per lane (host::order_variable_edges, as in bsl): the cost is
-    // the slot-word reads (one dword per slot, bank = slot mod 32); a word is passed as word << 2
-    // so that the byte-address banking of the search sees the slot and two lanes on the same
-    // edge word count once (check records < 2^14)
-    const char* eo = getenv("LDPC_BSC_VORDER");
-    const bool vorder = eo && atoi(eo) != 0;
-    std::vector<uint32_t> A;
-    std::vector<int> dl(64);
     for (int w = 0; w < NWp; ++w)
         for (int u = 0; u < k.VPL; ++u) {
             const int ch = p.vslot[(size_t)w * k.VPL + u];
             int dmax = 0, dmin = ch < 0 ? 0 : 1 << 30;
-            if (vorder && ch >= 0 && nc < (1 << 14)) {
-                // reorder the lanes' words first (in the table), the loop below leaves them
-                A.assign((size_t)64 * k.DVH, pad_word << 2);
-                std::fill(dl.begin(), dl.end(), 0);
-                int dm = 0;
-                for (int l = 0; l < 64; ++l) {
-                    const int o = 64 * ch + l;
-                    if (o >= nv) continue;
-                    const int v = p.vorder[o], j = v / z, hh = v - j * z;
-                    const int c0 = h.col_ptr[j], dv = h.col_ptr[j + 1] - c0;
-                    for (int f = 0; f < dv; ++f) {
-                        const int pe = h.col_pe[c0 + f], i = h.pe_row[pe];
-                        int hc = hh - h.pe_shift[pe];
-                        hc = hc < 0 ? hc + z : hc;
-                        A[(size_t)l * k.DVH + f] = (slot_of(i, pe - h.row_ptr[i], hc) | ((uint32_t)(i * z + hc) << 16)) << 2;
-                    }
-                    dl[l] = dv;
-                    dm = std::max(dm, dv);
-                }
-                host::order_variable_edges(A, dl, k.DVH, std::min(k.DVH, dm));
-                for (int l = 0; l < 64; ++l) {
-                    const int o = 64 * ch + l;
-                    if (o >= nv) { dmin = 0; continue; }
-                    uint32_t* q = &vn[((size_t)u * nl + 64 * w + l) * VNW];
-                    for (int f = 0; f < dl[l]; ++f) q[f] = A[(size_t)l * k.DVH + f] >> 2;
-                    q[k.DVH] = (uint32_t)p.vorder[o];
-                    dmax = std::max(dmax, dl[l]);
-                    dmin = std::min(dmin, dl[l]);
-                }
-                wdeg[2 * ((size_t)u * NWp + w)] = dmax;
-                wdeg[2 * ((size_t)u * NWp + w) + 1] = dmin;
-                continue;
-            }
             for (int l = 0; ch >= 0 && l < 64; ++l) {
                 const int o = 64 * ch + l;
                 if (o >= nv) { dmin = 0; continue; }
