@@ -44,7 +44,7 @@ struct BscArgs {
     int beta_id;                 // every beta is 1: Q(beta ch) = ch, no table
     const int32_t* row_ptr;
     const int32_t* row_lay;      // [M][2] slot layout (as bsl): first slot, j-block stride
-    const uint32_t* vn_tab;      // [VPL][64 nw][DVH + 1]: per edge slot | check << 16, variable
+    const uint32_t* vn_tab;      // [VPL][64 nw][DVH + 1]: per edge slot | (record offset / 16) << 16, variable
     const int32_t* vn_wdeg;      // [VPL][nw][2]
     const int32_t* cn_chunk;     // [nw][CPL]
     const uint32_t* cn_var;      // [chunks * 64][CVW] variables of the lane's edges (16-bit packed)
@@ -58,6 +58,13 @@ struct BscArgs {
 };
 
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
+// Check records in blocks of 16: the q1 words of records 16 b .. 16 b + 15 (256 B), then their q2
+// words (256 B), so q2 is q1 + 256 (an instruction offset) and a ds_read_b128 group of 16 lanes
+// on consecutive records covers 64 distinct banks (with 32-B records side by side it covered 32,
+// two-way).  Byte offset of record r inside REC:
+__host__ __device__ constexpr uint32_t rec_off(uint32_t r) { return ((r >> 4) << 9) + ((r & 15u) << 4); }
+constexpr uint32_t REC_Q2 = 256;
 typedef __attribute__((address_space(3))) v2u LdsD;
 __device__ __forceinline__ v2u lds_d(uint32_t addr) { return *reinterpret_cast<const LdsD*>(addr); }
 __device__ __forceinline__ void lds_dput(uint32_t addr, uint32_t x, uint32_t y) {
@@ -149,7 +156,8 @@ k_bsc(BscArgs a) {
     }
     if (tid == 0) a.bad[blockIdx.x] = 0u;
     // the zero edge / zero record (padding edges of the variable lanes), counters, tables
-    if (tid < 8) reinterpret_cast<uint32_t*>(smem + a.off_rec)[(size_t)a.n_checks * 8 + tid] = 0u;
+    if (tid < 8)
+        reinterpret_cast<uint32_t*>(smem + a.off_rec + rec_off((uint32_t)a.n_checks) + (tid >> 2) * REC_Q2)[tid & 3] = 0u;
     if (tid < 8) RED[tid] = (tid == 1) ? 0xFFFFFFFFu : 0u;
     for (int w = tid; w < AL; w += NT) ALUT[w] = a.alut[w];
     for (int w = tid; w < BL; w += NT) BLUT[w] = a.blut[w];
@@ -200,9 +208,9 @@ k_bsc(BscArgs a) {
                     if (f < dvu && f < dwu) {
                         const uint32_t wd = va[u][f];
                         const uint32_t sa = (wd & 0xFFFFu) << 2;
-                        const uint32_t ra = a.off_rec + ((wd >> 16) << 5);
+                        const uint32_t ra = a.off_rec + ((wd >> 16) << 4);
                         const uint32_t n = lds_w(sa), am = lds_w(sa + a.off_a);
-                        const v4u q1 = lds_q(ra), q2 = lds_q(ra + 16);
+                        const v4u q1 = lds_q(ra), q2 = lds_q(ra + REC_Q2);
                         uint32_t b[4];
                         b[0] = mux(am, q2.x, q1.x) ^ n;
                         b[1] = mux(am, q2.y, q1.y) ^ n;
@@ -284,7 +292,7 @@ k_bsc(BscArgs a) {
         gm[c] = __popc(wave_or((1u << ((gdeg[c] + LPC - 1) / LPC)) - 1u));
         (void)nwv;
         gslot[c] = (uint32_t)(4 * (a.row_lay[2 * ci] + cj * a.row_lay[2 * ci + 1] + (cc - ci * a.z)));
-        grec[c] = a.off_rec + 32u * (uint32_t)min(cc, a.n_checks - 1);
+        grec[c] = a.off_rec + rec_off((uint32_t)min(cc, a.n_checks - 1));
         gtab[c] = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * OB * 64);
 #pragma unroll
         for (int p = 0; p < CVW; ++p) gvar[c][p] = gchunk[c] >= 0 ? a.cn_var[(size_t)ql * CVW + p] : 0u;
@@ -327,7 +335,7 @@ k_bsc(BscArgs a) {
             v4u q1o = {0u, 0u, 0u, 0u}, q2o = {0u, 0u, 0u, 0u};
             if (t > 0) {
                 q1o = lds_q(grec[c]);
-                q2o = lds_q(grec[c] + 16);
+                q2o = lds_q(grec[c] + REC_Q2);
             }
             uint32_t Xs[EPL][4], ns[EPL];
 #pragma unroll
@@ -417,7 +425,7 @@ k_bsc(BscArgs a) {
 #pragma unroll
                 for (int b = 0; b < OB; ++b) {
                     lds_put(grec[c] + 4u * (uint32_t)(OB * cj + b), qb[b][0]);
-                    lds_put(grec[c] + 16u + 4u * (uint32_t)(OB * cj + b), qb[b][1]);
+                    lds_put(grec[c] + REC_Q2 + 4u * (uint32_t)(OB * cj + b), qb[b][1]);
                 }
             }
             // per edge: the C->V sign (par ^ own V->C sign, :251-254) and [|V->C| == min]
@@ -541,14 +549,16 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
         const float cu = clip / bs_step(mode);
         q.cu = cu > (float)bs_qmax(mode) ? cu : -1.f;
         q.lay = slot_layout(h, k.LPC, &q.nslot);
-        // LDS: SGN [nslot + 1] | ARG [nslot + 1] | REC [nc + 1][8] | TV [nv][6] | RED | ALUT | BLUT
+        // LDS: SGN [nslot + 1] | ARG [nslot + 1] | REC [(nc + 1) / 16 blocks][2][16][4] | TV [nv][6] |
+        // RED | ALUT | BLUT
         const size_t sgn = ((q.nslot + 1) * 4 + 127) & ~(size_t)127;
         if (q.nslot + 1 > 65535) continue;
         q.off_a = (uint32_t)sgn;
         size_t o = 2 * sgn;
         q.off_rec = (uint32_t)o;
-        o += (size_t)(nc + 1) * 32;
+        o += (size_t)((nc + 1 + 15) / 16) * 512;
         q.off_tv = (uint32_t)o;
+        if ((rec_off((uint32_t)nc) >> 4) > 65535) continue;     // 16-bit record field
         o += (size_t)nv * 24;
         o = (o + 15) & ~(size_t)15;
         q.off_red = (uint32_t)o;
@@ -579,7 +589,7 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     auto slot_of = [&](int i, int kk, int hc) {
         return (uint32_t)((size_t)p.lay[2 * i] + (size_t)(kk % LPC) * p.lay[2 * i + 1] + (size_t)(kk / LPC) * z + hc);
     };
-    const uint32_t pad_word = (uint32_t)p.nslot | ((uint32_t)nc << 16);    // zero slot, zero record
+    const uint32_t pad_word = (uint32_t)p.nslot | ((rec_off((uint32_t)nc) >> 4) << 16);    // zero slot, zero record
     std::vector<uint32_t> vn((size_t)k.VPL * nl * VNW, 0u);
     std::vector<int32_t> wdeg((size_t)2 * k.VPL * NWp, 0);
     for (int u = 0; u < k.VPL; ++u)
@@ -602,7 +612,7 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
                     const int pe = h.col_pe[c0 + f], i = h.pe_row[pe];
                     int hc = hh - h.pe_shift[pe];
                     hc = hc < 0 ? hc + z : hc;
-                    q[f] = slot_of(i, pe - h.row_ptr[i], hc) | ((uint32_t)(i * z + hc) << 16);
+                    q[f] = slot_of(i, pe - h.row_ptr[i], hc) | ((rec_off((uint32_t)(i * z + hc)) >> 4) << 16);
                 }
                 q[k.DVH] = (uint32_t)v;
                 dmax = std::max(dmax, dv);
