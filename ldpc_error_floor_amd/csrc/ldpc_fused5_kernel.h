@@ -225,7 +225,7 @@ struct Sel {
 // diagnostic phase marks: wave 0 lane 0 of each workgroup records s_memrealtime (100 MHz)
 #define F5_STAMP(i)                                                                         \
     do {                                                                                    \
-        if (a.stamps && tid == 0) a.stamps[(size_t)blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if (a.stamps && tid == 0) a.stamps[(size_t)bx * 32 + (i)] = __builtin_amdgcn_s_memrealtime();       \
     } while (0)
 
 // per-slot degree bound: a wave's first HG group slots take rows of degree <= MAXDEG, the
@@ -242,8 +242,8 @@ constexpr int f5_logcw(int cw) { return cw == 64 ? 6 : cw == 32 ? 5 : cw == 16 ?
 // WPE: the shape's occupancy target (waves per SIMD): the VGPR budget that lets the planned
 // number of workgroups share a CU (Shape5::wpe; plan5 assumes the same figure)
 template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, int WPE, bool UCN, bool PEW, bool OUT, bool LUT>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE)))
-k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ alpha_ucn) {
+__device__ __forceinline__ void
+f5_block(const F5Args& a, const float* __restrict__ alpha, const float* __restrict__ alpha_ucn, const int64_t bx) {
     using SL = Sel<MAXDEG>;                 // selector layout of every slot (light ones use a prefix)
     using GD = GDeg<MAXDEG, HG, LDEG>;
     constexpr int NSEL = SL::NSEL;
@@ -263,14 +263,14 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
     uint16_t* QT = reinterpret_cast<uint16_t*>(RED + 8);                          // [2][qslice]
 
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();   // edge addresses are LDS-absolute
-    if (a.only && a.only[((int64_t)blockIdx.x * CW) >> 5] == 0u) return;   // bit-sliced fixup
+    if (a.only && a.only[(bx * CW) >> 5] == 0u) return;   // bit-sliced fixup
     const int tid = threadIdx.x;
     const int NT = blockDim.x;
     const int NWV = NT >> 6;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int cw = lane & (CW - 1);
-    const int64_t b0 = (int64_t)blockIdx.x * CW;
+    const int64_t b0 = bx * CW;
     const int64_t nvalid = (b0 + CW <= a.B) ? CW : (a.B - b0);
     const unsigned long long cwmask = (CW == 64) ? ~0ull : ((1ull << CW) - 1);
     const unsigned long long valid_cw = (nvalid >= 64) ? ~0ull : ((1ull << nvalid) - 1);
@@ -802,7 +802,7 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         uint32_t hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        a.stamps[(size_t)blockIdx.x * 32 + 31] = ((unsigned long long)xcc << 32) | hw;
+        a.stamps[(size_t)bx * 32 + 31] = ((unsigned long long)xcc << 32) | hw;
     }
     if (tid == 0) {
         const unsigned long long wl = RED[0] & valid_cw;
@@ -826,6 +826,37 @@ k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ al
         __syncthreads();
         if (tid < nvalid)
             a.flags[b0 + tid] = (uint8_t)(((RED[5] >> tid) & 1) | (((RED[6] >> tid) & 1) << 1));
+    }
+}
+
+template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, int WPE, bool UCN, bool PEW, bool OUT, bool LUT>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_fused5(F5Args a, const float* __restrict__ alpha, const float* __restrict__ alpha_ucn) {
+    f5_block<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>(a, alpha, alpha_ucn, (int64_t)blockIdx.x);
+}
+
+// The bit-sliced kernels' fixup (a.only set): a grid of at most a few workgroups per CU walks the
+// blocks and decodes those of flagged packs.  One workgroup per block (k_fused5 with a.only)
+// launched the full 2^20 / CW grid, whose workgroups almost all exit at once: 59 us per C2
+// decode (1 % of it) for the dispatch alone.
+template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, int WPE, bool UCN, bool PEW, bool OUT, bool LUT>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_fused5_fix(F5Args a, const float* __restrict__ alpha, const float* __restrict__ alpha_ucn, int64_t nblk) {
+    // the flags of 64 of the workgroup's blocks per round, one per lane, loaded at once (every
+    // wave takes the same ballot, so the list is uniform without LDS); walking the blocks one
+    // flag load at a time cost 66 us per C2 decode in load latency alone
+    const int lane = threadIdx.x & 63;
+    for (int64_t base = blockIdx.x; base < nblk; base += 64 * (int64_t)gridDim.x) {
+        const int64_t cand = base + (int64_t)lane * gridDim.x;
+        const bool flagged = cand < nblk && a.only[(cand * CW) >> 5] != 0u;
+        unsigned long long m = __ballot(flagged);
+        while (m) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            f5_block<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>(a, alpha, alpha_ucn,
+                                                                        base + (int64_t)l * gridDim.x);
+            __syncthreads();
+        }
     }
 }
 
@@ -855,6 +886,8 @@ constexpr Shape5 kShapes5[] = {
     // 23.1 ms vs 18.7 ms; {4, 2, 24} (802.11n, 4 waves, seven WGs per CU) within 0.3% of {8, 2, 24}
 };
 
+constexpr int F5_FIX_GRID = 512;      // fixup grid (k_fused5_fix): two workgroups per CU
+
 template <int CW, int MAXG, int MAXDEG, int HG, int LDEG, int WPE, bool UCN, bool PEW, bool OUT, bool LUT>
 int launch5o(const F5Args& a, int nblocks, int nw, size_t lds, const float* alpha,
              const float* alpha_ucn, hipStream_t s) {
@@ -863,6 +896,18 @@ int launch5o(const F5Args& a, int nblocks, int nw, size_t lds, const float* alph
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused5<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)F5_LDS_MAX);
         attr = true;
+    }
+    if (a.only && !OUT) {
+        static bool attr_fix = false;
+        if (!attr_fix) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused5_fix<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)F5_LDS_MAX);
+            attr_fix = true;
+        }
+        const int grid = nblocks < F5_FIX_GRID ? nblocks : F5_FIX_GRID;
+        hipLaunchKernelGGL((k_fused5_fix<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>), dim3(grid), dim3(64 * nw), lds, s,
+                           a, alpha, alpha_ucn, (int64_t)nblocks);
+        return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
     }
     hipLaunchKernelGGL((k_fused5<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>), dim3(nblocks), dim3(64 * nw), lds, s,
                        a, alpha, alpha_ucn);

@@ -81,6 +81,25 @@ def test_off_grid_packs_fall_back_exactly(cuda_device, lpc):
     torch.cuda.synchronize()
 
 
+def test_off_grid_packs_many_blocks_per_fixup_workgroup(cuda_device):
+    """The v5 fixup walks more blocks than its grid has workgroups (k_fused5_fix: 512
+    workgroups, each taking the flags of 64 of its blocks per ballot): 2^20 codewords are 65,536
+    v5 blocks of 16, 128 per workgroup in two ballots; off-grid packs on several lanes of both of
+    one workgroup's ballots (blocks 5 + 512 k), in both halves of a pack, and the last pack."""
+    import torch
+    dec, cp = _wman(cuda_device)
+    B = 1 << 20
+    llr = dec.awgn(B, float(cp.sigma(2.5)), seed=21)
+    for k in (0, 1, 7, 63, 64, 100, 127):
+        llr[16 * (5 + 512 * k) + 3, 10 + k] += 0.1       # block 5 + 512 k
+    llr[16 * 1023 + 15, 0] = 40.0                        # the second block of a pack
+    llr[B - 1, 5] = -0.2
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
+    torch.cuda.synchronize()
+
+
 # ---- the large / UCN instances: 802.11n (C3: degree 22, [3,3,3] UCN, T=50) and 5G BG2 (C4:
 # 1,280 variables, [2,2,2] UCN per row and column, puncture and shortening) --------------------
 def _config(device, cfg, T=None):
