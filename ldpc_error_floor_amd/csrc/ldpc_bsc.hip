@@ -108,10 +108,10 @@ k_bsc(BscArgs a) {
         const uint32_t* vt = a.vn_tab + ((size_t)u * NT + tid) * VNW;
 #pragma unroll
         for (int p = 0; p < DVH; ++p) va[u][p] = (p < dvu) ? vt[p] : 0u;
-        vv[u] = (int)vt[DVH];
+        vv[u] = (int)vt[DVH];                                // v | Tv index << 16, or -1
         dw[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave)]);
         dwmin[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave) + 1]);
-        tab_b[u] = (a.bcols > 1 && vv[u] >= 0) ? (uint32_t)((vv[u] / (nv / a.bcols)) * BLUT_W * 4) : 0u;
+        tab_b[u] = (a.bcols > 1 && vv[u] >= 0) ? (uint32_t)(((vv[u] & 0xFFFF) / (nv / a.bcols)) * BLUT_W * 4) : 0u;
     }
     (void)dwmin;
 
@@ -127,7 +127,7 @@ k_bsc(BscArgs a) {
         bg[u] = 0u;
 #pragma unroll
         for (int p = 0; p < 4; ++p) cm[u][p] = 0u;
-        const int v = vv[u];
+        const int v = vv[u] < 0 ? -1 : (vv[u] & 0xFFFF);
         if (v >= 0) {
             const float* src = a.llr + b0 * nv + v;
             float xv[PACK];
@@ -175,7 +175,7 @@ k_bsc(BscArgs a) {
 #pragma unroll
             for (int p = 0; p < DVH; ++p)
                 if (p < dvu) asm volatile("" : "+v"(va[u][p]));
-            const int v = vv[u];
+            const int v = vv[u] < 0 ? -1 : (vv[u] & 0xFFFF);
             const bool counted = v >= 0 && v < a.target_bits;
             uint32_t lw[1][4];
             if (!last) {
@@ -253,7 +253,7 @@ k_bsc(BscArgs a) {
             add_b<SB>(S, lb, cs[u]);
             uint32_t Tv[6];
             clamp6<SB>(Tv, S);
-            const uint32_t ta = a.off_tv + 24u * (uint32_t)v;
+            const uint32_t ta = a.off_tv + 24u * ((uint32_t)vv[u] >> 16);     // the Tv index
             lds_dput(ta, Tv[0], Tv[1]);
             lds_dput(ta + 8, Tv[2], Tv[3]);
             lds_dput(ta + 16, Tv[4], Tv[5]);
@@ -553,6 +553,7 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
         // RED | ALUT | BLUT
         const size_t sgn = ((q.nslot + 1) * 4 + 127) & ~(size_t)127;
         if (q.nslot + 1 > 65535) continue;
+        if (nv > 32767) continue;                // v | Tv index << 16 as a non-negative int
         q.off_a = (uint32_t)sgn;
         size_t o = 2 * sgn;
         q.off_rec = (uint32_t)o;
@@ -589,6 +590,78 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     auto slot_of = [&](int i, int kk, int hc) {
         return (uint32_t)((size_t)p.lay[2 * i] + (size_t)(kk % LPC) * p.lay[2 * i + 1] + (size_t)(kk / LPC) * z + hc);
     };
+    // Tv slots: variable (column j, index hh) keeps its Tv at j z + (hh + toff_j) mod z.  The
+    // check phase reads the Tv of each lane's edge m (ds_read_b64, bank = dword mod 64, 6 dwords
+    // per variable: 32 lanes are conflict-free when their Tv indices differ mod 32); a half-wave
+    // holds 8 consecutive checks of 4 edges, i.e. 4 runs of 8 consecutive indices from 4
+    // columns, which overlap mod 32 for most column offsets.  A hill climb over the per-column
+    // rotations toff_j spreads them (BG1: 695 -> ~514 LDS cycles per Tv read round of a
+    // check pass in tools/bank_model's terms); the variable phase writes the same slot.
+    std::vector<int> toff(h.N, 0);
+    {
+        const char* e = getenv("LDPC_BSC_TVPERM");
+        const bool on = !(e && atoi(e) == 0);
+        std::vector<std::vector<std::pair<int, int>>> grp;          // (column, hh) per round
+        std::vector<std::vector<int>> bycol(h.N);
+        for (int h0 = 0; on && h0 < p.cn_lanes; h0 += 32)
+            for (int m = 0; m < EPL; ++m) {
+                std::vector<std::pair<int, int>> gl;
+                for (int ql = h0; ql < h0 + 32; ++ql) {
+                    const int cc = ql / LPC, cj = ql % LPC;
+                    if (cc >= nc) continue;
+                    const int i = cc / z, hc = cc - i * z, kk = LPC * m + cj;
+                    if (kk >= h.row_ptr[i + 1] - h.row_ptr[i]) continue;
+                    const int pe = h.row_ptr[i] + kk;
+                    gl.emplace_back(h.pe_col[pe], (hc + h.pe_shift[pe]) % z);
+                }
+                if (gl.empty()) continue;
+                for (const auto& x : gl)
+                    if (bycol[x.first].empty() || bycol[x.first].back() != (int)grp.size())
+                        bycol[x.first].push_back((int)grp.size());
+                grp.push_back(std::move(gl));
+            }
+        auto gcost = [&](const std::vector<std::pair<int, int>>& gl) {
+            int cnt[32] = {0}, mx = 0, sq = 0;
+            uint32_t seen[32];
+            int ns = 0;
+            for (const auto& x : gl) {
+                const uint32_t t = (uint32_t)(x.first * z + (x.second + toff[x.first]) % z);
+                bool dup = false;
+                for (int q = 0; q < ns && !dup; ++q) dup = seen[q] == t;
+                if (dup) continue;
+                seen[ns++] = t;
+                const int c = ++cnt[t & 31];
+                mx = std::max(mx, c);
+                sq += 2 * c - 1;
+            }
+            return mx * 4096 + sq;
+        };
+        std::vector<int> cost(grp.size());
+        for (size_t gi = 0; gi < grp.size(); ++gi) cost[gi] = gcost(grp[gi]);
+        uint64_t rng = 0x2545F4914F6CDD1Dull;
+        for (int it = 0; on && it < 20000; ++it) {
+            rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+            const int j = (int)((rng >> 33) % (uint64_t)h.N);
+            if (bycol[j].empty()) continue;
+            const int old = toff[j];
+            toff[j] = (int)((rng >> 13) % (uint64_t)z);
+            int before = 0, after = 0;
+            std::vector<int> nc2(bycol[j].size());
+            for (size_t q = 0; q < bycol[j].size(); ++q) {
+                before += cost[bycol[j][q]];
+                after += nc2[q] = gcost(grp[bycol[j][q]]);
+            }
+            if (after <= before) {
+                for (size_t q = 0; q < bycol[j].size(); ++q) cost[bycol[j][q]] = nc2[q];
+            } else {
+                toff[j] = old;
+            }
+        }
+    }
+    auto tv_index = [&](int v) -> uint32_t {
+        const int j = v / z, hh = v - j * z;
+        return (uint32_t)(j * z + (hh + toff[j]) % z);
+    };
     const uint32_t pad_word = (uint32_t)p.nslot | ((rec_off((uint32_t)nc) >> 4) << 16);    // zero slot, zero record
     std::vector<uint32_t> vn((size_t)k.VPL * nl * VNW, 0u);
     std::vector<int32_t> wdeg((size_t)2 * k.VPL * NWp, 0);
@@ -614,7 +687,7 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
                     hc = hc < 0 ? hc + z : hc;
                     q[f] = slot_of(i, pe - h.row_ptr[i], hc) | ((rec_off((uint32_t)(i * z + hc)) >> 4) << 16);
                 }
-                q[k.DVH] = (uint32_t)v;
+                q[k.DVH] = (uint32_t)v | (tv_index(v) << 16);
                 dmax = std::max(dmax, dv);
                 dmin = std::min(dmin, dv);
             }
@@ -638,7 +711,7 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
             const int kk = LPC * m + cj;
             if (kk >= h.row_ptr[i + 1] - h.row_ptr[i]) continue;
             const int pe = h.row_ptr[i] + kk;
-            const uint32_t v = (uint32_t)(h.pe_col[pe] * z + (hc + h.pe_shift[pe]) % z);
+            const uint32_t v = tv_index(h.pe_col[pe] * z + (hc + h.pe_shift[pe]) % z);
             cvar[(size_t)ql * CVW + (m >> 1)] |= v << (16 * (m & 1));
         }
     }
