@@ -261,6 +261,77 @@ std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch) 
     return cost;
 }
 
+// Per-column rotation of a per-variable LDS array (bsc: Tv, 6 dwords per variable; bsl UCN: the
+// hard decisions, 1 dword) read by the check lanes: variable (column j, index hh) is stored at
+// j z + (hh + toff_j) mod z.  A half-wave of check lanes (32 / LPC consecutive checks, LPC edges
+// each) reads, for edge position m, LPC runs of consecutive variables from LPC columns, which
+// overlap mod 32 (the bank, for b32 reads and for b64 reads of 6-dword records alike) for most
+// column pairs; a hill climb over the toff_j (the cost of a round: the most distinct indices on
+// one bank, the sum of squared bank loads as the tie-break) spreads them.
+std::vector<int> column_rotation(const host::GraphTables& h, int LPC, int EPL, int cn_lanes) {
+    const int z = h.z, nc = h.M * h.z;
+    std::vector<int> toff(h.N, 0);
+    {
+        std::vector<std::vector<std::pair<int, int>>> grp;          // (column, hh) per round
+        std::vector<std::vector<int>> bycol(h.N);
+        for (int h0 = 0; h0 < cn_lanes; h0 += 32)
+            for (int m = 0; m < EPL; ++m) {
+                std::vector<std::pair<int, int>> gl;
+                for (int ql = h0; ql < h0 + 32; ++ql) {
+                    const int cc = ql / LPC, cj = ql % LPC;
+                    if (cc >= nc) continue;
+                    const int i = cc / z, hc = cc - i * z, kk = LPC * m + cj;
+                    if (kk >= h.row_ptr[i + 1] - h.row_ptr[i]) continue;
+                    const int pe = h.row_ptr[i] + kk;
+                    gl.emplace_back(h.pe_col[pe], (hc + h.pe_shift[pe]) % z);
+                }
+                if (gl.empty()) continue;
+                for (const auto& x : gl)
+                    if (bycol[x.first].empty() || bycol[x.first].back() != (int)grp.size())
+                        bycol[x.first].push_back((int)grp.size());
+                grp.push_back(std::move(gl));
+            }
+        auto gcost = [&](const std::vector<std::pair<int, int>>& gl) {
+            int cnt[32] = {0}, mx = 0, sq = 0;
+            uint32_t seen[32];
+            int ns = 0;
+            for (const auto& x : gl) {
+                const uint32_t t = (uint32_t)(x.first * z + (x.second + toff[x.first]) % z);
+                bool dup = false;
+                for (int q = 0; q < ns && !dup; ++q) dup = seen[q] == t;
+                if (dup) continue;
+                seen[ns++] = t;
+                const int c = ++cnt[t & 31];
+                mx = std::max(mx, c);
+                sq += 2 * c - 1;
+            }
+            return mx * 4096 + sq;
+        };
+        std::vector<int> cost(grp.size());
+        for (size_t gi = 0; gi < grp.size(); ++gi) cost[gi] = gcost(grp[gi]);
+        uint64_t rng = 0x2545F4914F6CDD1Dull;
+        for (int it = 0; it < 20000; ++it) {
+            rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+            const int j = (int)((rng >> 33) % (uint64_t)h.N);
+            if (bycol[j].empty()) continue;
+            const int old = toff[j];
+            toff[j] = (int)((rng >> 13) % (uint64_t)z);
+            int before = 0, after = 0;
+            std::vector<int> nc2(bycol[j].size());
+            for (size_t q = 0; q < bycol[j].size(); ++q) {
+                before += cost[bycol[j][q]];
+                after += nc2[q] = gcost(grp[bycol[j][q]]);
+            }
+            if (after <= before) {
+                for (size_t q = 0; q < bycol[j].size(); ++q) cost[bycol[j][q]] = nc2[q];
+            } else {
+                toff[j] = old;
+            }
+        }
+    }
+    return toff;
+}
+
 // the per-decode weight tables of both bit-sliced kernels (k_bs_tables)
 int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, int qmax,
                    float cu, bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s) {
@@ -330,6 +401,16 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
             for (int f = 0; f < DV; ++f) put(q, f, p.off_zero);
             q[VNA] = 0xFFFFFFFFu;
         }
+    // UCN instances: the hard decisions HD live at a per-column rotation of the variable index
+    // (column_rotation: the check lanes' b32 reads of HD spread over the banks); a variable
+    // lane's table word carries it as v | (HD index << 16)
+    const char* ehd = getenv("LDPC_BS_HDPERM");
+    const std::vector<int> hoff = (k.UCN && !(ehd && atoi(ehd) == 0))
+                                      ? column_rotation(h, LPC, EPL, p.cn_lanes) : std::vector<int>(h.N, 0);
+    auto hd_index = [&](int v) -> uint32_t {
+        const int j = v / z, hh = v - j * z;
+        return (uint32_t)(j * z + (hh + hoff[j]) % z);
+    };
     const char* eo = getenv("LDPC_BS_VORDER");       // A/B: 0 keeps the graph's edge order
     const bool vorder = !(eo && atoi(eo) == 0);
     int vcost_before = 0, vcost_after = 0;
@@ -369,7 +450,7 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
                 uint32_t* q = &vn[((size_t)u * nl + 64 * w + l) * VNW];
                 for (int pw = 0; pw < VNA; ++pw) q[pw] = 0u;
                 for (int f = 0; f < DV; ++f) put(q, f, A[(size_t)l * DV + f]);
-                q[VNA] = (uint32_t)order[o];
+                q[VNA] = k.UCN ? ((uint32_t)order[o] | (hd_index(order[o]) << 16)) : (uint32_t)order[o];
             }
             wdeg[2 * ((size_t)u * p.nw + w)] = dmax;
             wdeg[2 * ((size_t)u * p.nw + w) + 1] = dmin;
@@ -401,7 +482,7 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
                     if (kk < h.row_ptr[i + 1] - h.row_ptr[i]) {
                         const int pe = h.row_ptr[i] + kk;
                         const int v = h.pe_col[pe] * z + (hc + h.pe_shift[pe]) % z;
-                        addr = (uint32_t)(4 * v);
+                        addr = 4 * hd_index(v);
                     }
                 }
                 chd[(size_t)ql * HDW + (m >> 1)] |= addr << (16 * (m & 1));

@@ -399,10 +399,10 @@ k_bs(BsArgs a) {
         const uint32_t* vt = a.vn_tab + ((size_t)u * NT + tid) * VNW;
 #pragma unroll
         for (int p = 0; p < VNA; ++p) va[u][p] = vt[p];
-        vv[u] = (int)vt[VNA];                                // -1: no variable
+        vv[u] = (int)vt[VNA];                                // -1: no variable (UCN: v | HD index << 16)
         dw[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave)]);
         dwmin[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave) + 1]);
-        tab_b[u] = (a.bcols > 1 && vv[u] >= 0) ? (uint32_t)((vv[u] / (nv / a.bcols)) * BLUT_W * 4) : 0u;
+        tab_b[u] = (a.bcols > 1 && vv[u] >= 0) ? (uint32_t)(((UCN ? (vv[u] & 0xFFFF) : vv[u]) / (nv / a.bcols)) * BLUT_W * 4) : 0u;
     }
     int cn_dmin = a.cn_dmin;
 
@@ -419,7 +419,7 @@ k_bs(BsArgs a) {
         bg[u] = 0u;
 #pragma unroll
         for (int p = 0; p < 4; ++p) cm[u][p] = 0u;
-        const int v = vv[u];
+        const int v = (UCN && vv[u] >= 0) ? (vv[u] & 0xFFFF) : vv[u];
         if (v >= 0 && !ABL(32)) {
             const float* src = a.llr + b0 * nv + v;
             // all 32 loads issued before any use: one HBM round trip per workgroup prologue (with
@@ -480,7 +480,8 @@ k_bs(BsArgs a) {
                 if constexpr (PK) return (f & 1) ? (va[u][f >> 1] >> 16) : (va[u][f >> 1] & 0xFFFFu);
                 else return va[u][f];
             };
-            const int v = vv[u];
+            const int v = (UCN && vv[u] >= 0) ? (vv[u] & 0xFFFF) : vv[u];
+            const uint32_t hda = UCN ? 4u * ((uint32_t)vv[u] >> 16) : 0u;     // HD slot (rotated)
             const bool counted = v >= 0 && v < a.target_bits;
             uint32_t lw[1][4];                   // |Q(beta_{t+1} ch)| (before the C->V: fewer live registers)
             if (!last) {
@@ -552,7 +553,7 @@ k_bs(BsArgs a) {
                     for (int i = 0; i < SB - 1; ++i) c = B3(T_MAJ, S[i], i < 4 ? (cm[u][i] ^ c_s) : c_s, c);
                     hd = B3(T_XNOR3, S[SB - 1], c_s, c);
                 }
-                if (UCN && !last && ucn && v >= 0) lds_put((uint32_t)(4 * v), hd);   // HD[v] (Main_Functions.py:184-188)
+                if (UCN && !last && ucn && v >= 0) lds_put(hda, hd);   // HD[v] (Main_Functions.py:184-188)
                 hd &= valid;                                     // APP >= 0 -> hard decision 1
                 if (ABL(8)) hd = 0u;
                 if (counted) {
@@ -574,7 +575,7 @@ k_bs(BsArgs a) {
             const int dwm = dwmin[u];
             if (first) {
                 // UCN at t = 0: the hard decision of x~ = Q(beta_0 ch) (Main_Functions.py:181-182)
-                if (UCN && ucn && v >= 0) lds_put((uint32_t)(4 * v), ~Tv[5]);
+                if (UCN && ucn && v >= 0) lds_put(hda, ~Tv[5]);
                 uint32_t x[7], X[4];
 #pragma unroll
                 for (int i = 0; i < 7; ++i) x[i] = Tv[i < 6 ? i : 5];

@@ -482,6 +482,7 @@ namespace bs {
 std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* nslot);
 std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap);
 std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch);
+std::vector<int> column_rotation(const host::GraphTables& h, int LPC, int EPL, int cn_lanes);
 int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, int qmax,
                    float cu, bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s);
 bool bs_mode(int mode);
@@ -597,67 +598,9 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     // columns, which overlap mod 32 for most column offsets.  A hill climb over the per-column
     // rotations toff_j spreads them (BG1: 695 -> ~514 LDS cycles per Tv read round of a
     // check pass in tools/bank_model's terms); the variable phase writes the same slot.
-    std::vector<int> toff(h.N, 0);
-    {
-        const char* e = getenv("LDPC_BSC_TVPERM");
-        const bool on = !(e && atoi(e) == 0);
-        std::vector<std::vector<std::pair<int, int>>> grp;          // (column, hh) per round
-        std::vector<std::vector<int>> bycol(h.N);
-        for (int h0 = 0; on && h0 < p.cn_lanes; h0 += 32)
-            for (int m = 0; m < EPL; ++m) {
-                std::vector<std::pair<int, int>> gl;
-                for (int ql = h0; ql < h0 + 32; ++ql) {
-                    const int cc = ql / LPC, cj = ql % LPC;
-                    if (cc >= nc) continue;
-                    const int i = cc / z, hc = cc - i * z, kk = LPC * m + cj;
-                    if (kk >= h.row_ptr[i + 1] - h.row_ptr[i]) continue;
-                    const int pe = h.row_ptr[i] + kk;
-                    gl.emplace_back(h.pe_col[pe], (hc + h.pe_shift[pe]) % z);
-                }
-                if (gl.empty()) continue;
-                for (const auto& x : gl)
-                    if (bycol[x.first].empty() || bycol[x.first].back() != (int)grp.size())
-                        bycol[x.first].push_back((int)grp.size());
-                grp.push_back(std::move(gl));
-            }
-        auto gcost = [&](const std::vector<std::pair<int, int>>& gl) {
-            int cnt[32] = {0}, mx = 0, sq = 0;
-            uint32_t seen[32];
-            int ns = 0;
-            for (const auto& x : gl) {
-                const uint32_t t = (uint32_t)(x.first * z + (x.second + toff[x.first]) % z);
-                bool dup = false;
-                for (int q = 0; q < ns && !dup; ++q) dup = seen[q] == t;
-                if (dup) continue;
-                seen[ns++] = t;
-                const int c = ++cnt[t & 31];
-                mx = std::max(mx, c);
-                sq += 2 * c - 1;
-            }
-            return mx * 4096 + sq;
-        };
-        std::vector<int> cost(grp.size());
-        for (size_t gi = 0; gi < grp.size(); ++gi) cost[gi] = gcost(grp[gi]);
-        uint64_t rng = 0x2545F4914F6CDD1Dull;
-        for (int it = 0; on && it < 20000; ++it) {
-            rng = rng * 6364136223846793005ull + 1442695040888963407ull;
-            const int j = (int)((rng >> 33) % (uint64_t)h.N);
-            if (bycol[j].empty()) continue;
-            const int old = toff[j];
-            toff[j] = (int)((rng >> 13) % (uint64_t)z);
-            int before = 0, after = 0;
-            std::vector<int> nc2(bycol[j].size());
-            for (size_t q = 0; q < bycol[j].size(); ++q) {
-                before += cost[bycol[j][q]];
-                after += nc2[q] = gcost(grp[bycol[j][q]]);
-            }
-            if (after <= before) {
-                for (size_t q = 0; q < bycol[j].size(); ++q) cost[bycol[j][q]] = nc2[q];
-            } else {
-                toff[j] = old;
-            }
-        }
-    }
+    const char* etv = getenv("LDPC_BSC_TVPERM");
+    const std::vector<int> toff = (etv && atoi(etv) == 0) ? std::vector<int>(h.N, 0)
+                                                           : column_rotation(h, LPC, EPL, p.cn_lanes);
     auto tv_index = [&](int v) -> uint32_t {
         const int j = v / z, hh = v - j * z;
         return (uint32_t)(j * z + (hh + toff[j]) % z);
