@@ -354,8 +354,13 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
 #else
 #define ABL(bit) 0
 #endif
+// C->V messages of a variable lane's first BS_KEEP edges kept in registers from the sum pass to
+// the V->C pass (the others are read from their slots again).  Measured per instance, same box,
+// 2 rounds (tools/bs_variant.sh -DBS_KEEP=k): C2 5.79 (0) / 5.70 (1) / 5.58 (2) / 5.56 (3) /
+// 5.55 (4) / 5.71 ms (6); C3 18.75 / 18.53 / 18.25 / 17.80 / 17.76 / 17.75; C4 18.15 / 17.97 /
+// 17.81 / 17.76 / 17.67 / 17.62 ms.
 #ifndef BS_KEEP
-#define BS_KEEP 0
+#define BS_KEEP 4
 #endif
 
 // Register budget: the small instances run at 64 VGPRs (WPE 8: three 9-wave workgroups per CU).
@@ -510,7 +515,7 @@ k_bs(BsArgs a) {
                 }
             }
             // C->V of the first KEEP edges stay in registers for the V->C pass, the others are read
-            // again (the register budget of three 9-wave workgroups per CU)
+            // again (BS_KEEP: 4 measured best within the 64-register budget)
             constexpr int KEEP = BS_KEEP < DV ? BS_KEEP : DV;
             uint32_t mn[KEEP > 0 ? KEEP : 1], mb[KEEP > 0 ? KEEP : 1][4];
             uint32_t S[SB];

@@ -897,17 +897,19 @@ int launch5o(const F5Args& a, int nblocks, int nw, size_t lds, const float* alph
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)F5_LDS_MAX);
         attr = true;
     }
-    if (a.only && !OUT) {
-        static bool attr_fix = false;
-        if (!attr_fix) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused5_fix<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)F5_LDS_MAX);
-            attr_fix = true;
+    if constexpr (!OUT) {               // (fixups are counters / flags only)
+        if (a.only) {
+            static bool attr_fix = false;
+            if (!attr_fix) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused5_fix<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)F5_LDS_MAX);
+                attr_fix = true;
+            }
+            const int grid = nblocks < F5_FIX_GRID ? nblocks : F5_FIX_GRID;
+            hipLaunchKernelGGL((k_fused5_fix<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>), dim3(grid), dim3(64 * nw), lds, s,
+                               a, alpha, alpha_ucn, (int64_t)nblocks);
+            return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
         }
-        const int grid = nblocks < F5_FIX_GRID ? nblocks : F5_FIX_GRID;
-        hipLaunchKernelGGL((k_fused5_fix<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>), dim3(grid), dim3(64 * nw), lds, s,
-                           a, alpha, alpha_ucn, (int64_t)nblocks);
-        return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
     }
     hipLaunchKernelGGL((k_fused5<CW, MAXG, MAXDEG, HG, LDEG, WPE, UCN, PEW, OUT, LUT>), dim3(nblocks), dim3(64 * nw), lds, s,
                        a, alpha, alpha_ucn);
