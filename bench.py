@@ -24,7 +24,8 @@ Prints ONE JSON line (rank 0).  Besides the driver's fields it carries:
                 bytes per launch (null without a profile of this kernel at this batch).
   cpu_baseline  the dense TF-graph-equivalent numpy restatement of the reference decoder
                 (oracle/nms_dense.py) on the C1 sample (B=120, T=20, 3.5 dB), rank 0, N=1,
-                every host core this process may run on
+                sharded over one single-threaded worker process per core of the box's CPU
+                share
   e2e_with_rng  K steps that each draw a fresh AWGN batch inside the timed region
                 (ldpc_decode_awgn: generated in the decoder's prologue; SURVEY §8 d
                 "separately time end-to-end with GPU RNG and counters")
@@ -94,24 +95,56 @@ def load_problem(T=None, config="C2"):
     return proto, g, W, CodeParams(proto, z, ps, pe, ss, se)
 
 
+def _cpu_worker(proto, W, X, T, barrier, q):
+    """One CPU-baseline process: builds the dense graph, waits for the others, decodes its
+    slice of the C1 batch single-threaded (threadpoolctl), reports its decode time."""
+    from threadpoolctl import threadpool_limits
+    from oracle import nms_dense
+    dg = nms_dense.DenseGraph(proto, 24)
+    with threadpool_limits(limits=1):
+        barrier.wait()
+        t0 = time.perf_counter()
+        if X.shape[0]:
+            nms_dense.decode(X, proto, 24, W.alpha, W.alpha_ucn, W.beta, T, 2, 5, graph=dg)
+        q.put(time.perf_counter() - t0)
+
+
 def cpu_baseline(proto, g, W, cp, B=120, T=20, snr=3.5):
-    """Dense TF-graph-equivalent numpy decoder on the C1 sample, all allowed host cores."""
+    """Dense TF-graph-equivalent numpy decoder on the C1 sample, sharded over worker processes.
+
+    The C1 batch is split into contiguous slices (fer.shard_range), one per worker process
+    (spawned: fresh interpreters, nothing inherited from this process's HIP state), each
+    decoding single-threaded after all have built their dense graph; value = B / the slowest
+    worker's decode time.  Workers = the host cores this process may use, capped by the box's
+    CPU share (OMP_NUM_THREADS, 16 on the GPU box): so `cores` is what actually ran."""
+    import multiprocessing as mp
     from threadpoolctl import threadpool_limits
     from ldpc_error_floor_amd.channel import create_mix_epoch
-    from oracle import nms_dense, nms_oracle
-    cores = len(os.sched_getaffinity(0))          # SURVEY §8 d: all host cores
+    from ldpc_error_floor_amd.fer import shard_range
+    from oracle import nms_oracle
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    cores = len(os.sched_getaffinity(0))
+    workers = max(1, min(cores, share if share > 0 else cores, B))
     sigma = float(cp.sigma(snr))
     wr, nr = np.random.RandomState(2044), np.random.RandomState(1076)
     X, _ = create_mix_epoch([sigma], wr, nr, B, g.N, g.N - g.M, 24, [], True, 2, 0, 0, 0, 0, 5, 20.0)
     X = X.reshape(B, -1).astype(np.float32)
-    dg = nms_dense.DenseGraph(proto, 24)
-    with threadpool_limits(limits=cores):
-        t0 = time.perf_counter()
-        nms_dense.decode(X, proto, 24, W.alpha, W.alpha_ucn, W.beta, T, 2, 5, graph=dg)
-        dt = time.perf_counter() - t0
+    ctx = mp.get_context("spawn")
+    barrier, q = ctx.Barrier(workers), ctx.Queue()
+    procs = []
+    for r in range(workers):
+        b0, b1 = shard_range(B, r, workers)
+        procs.append(ctx.Process(target=_cpu_worker, args=(proto, W, X[b0:b1], T, barrier, q)))
+    for pr in procs:
+        pr.start()
+    times = [q.get(timeout=900) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=60)
+    dt = max(times)
+    with threadpool_limits(limits=1):
         sg = nms_oracle.lifted_edges(proto, 24)
         t1 = time.perf_counter()
-        nms_oracle.decode(np.tile(X, (8, 1)), proto, 24, W.alpha, W.alpha_ucn, W.beta, T, 2, 5, graph=sg)
+        nms_oracle.decode(X, proto, 24, W.alpha, W.alpha_ucn, W.beta, T, 2, 5, graph=sg)
         dt_sparse = time.perf_counter() - t1
     cpu = platform.processor() or ""
     try:
@@ -119,14 +152,14 @@ def cpu_baseline(proto, g, W, cp, B=120, T=20, snr=3.5):
             cpu = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), cpu)
     except OSError:
         pass
-    return {"value": round(B / dt, 3), "unit": "codewords/s", "cores": cores, "kind": "port",
-            "threads": f"BLAS pool limited to {cores} (threadpoolctl; numpy elementwise ops run "
-                       f"single-threaded)",
+    return {"value": round(B / dt, 3), "unit": "codewords/s", "cores": workers, "kind": "port",
+            "threads": f"{workers} worker processes x 1 thread (threadpoolctl), one contiguous "
+                       f"slice of the batch each; {cores} cores in this process's affinity",
             "sample": f"C1: wman QMS q5 T={T}, B={B} host-channel codewords at {snr} dB (seeds "
                       f"2044/1076), dense TF-graph-equivalent numpy (oracle/nms_dense.py), "
-                      f"{dt:.1f} s",
+                      f"slowest worker {dt:.1f} s (per worker: {min(times):.1f}-{dt:.1f} s)",
             "cpu_model": cpu,
-            "sparse_oracle_cw_s": round(8 * B / dt_sparse, 1)}
+            "sparse_oracle_cw_s_1thread": round(B / dt_sparse, 1)}
 
 
 def _free_port():
@@ -205,7 +238,11 @@ def main():
         raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {ndev} GPUs visible")
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
-    if world > 1:
+    # launched as a rank (torch.distributed.run, or this script's own launcher; WORLD_SIZE set,
+    # 1 included): the process group is initialised and every collective below runs through it,
+    # so a one-GPU run with WORLD_SIZE=1 exercises the same RCCL calls as the 8-GPU job
+    dist_on = "WORLD_SIZE" in os.environ
+    if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -213,7 +250,7 @@ def main():
 
     def allreduce(t, op):
         """In-place all-reduce of a device tensor (host round trip for gloo)."""
-        if world == 1:
+        if not dist_on:
             return t
         if backend == "nccl":
             dist.all_reduce(t, op=op)
@@ -224,7 +261,7 @@ def main():
         return t
 
     def barrier():
-        if world > 1:
+        if dist_on:
             if backend == "nccl":
                 dist.barrier(device_ids=[gpu])
             else:
@@ -268,8 +305,8 @@ def main():
         t1 = time.perf_counter()
         barrier()
         elapsed = allreduce(torch.tensor([t1 - t0], dtype=torch.float64, device=dev),
-                            dist.ReduceOp.MAX if world > 1 else None)
-        cnt = allreduce(counters.clone(), dist.ReduceOp.SUM if world > 1 else None)
+                            dist.ReduceOp.MAX if dist_on else None)
+        cnt = allreduce(counters.clone(), dist.ReduceOp.SUM if dist_on else None)
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
         return dict(name=name, elapsed=float(elapsed.item()), kernel_ms=kernel_ms,
                     counters=cnt.cpu().tolist(), design_bytes=dec.kernel_info(T)[0])
@@ -304,7 +341,7 @@ def main():
         roofline = {"bound": "valu",
                     "achieved": round(rate, 1) if rate else None, "peak": VALU_PEAK_WINST,
                     "unit": "wave-instructions/s",
-                    "frac": vb.get("frac", issue),
+                    "frac": issue,
                     "issue_frac": issue,
                     "traffic": traffic,
                     "hbm_frac": (round(traffic / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
@@ -314,20 +351,24 @@ def main():
                     "valu_busy": vb or None,
                     "lds_busy": prof.get("lds_busy") if prof else None,
                     "wait_any_frac": prof.get("wait_any_frac") if prof else None,
-                    "profile": prof.get("source") if prof else None}
+                    "profile": prof.get("source") if prof else None,
+                    "profile_sources": prof.get("src_fingerprint") if prof else None}
         roofline["note"] = ("fused: all T iterations per codeword block in LDS/VGPRs; the only "
                             "HBM traffic is the LLR read, so the VALU pipe binds (the bit-sliced "
                             "bsl kernel: VALU issue and the LDS array together, lds_busy = "
-                            "SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM cycles / 8)). frac = VALU "
-                            "busy: quad-cycles with a VALU issue (SQ_INSTS_VALU - "
-                            "SQ_ACTIVE_INST_VALU2) / (1024 SIMDs x GRBM_GUI_ACTIVE/8/4), PMC of "
-                            "this build (profile above). issue_frac = achieved / peak with "
-                            "achieved = SQ_INSTS_VALU per launch / this run's kernel time (HIP "
-                            "events) and peak = one wave64 VALU issue per 2 cycles per SIMD at "
-                            "2.4 GHz, which only 2-cycle VOP1/VOP2 forms reach (VOP3/SDWA take "
-                            "a whole quad-cycle, DESIGN.md 3.2). effective_frac = SURVEY 8d "
-                            "two-kernel bytes/codeword x B / time / 8 TB/s (design comparison, "
-                            "not a bandwidth).")
+                            "SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM cycles / 8)). frac = "
+                            "issue_frac = achieved / peak with achieved = SQ_INSTS_VALU per "
+                            "launch (PMC of these sources: profile_sources = the sources' "
+                            "fingerprint, else null) / this run's kernel time (HIP events) and "
+                            "peak = one wave64 VALU issue per 2 cycles per SIMD at 2.4 GHz "
+                            "(MI355X_MICROARCH.md), which only 2-cycle VOP1/VOP2 forms reach "
+                            "(VOP3/SDWA/DPP and SGPR-operand forms take ~4.2 cycles, "
+                            "DESIGN.md 3.3). valu_busy = the busy model of the same PMC run: "
+                            "quad-cycles with a VALU issue (SQ_INSTS_VALU - "
+                            "SQ_ACTIVE_INST_VALU2) / (1024 SIMDs x GRBM_GUI_ACTIVE/8/4), at the "
+                            "clock of that run. effective_frac = SURVEY 8d two-kernel "
+                            "bytes/codeword x B / time / 8 TB/s (design comparison, not a "
+                            "bandwidth).")
     else:
         roofline = {"bound": "hbm", "achieved": round(effective, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(effective / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -373,14 +414,19 @@ def main():
     if (world == 1 and rank == 0 and not args.no_cpu_baseline and args.config == "C2"
             and args.decoding_type == 2 and args.q_bit == 5):
         out["cpu_baseline"] = cpu_baseline(proto, g, W, cp, T=T)
+    if dist_on:
+        out["process_group"] = {"backend": dist.get_backend(), "world": dist.get_world_size()}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 
 def load_profile(name, batch):
-    """profiles/traffic_<kernel>.json (tools/traffic_json.py) when it was taken at this batch."""
+    """profiles/traffic_<kernel>.json (tools/traffic_json.py) when it was taken at this batch
+    of a build from the current native sources (its src_fingerprint); None otherwise, so no
+    PMC figure of another build is reported beside this run's timing."""
+    from ldpc_error_floor_amd.build import source_fingerprint
     safe = "".join(ch if (ch.isalnum() or ch in "_.-") else "_" for ch in name)
     path = os.path.join(ROOT, "profiles", f"traffic_{safe}.json")
     try:
@@ -388,7 +434,9 @@ def load_profile(name, batch):
             tj = json.load(f)
     except (OSError, ValueError):
         return None
-    return tj if int(tj.get("batch", -1)) == batch else None
+    if int(tj.get("batch", -1)) != batch or tj.get("src_fingerprint") != source_fingerprint():
+        return None
+    return tj
 
 
 if __name__ == "__main__":

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LDPC_NMS_ABI_VERSION 1
+#define LDPC_NMS_ABI_VERSION 2     /* 2: ldpc_decode_outputs.iter_wrong, ldpc_ctx_last_kernel */
 
 typedef struct ldpc_graph ldpc_graph;
 typedef struct ldpc_ctx ldpc_ctx;
@@ -74,6 +74,11 @@ typedef struct ldpc_decode_outputs {
                                    frames wrong at every t, 2*loss (loss_type 2, etha 0)}
                                    for the all-zero codeword; or NULL */
     uint8_t* frame_flags;       /* [B] bit0 wrong at every t (uncor), bit1 wrong @T-1; or NULL */
+    uint32_t* iter_wrong;       /* [T][ceil(B/32)]: bit b%32 of word (t, b/32) = frame b has a hard
+                                   decision 1 among the target bits at iteration t (the per-iteration
+                                   frame error of calc_ber_fer, Print_Functions.py:100-118; the
+                                   all-zero codeword), bits past B zero; or NULL.  Every kernel
+                                   serves it, the counters-only ones included. */
 } ldpc_decode_outputs;
 
 int ldpc_abi_version(void);
@@ -103,6 +108,13 @@ int ldpc_decode(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_
    roofline report), and a short kernel name.  Returns 0 if unsupported. */
 int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* bytes_per_cw,
                      char* name, int32_t name_len);
+
+/* Name of the kernel that served the last successful ldpc_decode / ldpc_decode_awgn on this
+   context (empty before the first).  Which kernel runs depends on the requested outputs: APP
+   exports run v5 or flood, counters / frame flags / iter_wrong / hard_bits / synd_bits of the
+   QMS grids the bit-sliced kernels ("bsl[...]", "bsc[...]"), whose hard-bit export is a
+   separate build of the same kernel that also stores each iteration's hard decisions. */
+int ldpc_ctx_last_kernel(const ldpc_ctx* c, char* name, int32_t name_len);
 
 /* On-GPU AWGN channel for the all-zero codeword (create_mix_epoch, Print_Functions.py:29-72):
    writes llr_dev [B][n_vars] f32 = Q(2(sigma*n - 1)/sigma^2) with punctured (1-based bits

@@ -53,6 +53,31 @@ LIB = os.path.join(PKG, "libldpc_nms.so")
 EXT = os.path.join(PKG, "_ldpc_nms" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
+def source_fingerprint() -> str:
+    """sha256 (first 16 hex digits) of every native source and header this build compiles, plus
+    the compile flags: a profile taken of one build (tools/traffic_json.py) records it, and
+    bench.py uses the profile's PMC-derived figures only for the same sources."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(HIP_SOURCES + HEADERS + HOST_SOURCES + [F5_SHAPE_SRC, BS_INST_SRC])
+    for f in files:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    with open(os.path.join(INCLUDE, "ldpc_nms.h"), "rb") as fh:
+        h.update(fh.read())
+    h.update(" ".join(_flags()).encode())
+    return h.hexdigest()[:16]
+
+
+def _flags(absolute=False):
+    inc = (INCLUDE, CSRC) if absolute else (os.path.relpath(INCLUDE, ROOT), os.path.relpath(CSRC, ROOT))
+    # the fused kernels' per-group loops must unroll completely (register-resident per-group
+    # state); the default pragma threshold gives up on the wide shapes
+    return ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+            "-I" + inc[0], "-I" + inc[1], "-Wall", "-Wno-unused-result",
+            "-mllvm", "-pragma-unroll-threshold=500000"]
+
+
 def _hipcc():
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and os.path.exists(cand):
@@ -78,11 +103,7 @@ def build(force=False, jobs=4, verbose=False):
     os.makedirs(BUILD, exist_ok=True)
     hipcc = _hipcc()
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "ldpc_nms.h")]
-    flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-             "-I" + INCLUDE, "-I" + CSRC, "-Wall", "-Wno-unused-result",
-             # the fused kernels' per-group loops must unroll completely (register-resident
-             # per-group state); the default pragma threshold gives up on the wide shapes
-             "-mllvm", "-pragma-unroll-threshold=500000"]
+    flags = _flags(absolute=True)
     objs, jobs_list = [], []
     units = [(src, src.replace(".hip", ".o"), []) for src in HIP_SOURCES]
     units += [(src, src.replace(".cpp", ".o"), []) for src in HOST_SOURCES]

@@ -124,7 +124,7 @@ int bs_qmax(int mode) { return mode == MODE_Q4 ? 7 : mode == MODE_Q3 ? 3 : QMAX;
 static float mode_step_bs(int mode) { return bs_step(mode); }
 
 // the plan of one instance (ok = it serves the graph)
-static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_cdeg, int mode) {
+static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_cdeg, int mode, int T) {
     BsPlan p;
     const BsInst& k = kBsInst[i];
     const host::GraphTables& h = *g.host;
@@ -166,7 +166,7 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     if (k.UCN && p.off_hdz > 65535) return p;
     o = (slot_end + 15) & ~(size_t)15;
     p.off_red = (uint32_t)o;
-    o += 64;
+    o += 64 + (size_t)4 * T;                       // + the per-iteration frame-error words
     p.off_alut = (uint32_t)o;
     o += (size_t)2 * (k.UCN ? 2 : 1) * p.arows * LUT_W * 4;
     p.off_blut = (uint32_t)o;
@@ -177,7 +177,7 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     return p;
 }
 
-BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip) {
+BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T) {
     BsPlan p;
     const char* e = getenv("LDPC_BS");
     if (e && atoi(e) == 0) return p;
@@ -191,7 +191,7 @@ BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float cli
     if (min_cdeg < 2) return p;                                   // ("no other edge" rule unneeded)
     for (int i = 0; i < kBsNInst; ++i) {
         if (want_lpc != 0 && want_lpc != kBsInst[i].LPC) continue;
-        BsPlan q = plan_inst(g, i, ucn, clip, min_cdeg, mode);
+        BsPlan q = plan_inst(g, i, ucn, clip, min_cdeg, mode, T);
         if (q.ok) return q;
     }
     return p;
@@ -201,14 +201,14 @@ BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float cli
 
 using namespace bs;
 
-bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip) {
-    return bs_plan(g, mode, ucn, per_edge_w, clip).ok || bsc_supported(g, mode, ucn, per_edge_w, clip);
+bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T) {
+    return bs_plan(g, mode, ucn, per_edge_w, clip, T).ok || bsc_supported(g, mode, ucn, per_edge_w, clip, T);
 }
 
-const char* bs_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip) {
+const char* bs_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T) {
     static thread_local char buf[64];
-    const BsPlan p = bs_plan(g, mode, ucn, per_edge_w, clip);
-    if (!p.ok) return bsc_kernel_name(g, mode, ucn, per_edge_w, clip);
+    const BsPlan p = bs_plan(g, mode, ucn, per_edge_w, clip, T);
+    if (!p.ok) return bsc_kernel_name(g, mode, ucn, per_edge_w, clip, T);
     const BsInst& k = kBsInst[p.inst];
     if (k.VPL == 1 && k.CPL == 1)
         snprintf(buf, sizeof(buf), "bsl[p32,w%d,d%d,v%d,l%d%s]", p.nw, k.D, k.DV, k.LPC, p.ucn ? ",ucn" : "");
@@ -420,8 +420,11 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
         for (int u = 0; u < k.VPL; ++u) {
             const int ch = vslot[(size_t)w * k.VPL + u];
             int dmax = 0, dmin = 1 << 30;
-            if (ch < 0) dmin = 0;
-            if (ch < 0) continue;
+            if (ch < 0) {                 // no chunk at this place: the kernel skips it (dw < 0)
+                wdeg[2 * ((size_t)u * p.nw + w)] = -1;
+                wdeg[2 * ((size_t)u * p.nw + w) + 1] = 0;
+                continue;
+            }
             std::fill(A.begin(), A.end(), p.off_zero);
             std::fill(dl.begin(), dl.end(), 0);
             for (int l = 0; l < 64; ++l) {
@@ -514,9 +517,9 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
 }
 
 int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
-              bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s) {
-    const BsPlan p = bs_plan(g, mode, ucn, false, b.clip);
-    if (!p.ok) return bsc_decode(g, b, ws, llr, mode, ucn, counters, flags, bad, s);
+              bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, uint32_t* hdx, hipStream_t s) {
+    const BsPlan p = bs_plan(g, mode, ucn, false, b.clip, b.T);
+    if (!p.ok) return bsc_decode(g, b, ws, llr, mode, ucn, counters, flags, bad, hdx, s);
     if (ws.bs_graph && ws.bs_graph_inst != p.inst) {
         (void)hipFree(ws.bs_graph);
         ws.bs_graph = nullptr;
@@ -561,6 +564,8 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.counters = counters;
     a.flags = flags;
     a.bad = bad;
+    a.iter_wrong = b.iter_wrong;
+    a.hdx = hdx;
     a.off_slots = p.off_slots;
     a.off_pad = p.off_pad;
     a.off_zero = p.off_zero;

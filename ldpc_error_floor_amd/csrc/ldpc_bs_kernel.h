@@ -83,7 +83,11 @@ struct BsArgs {
     int64_t* counters;
     uint8_t* flags;
     uint32_t* bad;               // [packs] 1: decoded by the v5 fixup instead
+    uint32_t* iter_wrong;        // [T][packs] per-iteration frame-error words, or null
+    uint32_t* hdx;               // XP builds: [T][packs][n_vars] hard decisions (bit r = codeword
+                                 // 32 pack + r), the hard-bit / syndrome export
     uint32_t off_slots, off_pad, off_zero, off_red, off_alut, off_blut, off_hdz;   // LDS byte offsets
+                                 // (RED: 16 words, then T words: iteration t's frame-error word)
     int ablate;   // timing diagnostics, builds with -DBS_DIAG only (LDPC_DIAG_ABLATE, wrong
                   // results): 1 no check phase, 2 no beta table, 4 no V->C pass, 8 no frame
                   // flags, 16 no iterations, 32 no LLR loads.  (Compiled in, the uniform
@@ -362,11 +366,17 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
 #ifndef BS_KEEP
 #define BS_KEEP 4
 #endif
+// variable places without a chunk skipped (A/B switch: -DBS_VSKIP=0 runs their table work)
+#ifndef BS_VSKIP
+#define BS_VSKIP 1
+#endif
 
 // Register budget: the small instances run at 64 VGPRs (WPE 8: three 9-wave workgroups per CU).
 // At a 72-register budget only two were resident (the waves of a workgroup are not spread evenly
 // over the SIMDs): measured 7.56 ms (72 VGPRs) -> 6.51 ms (64) per 2^20-codeword C2 decode.
-template <int D, int DV, int LPC, int VPL, int CPL, bool UCN, bool BIG, bool PK, int WPE>
+// XP: the hard-bit export build (a.hdx: every iteration's hard decisions, for the hard_bits /
+// synd_bits outputs); the counters-only build is the one the bench and the sweeps run.
+template <int D, int DV, int LPC, int VPL, int CPL, bool UCN, bool BIG, bool PK, int WPE, bool XP>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_bs(BsArgs a) {
     static_assert(LPC == 2 || LPC == 4, "lanes per check");
@@ -479,6 +489,9 @@ k_bs(BsArgs a) {
         uint32_t wr = 0u, apos = 0u, nb = 0u;
 #pragma unroll
         for (int u = 0; u < VPL; ++u) {
+            // a (wave, u) place without a variable chunk (dw = -1, wave-uniform): nothing to do
+            // (5G BG2: 20 chunks on 32 places; their beta table and Tv work used to run anyway)
+            if (BS_VSKIP && VPL > 1 && dw[u] < 0) continue;
 #pragma unroll
             for (int p = 0; p < VNA; ++p) asm volatile("" : "+v"(va[u][p]));   // unpacked per use
             auto vaddr = [&](int f) __attribute__((always_inline)) -> uint32_t {
@@ -560,6 +573,9 @@ k_bs(BsArgs a) {
                 }
                 if (UCN && !last && ucn && v >= 0) lds_put(hda, hd);   // HD[v] (Main_Functions.py:184-188)
                 hd &= valid;                                     // APP >= 0 -> hard decision 1
+                if constexpr (XP) {                              // iteration tb - 1's hard decisions
+                    if (v >= 0) a.hdx[((size_t)(tb - 1) * (size_t)((a.B + 31) >> 5) + blockIdx.x) * nv + v] = hd;
+                }
                 if (ABL(8)) hd = 0u;
                 if (counted) {
                     wr |= hd;
@@ -662,6 +678,9 @@ k_bs(BsArgs a) {
 
     for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
         if (tid == 0 && t > 0) {            // fold iteration t-1's frame flags
+            // (kept in LDS for the iter_wrong export after the loop: a global pointer held
+            // through the loop cost the 64-VGPR build 17 more SGPR spill moves in it)
+            RED[16 + t - 1] = RED[0];
             RED[1] &= RED[0];
             RED[0] = 0u;
         }
@@ -835,6 +854,7 @@ k_bs(BsArgs a) {
         const uint32_t wl = RED[0] & valid;
         const uint32_t all = RED[1] & RED[0] & valid;
         const uint32_t ap = RED[2] & valid;
+        RED[16 + a.T - 1] = RED[0];
         if (a.counters) {
             unsigned long long* cc = reinterpret_cast<unsigned long long*>(a.counters);
             const unsigned long long c0 = RED[3], c1 = __popc(wl), c2 = __popc(all),
@@ -847,17 +867,20 @@ k_bs(BsArgs a) {
         RED[5] = all;
         RED[6] = wl;
     }
-    if (a.flags) {
+    if (a.flags || a.iter_wrong) {
         __syncthreads();
-        if (tid < nvalid)
+        if (a.flags && tid < nvalid)
             a.flags[b0 + tid] = (uint8_t)(((RED[5] >> tid) & 1) | (((RED[6] >> tid) & 1) << 1));
+        if (a.iter_wrong)                   // [T][packs]: iteration t's frame-error word
+            for (int t = tid; t < a.T; t += NT)
+                a.iter_wrong[(size_t)t * (size_t)((a.B + 31) >> 5) + blockIdx.x] = RED[16 + t] & valid;
     }
 }
 
-template <int I>
-int launch_bs(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
+template <int I, bool XP>
+int launch_bs_x(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     constexpr BsInst k = kBsInst[I];
-    auto* fn = &k_bs<k.D, k.DV, k.LPC, k.VPL, k.CPL, k.UCN, k.BIG, k.PK, k.WPE>;
+    auto* fn = &k_bs<k.D, k.DV, k.LPC, k.VPL, k.CPL, k.UCN, k.BIG, k.PK, k.WPE, XP>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -866,6 +889,10 @@ int launch_bs(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     }
     hipLaunchKernelGGL(fn, dim3(nblocks), dim3(64 * nw), lds, s, a);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+}
+template <int I>
+int launch_bs(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
+    return a.hdx ? launch_bs_x<I, true>(a, nblocks, nw, lds, s) : launch_bs_x<I, false>(a, nblocks, nw, lds, s);
 }
 
 // per-instance translation units (ldpc_bs_inst.hip, -DBS_INST=i)

@@ -54,7 +54,10 @@ struct BscArgs {
     int64_t* counters;
     uint8_t* flags;
     uint32_t* bad;
+    uint32_t* iter_wrong;        // [T][packs] per-iteration frame-error words, or null
+    uint32_t* hdx;               // XP builds: [T][packs][n_vars] hard decisions (as bsl's)
     uint32_t off_a, off_rec, off_tv, off_red, off_alut, off_blut;   // SGN at LDS byte 0
+                                 // (RED: 16 words, then T words: iteration t's frame-error word)
 };
 
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
@@ -74,7 +77,7 @@ __device__ __forceinline__ void lds_dput(uint32_t addr, uint32_t x, uint32_t y) 
     *reinterpret_cast<LdsD*>(addr) = v;
 }
 
-template <int D, int DVH, int DVL, int LPC, int VPL, int CPL, int WPE>
+template <int D, int DVH, int DVL, int LPC, int VPL, int CPL, int WPE, bool XP>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_bsc(BscArgs a) {
     constexpr int SB = (DVH * QMAX + QMAX <= 127) ? 8 : 9;
@@ -172,6 +175,7 @@ k_bsc(BscArgs a) {
 #pragma unroll
         for (int u = 0; u < VPL; ++u) {
             const int dvu = u == 0 ? DVH : DVL;
+            if (BS_VSKIP && dw[u] < 0) continue;   // no variable chunk at this (wave, u) place
 #pragma unroll
             for (int p = 0; p < DVH; ++p)
                 if (p < dvu) asm volatile("" : "+v"(va[u][p]));
@@ -238,6 +242,9 @@ k_bsc(BscArgs a) {
                     hd = B3(T_XNOR3, S[SB - 1], c_s, c);
                 }
                 hd &= valid;
+                if constexpr (XP) {                              // iteration tb - 1's hard decisions
+                    if (v >= 0) a.hdx[((size_t)(tb - 1) * (size_t)((a.B + 31) >> 5) + blockIdx.x) * nv + v] = hd;
+                }
                 if (counted) {
                     wr |= hd;
                     if (last) {
@@ -303,6 +310,7 @@ k_bsc(BscArgs a) {
 
     for (int t = 0; t < a.T; ++t) {
         if (tid == 0 && t > 0) {
+            RED[16 + t - 1] = RED[0];                 // (exported after the loop)
             RED[1] &= RED[0];
             RED[0] = 0u;
         }
@@ -453,6 +461,7 @@ k_bsc(BscArgs a) {
         const uint32_t wl = RED[0] & valid;
         const uint32_t all = RED[1] & RED[0] & valid;
         const uint32_t ap = RED[2] & valid;
+        RED[16 + a.T - 1] = RED[0];
         if (a.counters) {
             unsigned long long* cc = reinterpret_cast<unsigned long long*>(a.counters);
             const unsigned long long c0 = RED[3], c1 = __popc(wl), c2 = __popc(all),
@@ -465,10 +474,13 @@ k_bsc(BscArgs a) {
         RED[5] = all;
         RED[6] = wl;
     }
-    if (a.flags) {
+    if (a.flags || a.iter_wrong) {
         __syncthreads();
-        if (tid < nvalid)
+        if (a.flags && tid < nvalid)
             a.flags[b0 + tid] = (uint8_t)(((RED[5] >> tid) & 1) | (((RED[6] >> tid) & 1) << 1));
+        if (a.iter_wrong)
+            for (int t = tid; t < a.T; t += NT)
+                a.iter_wrong[(size_t)t * (size_t)((a.B + 31) >> 5) + blockIdx.x] = RED[16 + t] & valid;
     }
 }
 
@@ -504,7 +516,7 @@ struct BscPlan {
     std::vector<int> vorder, vslot;      // variables by degree; chunk of each (wave, u) place
 };
 
-static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip) {
+static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T) {
     BscPlan p;
     const char* e = getenv("LDPC_BS");
     if (e && atoi(e) == 0) return p;
@@ -564,7 +576,7 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
         o += (size_t)nv * 24;
         o = (o + 15) & ~(size_t)15;
         q.off_red = (uint32_t)o;
-        o += 64;
+        o += 64 + (size_t)4 * T;                 // + the per-iteration frame-error words
         q.off_alut = (uint32_t)o;
         o += (size_t)2 * q.arows * LUT_W * 4;
         q.off_blut = (uint32_t)o;
@@ -617,7 +629,7 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     for (int w = 0; w < NWp; ++w)
         for (int u = 0; u < k.VPL; ++u) {
             const int ch = p.vslot[(size_t)w * k.VPL + u];
-            int dmax = 0, dmin = ch < 0 ? 0 : 1 << 30;
+            int dmax = ch < 0 ? -1 : 0, dmin = ch < 0 ? 0 : 1 << 30;     // -1: no chunk (skipped)
             for (int l = 0; ch >= 0 && l < 64; ++l) {
                 const int o = 64 * ch + l;
                 if (o >= nv) { dmin = 0; continue; }
@@ -682,10 +694,10 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     return LDPC_OK;
 }
 
-template <int I>
+template <int I, bool XP>
 static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     constexpr BscInst k = kBscInst[I];
-    auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE>;
+    auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE, XP>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -700,13 +712,13 @@ static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStre
 
 using namespace bs;
 
-bool bsc_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip) {
-    return bsc_plan(g, mode, ucn, per_edge_w, clip).ok;
+bool bsc_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T) {
+    return bsc_plan(g, mode, ucn, per_edge_w, clip, T).ok;
 }
 
-const char* bsc_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip) {
+const char* bsc_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T) {
     static thread_local char buf[64];
-    const BscPlan p = bsc_plan(g, mode, ucn, per_edge_w, clip);
+    const BscPlan p = bsc_plan(g, mode, ucn, per_edge_w, clip, T);
     if (!p.ok) return "";
     const BscInst& k = kBscInst[p.inst];
     snprintf(buf, sizeof(buf), "bsc[p32,w%d,d%d,v%d/%d,l%d,x%d/%d]", p.nw, k.D, k.DVH, k.DVL, k.LPC,
@@ -715,8 +727,8 @@ const char* bsc_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge
 }
 
 int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
-               bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s) {
-    const BscPlan p = bsc_plan(g, mode, ucn, false, b.clip);
+               bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, uint32_t* hdx, hipStream_t s) {
+    const BscPlan p = bsc_plan(g, mode, ucn, false, b.clip, b.T);
     if (!p.ok) return LDPC_ERR_UNSUPPORTED;
     int st = bsc_tables(g, p, ws, s);
     if (st != LDPC_OK) return st;
@@ -754,6 +766,8 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     a.counters = counters;
     a.flags = flags;
     a.bad = bad;
+    a.iter_wrong = b.iter_wrong;
+    a.hdx = hdx;
     a.off_a = p.off_a;
     a.off_rec = p.off_rec;
     a.off_tv = p.off_tv;
@@ -762,8 +776,8 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     a.off_blut = p.off_blut;
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
     switch (p.inst) {
-        case 1: return bsc_launch<1>(a, nblocks, p.nw, p.lds, s);
-        default: return bsc_launch<0>(a, nblocks, p.nw, p.lds, s);
+        case 1: return hdx ? bsc_launch<1, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<1, false>(a, nblocks, p.nw, p.lds, s);
+        default: return hdx ? bsc_launch<0, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<0, false>(a, nblocks, p.nw, p.lds, s);
     }
 }
 

@@ -44,6 +44,7 @@ struct ldpc_ctx {
     // LLR buffer for ldpc_decode_awgn when the kernel cannot generate in its prologue
     float* llr_scratch = nullptr;
     int64_t llr_scratch_n = 0;
+    char last_kernel[64] = {0};   // ldpc_ctx_last_kernel
 };
 
 namespace {
@@ -79,36 +80,50 @@ void dev_free(T*& p) {
 }
 
 // ---- compat kernels --------------------------------------------------------------------
-__global__ void k_export_hard(Bufs p, uint32_t* __restrict__ out, int T, int nwords) {
-    const int64_t total = (int64_t)T * p.B * nwords;
+// The hard decision of codeword b, variable v at iteration t, wherever the decode left it: the
+// tile layout of flood / v5 (Bufs::hd, slot t + 1), or the bit-sliced kernels' packed words
+// (except packs the v5 fixup decoded, which are in the tile layout).
+struct HdSrc {
+    const uint64_t* tile;
+    const uint32_t* pack;
+    const uint32_t* bad;
+    int64_t npk;
+    int ntiles, n_vars;
+    __device__ uint32_t bit(int t, int64_t b, int v) const {
+        const int64_t pk = b >> 5;
+        if (pack && !bad[pk]) return (pack[((size_t)t * npk + pk) * n_vars + v] >> (b & 31)) & 1u;
+        const int64_t ti = b / TILE;
+        const int bl = (int)(b - ti * TILE);
+        return (uint32_t)((tile[(((size_t)(t + 1) * ntiles + ti) * n_vars + v) * 4 + (bl & 3)] >> (bl >> 2)) & 1u);
+    }
+};
+
+__global__ void k_export_hard(HdSrc src, int64_t B, uint32_t* __restrict__ out, int T, int nwords) {
+    const int64_t total = (int64_t)T * B * nwords;
     for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
          id += (int64_t)gridDim.x * blockDim.x) {
         const int w = (int)(id % nwords);
-        const int64_t b = (id / nwords) % p.B;
-        const int t = (int)(id / ((int64_t)nwords * p.B));
-        const int64_t tile = b / TILE;
-        const int bl = (int)(b - tile * TILE);
-        const int lane = bl >> 2, q = bl & 3;
+        const int64_t b = (id / nwords) % B;
+        const int t = (int)(id / ((int64_t)nwords * B));
         uint32_t word = 0;
         for (int k = 0; k < 32; ++k) {
             const int v = w * 32 + k;
-            if (v >= p.n_vars) break;
-            word |= (uint32_t)((p.hd[hd_index(p, t, tile, v) + q] >> lane) & 1) << k;
+            if (v >= src.n_vars) break;
+            word |= src.bit(t, b, v) << k;
         }
         out[id] = word;
     }
 }
 
-__global__ void k_export_synd(DevGraph g, Bufs p, uint32_t* __restrict__ out, int T, int nwords) {
-    const int64_t total = (int64_t)T * p.B * nwords;
+// syndrome H hd_t mod 2 per check (the quantity the reference computes as the UCN indicator of
+// iteration t + 1, Main_Functions.py:180-209)
+__global__ void k_export_synd(DevGraph g, HdSrc src, int64_t B, uint32_t* __restrict__ out, int T, int nwords) {
+    const int64_t total = (int64_t)T * B * nwords;
     for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
          id += (int64_t)gridDim.x * blockDim.x) {
         const int w = (int)(id % nwords);
-        const int64_t b = (id / nwords) % p.B;
-        const int t = (int)(id / ((int64_t)nwords * p.B));
-        const int64_t tile = b / TILE;
-        const int bl = (int)(b - tile * TILE);
-        const int lane = bl >> 2, q = bl & 3;
+        const int64_t b = (id / nwords) % B;
+        const int t = (int)(id / ((int64_t)nwords * B));
         uint32_t word = 0;
         for (int k = 0; k < 32; ++k) {
             const int c = w * 32 + k;
@@ -118,9 +133,29 @@ __global__ void k_export_synd(DevGraph g, Bufs p, uint32_t* __restrict__ out, in
             for (int pe = g.row_ptr[i]; pe < g.row_ptr[i + 1]; ++pe) {
                 const int s = h + g.pe_shift[pe];
                 const int v = g.pe_col[pe] * g.z + (s >= g.z ? s - g.z : s);
-                par ^= (uint32_t)((p.hd[hd_index(p, t, tile, v) + q] >> lane) & 1);
+                par ^= src.bit(t, b, v);
             }
             word |= par << k;
+        }
+        out[id] = word;
+    }
+}
+
+// flood's per-iteration frame flags (Bufs::wrong, [T][tiles][4] ballot words) -> iter_wrong
+__global__ void k_iter_wrong(Bufs p, uint32_t* __restrict__ out) {
+    const int64_t npk = (p.B + 31) >> 5;
+    const int64_t total = (int64_t)p.T * npk;
+    for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
+         id += (int64_t)gridDim.x * blockDim.x) {
+        const int t = (int)(id / npk);
+        const int64_t pk = id - (int64_t)t * npk;
+        uint32_t word = 0;
+        for (int r = 0; r < 32; ++r) {
+            const int64_t b = 32 * pk + r;
+            if (b >= p.B) break;
+            const int64_t ti = b / TILE;
+            const int bl = (int)(b - ti * TILE);
+            word |= (uint32_t)((p.wrong[((size_t)t * p.ntiles + ti) * 4 + (bl & 3)] >> (bl >> 2)) & 1u) << r;
         }
         out[id] = word;
     }
@@ -454,7 +489,7 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     if (gen && (kern != LDPC_KERNEL_FUSED || fl)) return LDPC_ERR_UNSUPPORTED;   // caller falls back
 
     const int ntiles = (int)((B + TILE - 1) / TILE);
-    const bool count = out.counters || out.frame_flags;
+    const bool count = out.counters || out.frame_flags || out.iter_wrong;
     Bufs b{};
     b.B = B;
     b.ntiles = ntiles;
@@ -471,6 +506,10 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     b.anypos = c->anypos;
     b.biterr = c->biterr;
     b.awgn = gen;
+    b.iter_wrong = out.iter_wrong;
+    if (out.iter_wrong &&
+        hipMemsetAsync(out.iter_wrong, 0, (size_t)p->T * ((B + 31) / 32) * sizeof(uint32_t), s) != hipSuccess)
+        return LDPC_ERR_HIP;
 
     if (count && kern == LDPC_KERNEL_FLOOD) {
         if (hipMemsetAsync(c->wrong, 0, (size_t)p->T * ntiles * 4 * sizeof(uint64_t), s) != hipSuccess ||
@@ -498,29 +537,54 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
                           c->T_max, g->per_edge_w, out.counters, out.frame_flags, s);
     }
     if (st != LDPC_OK) return st;
+    const char* served = kern == LDPC_KERNEL_FLOOD ? "flood"
+                         : fl ? ffl_kernel_name(g->dev, mode, ucn, g->per_edge_w != 0)
+                              : c->fused.last_kernel;
+    std::strncpy(c->last_kernel, served, sizeof(c->last_kernel) - 1);
 
     if (count && kern == LDPC_KERNEL_FLOOD) {
         hipLaunchKernelGGL(k_finalize, dim3(std::min(1024, (ntiles + 255) / 256)), dim3(256), 0, s, b,
                            out.counters, out.frame_flags);
+        if (out.iter_wrong) {
+            const int64_t total = (int64_t)p->T * ((B + 31) / 32);
+            hipLaunchKernelGGL(k_iter_wrong, dim3((unsigned)std::min<int64_t>(4096, (total + 255) / 256)),
+                               dim3(256), 0, s, b, out.iter_wrong);
+        }
     }
     if (want_bits) {
-        Bufs be = b;
-        if (kern == LDPC_KERNEL_FUSED) fused_bits_view(c->fused, be);
-        else { be.hd = c->hd; be.hd_all = 1; }
+        HdSrc src{};
+        src.npk = (B + 31) / 32;
+        src.ntiles = ntiles;
+        src.n_vars = g->h.N * g->h.z;
+        if (kern == LDPC_KERNEL_FUSED) {
+            const HdView v = fused_bits_view(c->fused);
+            src.tile = v.tile;
+            src.pack = v.pack;
+            src.bad = v.bad;
+        } else {
+            src.tile = c->hd;
+        }
         if (out.hard_bits) {
             const int nw = (g->h.N * g->h.z + 31) / 32;
             const int64_t total = (int64_t)p->T * B * nw;
             hipLaunchKernelGGL(k_export_hard, dim3((unsigned)std::min<int64_t>(4096, (total + 255) / 256)),
-                               dim3(256), 0, s, be, out.hard_bits, p->T, nw);
+                               dim3(256), 0, s, src, B, out.hard_bits, p->T, nw);
         }
         if (out.synd_bits) {
             const int nw = (g->h.M * g->h.z + 31) / 32;
             const int64_t total = (int64_t)p->T * B * nw;
             hipLaunchKernelGGL(k_export_synd, dim3((unsigned)std::min<int64_t>(4096, (total + 255) / 256)),
-                               dim3(256), 0, s, g->dev, be, out.synd_bits, p->T, nw);
+                               dim3(256), 0, s, g->dev, src, B, out.synd_bits, p->T, nw);
         }
     }
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+}
+
+int ldpc_ctx_last_kernel(const ldpc_ctx* c, char* name, int32_t name_len) {
+    if (!c || !name || name_len <= 0) return LDPC_ERR_ARG;
+    std::strncpy(name, c->last_kernel, (size_t)name_len - 1);
+    name[name_len - 1] = 0;
+    return LDPC_OK;
 }
 
 }  // extern "C"

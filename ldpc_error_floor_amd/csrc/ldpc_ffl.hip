@@ -53,6 +53,7 @@ struct FflArgs {
     const float* beta;           // [T][N]
     int64_t* counters;
     uint8_t* flags;
+    uint32_t* iter_wrong;        // [T][ceil(B/32)] per-iteration frame-error words (zeroed), or null
     uint32_t off_tv, off_rec, off_hd, off_red;
 };
 
@@ -69,12 +70,14 @@ __device__ __forceinline__ uint32_t fold(uint64_t m) {
 
 // frame flags / counters of the block from the LDS reductions (RED[0]: some bit wrong at the
 // last iteration, RED[1]: wrong at every earlier one, RED[2]: some app > 0, RED[3]: bit errors)
+template <int CW>
 __device__ __forceinline__ void block_finish(const FflArgs& a, uint32_t* RED, int tid, int64_t b0,
                                              int nvalid, uint32_t valid) {
     if (tid == 0) {
         const uint32_t wl = RED[0] & valid;
         const uint32_t all = RED[1] & RED[0] & valid;
         const uint32_t ap = RED[2] & valid;
+        if (a.iter_wrong) put_iter_wrong(a.iter_wrong, a.B, a.T - 1, b0, CW, wl);
         if (a.counters) {
             unsigned long long* cc = reinterpret_cast<unsigned long long*>(a.counters);
             const unsigned long long c0 = RED[3], c1 = __popc(wl), c2 = __popc(all),
@@ -146,6 +149,7 @@ k_ffl(FflArgs a) {
 
     for (int t = 0; t < a.T; ++t) {
         if (tid == 0 && t > 0) {            // fold iteration t-1's frame flags
+            if (a.iter_wrong) put_iter_wrong(a.iter_wrong, a.B, t - 1, b0, CW, RED[0] & valid);
             RED[1] &= RED[0];
             RED[0] = 0u;
         }
@@ -289,7 +293,7 @@ k_ffl(FflArgs a) {
         }
         __syncthreads();
     }
-    block_finish(a, RED, tid, b0, nvalid, valid);
+    block_finish<CW>(a, RED, tid, b0, nvalid, valid);
 }
 
 // ---- sum-product (decoding_type 0): flood's cn_update_sp / k_vn_update on LDS ---------------
@@ -346,6 +350,7 @@ k_ffs(FflArgs a) {
 
     for (int t = 0; t < a.T; ++t) {
         if (tid == 0 && t > 0) {
+            if (a.iter_wrong) put_iter_wrong(a.iter_wrong, a.B, t - 1, b0, CW, RED[0] & valid);
             RED[1] &= RED[0];
             RED[0] = 0u;
         }
@@ -460,7 +465,7 @@ k_ffs(FflArgs a) {
         }
         __syncthreads();
     }
-    block_finish(a, RED, tid, b0, nvalid, valid);
+    block_finish<CW>(a, RED, tid, b0, nvalid, valid);
 }
 
 struct FflPlan {
@@ -583,6 +588,7 @@ int ffl_decode(const DevGraph& g, const Bufs& b, const float* llr, int mode, boo
     a.beta = b.beta;
     a.counters = counters;
     a.flags = flags;
+    a.iter_wrong = b.iter_wrong;
     a.off_tv = p.off_tv;
     a.off_rec = p.off_rec;
     a.off_hd = p.off_hd;

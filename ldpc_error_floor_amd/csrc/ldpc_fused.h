@@ -15,6 +15,10 @@ struct FusedWorkspace {
     size_t bs_lut_bytes = 0;
     uint32_t* bs_bad = nullptr;    // [packs] 1: pack decoded by the v5 fixup
     int64_t bs_bad_n = 0;
+    uint32_t* hdx = nullptr;       // [T][packs][n_vars] bit-sliced hard decisions (bit export of
+    int64_t hdx_elems = 0;         // the bit-sliced kernels; fixup packs are in `hd` instead)
+    bool bits_packed = false;      // the last bit-exporting decode wrote hdx (+ hd for bad packs)
+    const char* last_kernel = "";  // the kernel that served the last decode (ldpc_ctx_last_kernel)
     // what the per-decode table kernels last wrote (they depend only on the graph, the weights
     // and T): a decode with the same key skips them
     uint64_t key_gad[4] = {~0ull, 0, 0, 0}, key_qtab[4] = {~0ull, 0, 0, 0}, key_bslut[4] = {~0ull, 0, 0, 0};
@@ -26,7 +30,13 @@ int64_t fused_bytes_per_cw(const DevGraph& g, int T);
 int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
                  bool ucn, bool want_bits, int ntiles_max, int T_max, int per_edge_w,
                  int64_t* counters, uint8_t* flags, hipStream_t s);
-void fused_bits_view(const FusedWorkspace& ws, Bufs& b);
+// where the last bit-exporting fused decode left its hard decisions (ldpc_capi.hip's HdSrc)
+struct HdView {
+    const uint64_t* tile;      // [T+1][tiles][n_vars][4] (Bufs::hd layout, slot t + 1), or null
+    const uint32_t* pack;      // [T][packs][n_vars] bit-sliced, or null
+    const uint32_t* bad;       // [packs] 1: this pack's bits are in `tile` (v5 fixup)
+};
+HdView fused_bits_view(const FusedWorkspace& ws);
 const char* fused_kernel_name(const DevGraph& g, int mode, int T, float clip_llr, bool ucn,
                               bool per_edge_w);
 
@@ -42,15 +52,18 @@ int fused5_cw(const DevGraph& g, int T);
 
 // bit-sliced (ldpc_bs.hip): 32 codewords per word, counters / flags only, QMS q = 5 / -5
 // (clip: clip_LLR, the LLR of shortened bits)
-bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip);
-const char* bs_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip);
+// (T: the iteration count, whose per-iteration frame words take 4 T bytes of LDS)
+bool bs_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T);
+const char* bs_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T);
+// hdx: null, or [T][packs][n_vars] u32: also store every iteration's hard decisions (bit r of
+// word (t, pack, v) = codeword 32 pack + r; the export build of the kernel)
 int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
-              bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s);
+              bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, uint32_t* hdx, hipStream_t s);
 // compressed bit-sliced kernel (ldpc_bsc.hip): the graphs whose per-edge slots exceed the LDS
-bool bsc_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip);
-const char* bsc_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip);
+bool bsc_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T);
+const char* bsc_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T);
 int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
-               bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, hipStream_t s);
+               bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, uint32_t* hdx, hipStream_t s);
 void fused_free(FusedWorkspace& ws);
 
 // float-mode fused decoder (ldpc_ffl.hip): MS, MS without nudge, QMS q = 6, sum-product; counters / flags

@@ -50,14 +50,14 @@ bool fused_supported(const DevGraph& g, int mode, int T, float clip_llr) {
 // counters-only decodes (throughput mode) run the bit-sliced kernel when it applies
 static bool use_bs(const DevGraph& g, int mode, int T, bool ucn, bool per_edge_w, float clip) {
     const int cw = fused5_cw(g, T);
-    return cw > 0 && cw <= 32 && bs_supported(g, mode, ucn, per_edge_w, clip);
+    return cw > 0 && cw <= 32 && bs_supported(g, mode, ucn, per_edge_w, clip, T);
 }
 
 // the kernel a counters-only decode runs (the throughput / roofline report)
 const char* fused_kernel_name(const DevGraph& g, int mode, int T, float clip_llr, bool ucn,
                               bool per_edge_w) {
     if (!fused_supported(g, mode, T, clip_llr)) return "";
-    if (use_bs(g, mode, T, ucn, per_edge_w, clip_llr)) return bs_kernel_name(g, mode, ucn, per_edge_w, clip_llr);
+    if (use_bs(g, mode, T, ucn, per_edge_w, clip_llr)) return bs_kernel_name(g, mode, ucn, per_edge_w, clip_llr, T);
     return fused5_shape_name(g, T);
 }
 
@@ -74,11 +74,15 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
     // counters-only decodes the bit-sliced kernel serves read their LLRs: with an in-kernel
     // channel requested, the caller (ldpc_decode_awgn) generates them into HBM first — the
     // channel kernel plus the bit-sliced decode beat the v5 kernel's in-prologue channel
-    if (b.awgn && !want_bits && !b.app_out && use_bs(g, mode, b.T, ucn, per_edge_w != 0, b.clip))
+    if (b.awgn && !b.app_out && use_bs(g, mode, b.T, ucn, per_edge_w != 0, b.clip))
         return LDPC_ERR_UNSUPPORTED;
     const float step = mode_step(mode);
     const int cu = clip_units(mode, b.clip);
     uint64_t* hd_out = nullptr;
+    // counters / frame flags / bit exports without APP: the bit-sliced kernel when it applies
+    // (its export build stores every iteration's hard decisions, bit-sliced, in ws.hdx)
+    const bool bs = !b.app_out && !b.awgn && use_bs(g, mode, b.T, ucn, per_edge_w != 0, b.clip);
+    ws.bits_packed = false;
     if (want_bits) {
         const size_t elems = (size_t)(T_max + 1) * ntiles_max * g.n_vars * 4;
         if ((int64_t)elems > ws.hd_elems) {
@@ -95,9 +99,24 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
             return LDPC_ERR_HIP;
         hd_out = ws.hd;
     }
-    if (!want_bits && !b.app_out && !b.awgn && use_bs(g, mode, b.T, ucn, per_edge_w != 0, b.clip)) {
+    if (bs) {
         // bit-sliced kernel; packs whose LLRs are off the quantizer grid go to the v5 kernel
         const int64_t npk = (b.B + 31) / 32;
+        uint32_t* hdx = nullptr;
+        if (want_bits) {
+            const int64_t n = (int64_t)b.T * npk * g.n_vars;
+            if (n > ws.hdx_elems) {
+                if (ws.hdx) (void)hipFree(ws.hdx);
+                ws.hdx = nullptr;
+                ws.hdx_elems = 0;
+                if (hipMalloc(reinterpret_cast<void**>(&ws.hdx), (size_t)n * 4) != hipSuccess) {
+                    (void)hipGetLastError();
+                    return LDPC_ERR_OOM;
+                }
+                ws.hdx_elems = n;
+            }
+            hdx = ws.hdx;
+        }
         if (npk > ws.bs_bad_n) {
             if (ws.bs_bad) (void)hipFree(ws.bs_bad);
             ws.bs_bad = nullptr;
@@ -109,22 +128,31 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
             }
             ws.bs_bad_n = n;
         }
-        int st = bs_decode(g, b, ws, llr, mode, ucn, counters, flags, ws.bs_bad, s);
+        int st = bs_decode(g, b, ws, llr, mode, ucn, counters, flags, ws.bs_bad, hdx, s);
         if (st != LDPC_OK) return st;
+        ws.last_kernel = fused_kernel_name(g, mode, b.T, b.clip, ucn, per_edge_w != 0);
+        ws.bits_packed = want_bits;
         // test hook: LDPC_BS_FIXUP=0 skips the v5 fixup, so a test can tell that a batch was
-        // decoded by the bit-sliced kernel alone (flagged packs then contribute nothing)
-        static const bool fixup = !(getenv("LDPC_BS_FIXUP") && atoi(getenv("LDPC_BS_FIXUP")) == 0);
-        if (!fixup) return LDPC_OK;
-        return fused5_decode(g, b, ws, llr, mode_qmax(mode), step, cu, per_edge_w != 0, nullptr,
+        // decoded by the bit-sliced kernel alone (flagged packs then contribute nothing).  Read
+        // per decode (a test sets it after other decodes ran in the same process).
+        const char* fx = getenv("LDPC_BS_FIXUP");
+        if (fx && atoi(fx) == 0) return LDPC_OK;
+        return fused5_decode(g, b, ws, llr, mode_qmax(mode), step, cu, per_edge_w != 0, hd_out,
                              counters, flags, s, ws.bs_bad);
     }
+    ws.last_kernel = fused5_shape_name(g, b.T);
     return fused5_decode(g, b, ws, llr, mode_qmax(mode), step, cu, per_edge_w != 0, hd_out,
                          counters, flags, s);
 }
 
-void fused_bits_view(const FusedWorkspace& ws, Bufs& b) {
-    b.hd = ws.hd;
-    b.hd_all = 1;
+HdView fused_bits_view(const FusedWorkspace& ws) {
+    HdView v{};
+    v.tile = ws.hd;
+    if (ws.bits_packed) {
+        v.pack = ws.hdx;
+        v.bad = ws.bs_bad;
+    }
+    return v;
 }
 
 void fused_free(FusedWorkspace& ws) {
@@ -142,6 +170,10 @@ void fused_free(FusedWorkspace& ws) {
     if (ws.bs_bad) (void)hipFree(ws.bs_bad);
     ws.bs_bad = nullptr;
     ws.bs_bad_n = 0;
+    if (ws.hdx) (void)hipFree(ws.hdx);
+    ws.hdx = nullptr;
+    ws.hdx_elems = 0;
+    ws.bits_packed = false;
     ws.key_gad[0] = ws.key_qtab[0] = ws.key_bslut[0] = ~0ull;
 }
 

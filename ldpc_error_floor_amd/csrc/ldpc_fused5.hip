@@ -301,6 +301,7 @@ int fused5_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const fl
     }
     a.zmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.z - 1) / (uint64_t)g.z);
     a.only = only;
+    a.iter_wrong = b.iter_wrong;
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // timing only
     // shared tables: one small launch per decode instead of per-workgroup dependent loads
     const size_t nqt = (size_t)b.T * qslice;

@@ -108,6 +108,7 @@ struct F5Args {
     uint32_t zmagic;
     int ablate;        // diagnostic only (LDPC_DIAG_ABLATE): 1 skip CN pass 1, 2 skip pass 2, 4 skip VN
     const uint32_t* only;  // null, or [packs of 32 codewords]: decode only blocks of flagged packs
+    uint32_t* iter_wrong;  // [T][ceil(B/32)] per-iteration frame-error words (zeroed), or null
 };
 
 __device__ __forceinline__ int q_units5(float x, float inv, int qmax) {
@@ -380,6 +381,7 @@ f5_block(const F5Args& a, const float* __restrict__ alpha, const float* __restri
     for (int t = 0; t < a.T; ++t) {
         if (t < 22) F5_STAMP(8 + t);
         if (tid == 0 && t > 0) {        // fold iteration t-1's frame flags (its VN phase is done)
+            if (a.iter_wrong) put_iter_wrong(a.iter_wrong, a.B, t - 1, b0, CW, RED[0] & valid_cw);
             RED[1] &= RED[0];
             RED[0] = 0;
         }
@@ -808,6 +810,7 @@ f5_block(const F5Args& a, const float* __restrict__ alpha, const float* __restri
         const unsigned long long wl = RED[0] & valid_cw;
         const unsigned long long all = RED[1] & RED[0] & valid_cw;
         const unsigned long long ap = RED[2] & valid_cw;
+        if (a.iter_wrong) put_iter_wrong(a.iter_wrong, a.B, a.T - 1, b0, CW, wl);
         if (a.counters) {
             const unsigned long long c0 = RED[3];
             const unsigned long long c1 = __popcll(wl);
@@ -897,7 +900,8 @@ int launch5o(const F5Args& a, int nblocks, int nw, size_t lds, const float* alph
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)F5_LDS_MAX);
         attr = true;
     }
-    if constexpr (!OUT) {               // (fixups are counters / flags only)
+    if constexpr (!PEW) {               // (the bit-sliced kernels serve row-uniform weights only;
+                                        // OUT: their hard-decision export build)
         if (a.only) {
             static bool attr_fix = false;
             if (!attr_fix) {

@@ -54,7 +54,25 @@ struct Bufs {
     float clip;
     const void* awgn;          // AwgnParams* (ldpc_awgn.h): generate the LLRs in the fused
                                // prologue instead of reading them (fused v5 only), or null
+    uint32_t* iter_wrong;      // [T][ceil(B/32)] per-iteration frame-error words, or null
+                               // (ldpc_decode_outputs::iter_wrong; zeroed before the decode)
 };
+
+// per-iteration frame-error words (ldpc_decode_outputs::iter_wrong) of one block of codewords
+// b0 .. b0 + CW - 1 (CW a power of two <= 64, b0 a multiple of CW) at iteration t: `m` holds
+// bit r = codeword b0 + r (already masked to the valid codewords).  Blocks narrower than a word
+// share it, so they OR into the zeroed buffer.
+__device__ inline void put_iter_wrong(uint32_t* iw, int64_t B, int t, int64_t b0, int CW,
+                                      unsigned long long m) {
+    const int64_t nwd = (B + 31) >> 5;
+    uint32_t* row = iw + (size_t)t * nwd;
+    if (CW >= 32) {
+        row[b0 >> 5] = (uint32_t)m;
+        if (CW == 64 && (b0 >> 5) + 1 < nwd) row[(b0 >> 5) + 1] = (uint32_t)(m >> 32);
+    } else if (m) {
+        atomicOr(row + (b0 >> 5), (uint32_t)m << (b0 & 31));
+    }
+}
 
 // hard decisions of iteration s (s = -1: prologue's lw_0) live in slot s+1 (or ring (s+1)&1)
 __host__ __device__ inline size_t hd_index(const Bufs& p, int s, int64_t tile, int v) {

@@ -96,7 +96,7 @@ PYBIND11_MODULE(_ldpc_nms, m) {
         "decode",
         [](Ctx& c, uintptr_t llr, int64_t B, int T, int decoding_type, int q_bit, int target_bits,
            float clip, int kernel, uintptr_t app, uintptr_t hard, uintptr_t synd,
-           uintptr_t counters, uintptr_t flags, uintptr_t stream) {
+           uintptr_t counters, uintptr_t flags, uintptr_t stream, uintptr_t iter_wrong) {
             ldpc_decode_params p = make_params(T, decoding_type, q_bit, target_bits, clip, kernel);
             ldpc_decode_outputs o{};
             o.app_all = reinterpret_cast<float*>(app);
@@ -104,6 +104,7 @@ PYBIND11_MODULE(_ldpc_nms, m) {
             o.synd_bits = reinterpret_cast<uint32_t*>(synd);
             o.counters = reinterpret_cast<int64_t*>(counters);
             o.frame_flags = reinterpret_cast<uint8_t*>(flags);
+            o.iter_wrong = reinterpret_cast<uint32_t*>(iter_wrong);
             int st;
             {
                 py::gil_scoped_release nogil;
@@ -115,12 +116,12 @@ PYBIND11_MODULE(_ldpc_nms, m) {
         py::arg("ctx"), py::arg("llr"), py::arg("B"), py::arg("T"), py::arg("decoding_type"),
         py::arg("q_bit"), py::arg("target_bits"), py::arg("clip"), py::arg("kernel"),
         py::arg("app") = 0, py::arg("hard") = 0, py::arg("synd") = 0, py::arg("counters") = 0,
-        py::arg("flags") = 0, py::arg("stream") = 0);
+        py::arg("flags") = 0, py::arg("stream") = 0, py::arg("iter_wrong") = 0);
     m.def(
         "decode_awgn",
         [](Ctx& c, int64_t B, int T, int decoding_type, int q_bit, int target_bits, float clip,
            int kernel, double sigma, uint64_t seed, int64_t offset, int ps, int pe, int ss, int se,
-           uintptr_t app, uintptr_t counters, uintptr_t flags, uintptr_t stream) {
+           uintptr_t app, uintptr_t counters, uintptr_t flags, uintptr_t stream, uintptr_t iter_wrong) {
             ldpc_decode_params p = make_params(T, decoding_type, q_bit, target_bits, clip, kernel);
             ldpc_channel_params ch{};
             ch.sigma = sigma;
@@ -134,6 +135,7 @@ PYBIND11_MODULE(_ldpc_nms, m) {
             o.app_all = reinterpret_cast<float*>(app);
             o.counters = reinterpret_cast<int64_t*>(counters);
             o.frame_flags = reinterpret_cast<uint8_t*>(flags);
+            o.iter_wrong = reinterpret_cast<uint32_t*>(iter_wrong);
             int st;
             {
                 py::gil_scoped_release nogil;
@@ -145,7 +147,7 @@ PYBIND11_MODULE(_ldpc_nms, m) {
         py::arg("target_bits"), py::arg("clip"), py::arg("kernel"), py::arg("sigma"),
         py::arg("seed"), py::arg("offset"), py::arg("punct_start"), py::arg("punct_end"),
         py::arg("short_start"), py::arg("short_end"), py::arg("app") = 0, py::arg("counters") = 0,
-        py::arg("flags") = 0, py::arg("stream") = 0);
+        py::arg("flags") = 0, py::arg("stream") = 0, py::arg("iter_wrong") = 0);
     m.def(
         "channel_awgn",
         [](uintptr_t llr, int64_t B, int n_vars, double sigma, uint64_t seed, int64_t offset,
@@ -191,10 +193,18 @@ PYBIND11_MODULE(_ldpc_nms, m) {
         [](Ctx& c, int T, int decoding_type, int q_bit, int target_bits, int kernel, float clip) {
             ldpc_decode_params p = make_params(T, decoding_type, q_bit, target_bits, clip, kernel);
             int64_t bytes = 0;
-            char name[32] = {0};
-            check(ldpc_kernel_info(c.h, &p, &bytes, name, 32), "ldpc_kernel_info");
+            char name[64] = {0};
+            check(ldpc_kernel_info(c.h, &p, &bytes, name, 64), "ldpc_kernel_info");
             return py::make_tuple(bytes, std::string(name));
         },
         py::arg("ctx"), py::arg("T"), py::arg("decoding_type"), py::arg("q_bit"),
         py::arg("target_bits"), py::arg("kernel"), py::arg("clip_llr") = 20.0f);
+    m.def(
+        "last_kernel",
+        [](Ctx& c) {
+            char name[64] = {0};
+            check(ldpc_ctx_last_kernel(c.h, name, 64), "ldpc_ctx_last_kernel");
+            return std::string(name);
+        },
+        py::arg("ctx"));
 }

@@ -31,6 +31,13 @@ class DecodeResult:
     synd: Optional["object"] = None         # torch int32 [T, B, ceil(M*z/32)]
     counters: Optional["object"] = None     # torch int64 [4]
     flags: Optional["object"] = None        # torch uint8 [B]
+    iter_wrong: Optional["object"] = None   # torch int32 [T, ceil(B/32)]: bit b%32 of word
+                                            # (t, b//32) = frame b wrong at iteration t
+
+    def frame_errors(self, B: int) -> np.ndarray:
+        """``iter_wrong`` unpacked on the host: bool [T, B] (calc_ber_fer's per-iteration frame
+        error, ``Print_Functions.py:100-118``)."""
+        return unpack_bits(self.iter_wrong.cpu().numpy(), B).astype(bool)
 
     def ya_output_all(self):
         """``ya_output_all`` layout: iterations stacked on axis 0 -> [T*B, Nt*z]."""
@@ -131,10 +138,11 @@ class NMSDecoder:
 
     def decode(self, llr, T: Optional[int] = None, app: bool = True, hard: bool = False,
                synd: bool = False, counters=None, flags: bool = False, kernel: Optional[str] = None,
-               stream=None, target_bits: Optional[int] = None) -> DecodeResult:
+               stream=None, target_bits: Optional[int] = None, iter_wrong: bool = False) -> DecodeResult:
         """Decode a batch.  ``counters`` may be a caller-owned int64[4] device tensor that is
         accumulated into (``+=``); pass ``True`` to get a fresh one.  ``target_bits``
-        overrides the output / FER bit range (default Nt*z)."""
+        overrides the output / FER bit range (default Nt*z).  ``iter_wrong``: the per-iteration
+        frame-error words (every kernel, the counters-only ones included)."""
         torch = self._torch
         T = self.T if T is None else int(T)
         nt = self.target_bits if target_bits is None else int(target_bits)
@@ -143,7 +151,7 @@ class NMSDecoder:
         llr = self._as_llr(llr)
         B = int(llr.shape[0])
         if B == 0:
-            return self._empty_result(T, nt, hard, synd, counters, flags, app)
+            return self._empty_result(T, nt, hard, synd, counters, flags, app, iter_wrong)
         ctx = self._ensure_ctx(B, T)
         res = DecodeResult()
         dev = self.device
@@ -165,16 +173,22 @@ class NMSDecoder:
             res.flags = flags
         elif flags:
             res.flags = torch.empty(B, dtype=torch.uint8, device=dev)
+        if iter_wrong:
+            res.iter_wrong = torch.empty((T, (B + 31) // 32), dtype=torch.int32, device=dev)
         if stream is None:
             stream = torch.cuda.current_stream(dev)
         ptr = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
         self._ext.decode(ctx, llr.data_ptr(), B, T, self.decoding_type, self.q_bit,
                          nt, self.clip, KERNELS[kernel or self.kernel],
                          ptr(res.app), ptr(res.hard), ptr(res.synd), ptr(res.counters),
-                         ptr(res.flags), stream.cuda_stream)
+                         ptr(res.flags), stream.cuda_stream, ptr(res.iter_wrong))
         return res
 
-    def _empty_result(self, T, nt, hard, synd, counters, flags, app):
+    def last_kernel(self) -> str:
+        """The kernel that served this decoder's last decode (``ldpc_ctx_last_kernel``)."""
+        return "" if self._ctx is None else self._ext.last_kernel(self._ctx)
+
+    def _empty_result(self, T, nt, hard, synd, counters, flags, app, iter_wrong=False):
         """An empty batch decodes to empty outputs; a caller's counters are left unchanged."""
         torch = self._torch
         dev = self.device
@@ -192,11 +206,13 @@ class NMSDecoder:
             res.flags = flags[:0]
         elif flags:
             res.flags = torch.empty(0, dtype=torch.uint8, device=dev)
+        if iter_wrong:
+            res.iter_wrong = torch.empty((T, 0), dtype=torch.int32, device=dev)
         return res
 
     def decode_awgn(self, B: int, sigma: float, seed: int, offset: int = 0, punct=None, short=None,
                     T: Optional[int] = None, app: bool = False, counters=None, flags=None,
-                    kernel: Optional[str] = None, stream=None) -> DecodeResult:
+                    kernel: Optional[str] = None, stream=None, iter_wrong: bool = False) -> DecodeResult:
         """Decode B codewords whose LLRs come from the on-GPU AWGN channel, generated inside
         the decoder (``ldpc_decode_awgn``): identical to ``decode(awgn(...))`` without the
         LLRs ever being written to HBM.  ``counters`` / ``flags`` as in ``decode``."""
@@ -205,7 +221,7 @@ class NMSDecoder:
         punct = getattr(self, "punct", (0, 0)) if punct is None else punct
         short = getattr(self, "short", (0, 0)) if short is None else short
         if int(B) == 0:
-            return self._empty_result(T, self.target_bits, False, False, counters, flags, app)
+            return self._empty_result(T, self.target_bits, False, False, counters, flags, app, iter_wrong)
         ctx = self._ensure_ctx(int(B), T)
         dev = self.device
         res = DecodeResult()
@@ -223,6 +239,8 @@ class NMSDecoder:
             res.flags = flags
         elif flags:
             res.flags = torch.empty(B, dtype=torch.uint8, device=dev)
+        if iter_wrong:
+            res.iter_wrong = torch.empty((T, (int(B) + 31) // 32), dtype=torch.int32, device=dev)
         if stream is None:
             stream = torch.cuda.current_stream(dev)
         ptr = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
@@ -230,7 +248,7 @@ class NMSDecoder:
                               self.clip, KERNELS[kernel or self.kernel], float(sigma), int(seed),
                               int(offset), int(punct[0]), int(punct[1]), int(short[0]),
                               int(short[1]), ptr(res.app), ptr(res.counters), ptr(res.flags),
-                              stream.cuda_stream)
+                              stream.cuda_stream, ptr(res.iter_wrong))
         return res
 
     def collect_uncorrected(self, flags, llr, stream=None):

@@ -23,7 +23,8 @@ import numpy as np
 from .channel import append_uncor_rows, create_mix_epoch, read_uncor_llr, write_uncor_file
 from .metrics import Counters, calc_ber_fer
 
-__all__ = ["compute_results", "fer_sweep", "shard_range", "SweepCheckpoint", "collect_uncor_inputs"]
+__all__ = ["compute_results", "fer_sweep", "shard_range", "SweepCheckpoint", "collect_uncor_inputs",
+           "decoder_fingerprint"]
 
 
 def compute_results(sample_num, input_llr, input_codeword, SNR_sigma, wordRandom, noiseRandom,
@@ -111,18 +112,42 @@ class SweepCheckpoint:
         os.replace(tmp, self.path)
 
 
+def decoder_fingerprint(decoder, T=None):
+    """What a checkpointed sweep decoded with: graph, lifting, mode, clip, weights, iterations
+    (a resume with another decoder would add its counters to the old ones)."""
+    import hashlib
+    h = hashlib.sha256()
+    proto = getattr(getattr(decoder, "graph", None), "proto", None)
+    if proto is None:
+        proto = getattr(decoder, "proto", None)
+    if proto is not None:
+        h.update(np.ascontiguousarray(np.asarray(proto, np.int64)).tobytes())
+    W = getattr(decoder, "weights", None) or getattr(decoder, "W", None)
+    for a in (getattr(W, "alpha", None), getattr(W, "alpha_ucn", None), getattr(W, "beta", None)):
+        if a is not None:
+            h.update(np.ascontiguousarray(np.asarray(a, np.float32)).tobytes())
+        h.update(b"|")
+    return {"graph_weights_sha256": h.hexdigest()[:32], "z": int(getattr(decoder, "z", 0)),
+            "decoding_type": int(getattr(decoder, "decoding_type", getattr(decoder, "dt", -1))),
+            "q_bit": int(getattr(decoder, "q_bit", getattr(decoder, "q", 0))),
+            "clip": float(getattr(decoder, "clip", 20.0)),
+            "target_bits": int(getattr(decoder, "target_bits", 0)),
+            "T": int(getattr(decoder, "T", 0) if T is None else T)}
+
+
 def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T=None,
               punct=None, short=None, kernel=None, group=None, progress=None,
               uncor_path=None, checkpoint=None, checkpoint_every: int = 64,
-              resume: bool = False):
+              resume: bool = False, point_seeds=None):
     """Decode ``n_codewords`` per SNR point (split across ranks) with GPU LLRs and device
     counters.  Returns a list of ``Counters`` (global totals on every rank).
 
     ``punct`` / ``short``: 1-based inclusive ranges of the channel (``create_mix_epoch``,
     ``Print_Functions.py:29-72``); ``None`` uses the decoder's own (``Decoder(..., punct,
     short)`` / ``build_session``).  SNR point ``si`` uses the Philox stream ``seed + 7919 si``
-    indexed by the global codeword number, so any partition of the codewords (ranks, batches,
-    a resume) decodes the same words.
+    (or ``point_seeds[si]``: callers that sweep the same SNR in separate runs give each point
+    its own stream) indexed by the global codeword number, so any partition of the codewords
+    (ranks, batches, a resume) decodes the same words.
 
     ``uncor_path``: append the frames wrong at every iteration to this file in the
     ``Uncor.txt`` format (``sampling_type == 2``, ``Print_Functions.py:155-156``), collected on
@@ -137,6 +162,11 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
     rank = dist.get_rank(group) if dist_on else 0
     world = dist.get_world_size(group) if dist_on else 1
     sigmas = np.atleast_1d(np.asarray(sigmas, np.float64))
+    if point_seeds is None:
+        point_seeds = [seed + 7919 * si for si in range(sigmas.size)]
+    point_seeds = [int(x) for x in point_seeds]
+    if len(point_seeds) != sigmas.size:
+        raise ValueError("point_seeds needs one seed per SNR point")
     dev = decoder.device
     punct = tuple(getattr(decoder, "punct", (0, 0)) if punct is None else punct)
     short = tuple(getattr(decoder, "short", (0, 0)) if short is None else short)
@@ -151,11 +181,17 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
     si0, pos0 = 0, begin
     if checkpoint is not None:
         ck = SweepCheckpoint(checkpoint if world == 1 else f"{checkpoint}.rank{rank}")
-        key = {"seed": int(seed), "sigmas": [float(x) for x in sigmas],
+        key = {"seed": int(seed), "point_seeds": point_seeds, "sigmas": [float(x) for x in sigmas],
                "n_codewords": int(n_codewords), "batch": int(batch),
                "T": None if T is None else int(T), "punct": list(punct), "short": list(short),
-               "rank": rank, "world": world, "uncor": upath is not None}
+               "rank": rank, "world": world, "uncor": upath is not None,
+               "decoder": decoder_fingerprint(decoder, T)}
         st = ck.load() if resume else None
+        if st is None and upath is not None and os.path.exists(upath):
+            # a sweep that starts from the beginning owns its uncorrected-word file: rows left by
+            # an earlier attempt (e.g. one that died before its first checkpoint) would be
+            # written again
+            os.remove(upath)
         if st is not None:
             if st["key"] != key:
                 raise ValueError(f"{ck.path}: checkpoint is for {st['key']}, this sweep is {key}")
@@ -178,10 +214,10 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
             b = min(batch, end - pos)
             if fused_channel:
                 # LLRs generated inside the decoder (ldpc_decode_awgn): no HBM round trip
-                decoder.decode_awgn(b, float(sigma), seed + 7919 * si, offset=pos, punct=punct,
+                decoder.decode_awgn(b, float(sigma), point_seeds[si], offset=pos, punct=punct,
                                     short=short, T=T, counters=counters[si], kernel=kernel)
             else:
-                decoder.awgn(b, float(sigma), seed + 7919 * si, offset=pos, punct=punct,
+                decoder.awgn(b, float(sigma), point_seeds[si], offset=pos, punct=punct,
                              short=short, out=llr[:b])
                 decoder.decode(llr[:b], T=T, app=False, counters=counters[si], kernel=kernel,
                                flags=None if flags is None else flags[:b])
@@ -197,7 +233,8 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
                 progress(si, pos - begin, end - begin)
         if ck is not None:
             save(si + 1, begin, done=(si + 1 == sigmas.size))
-    if dist_on and world > 1:
+    if dist_on:
+        # (a world of one included: the same collective the multi-GPU job runs)
         dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
     host = counters.cpu().numpy()
     return [Counters.from_array(host[i], int(n_codewords), decoder.n_vars)

@@ -7,6 +7,13 @@ X, net_dict['ya']: Y, net_dict['etha']: e, net_dict['learn_rate']: 0})``
 ``net_dict`` maps the same keys to string handles and ``sess.run`` accepts those handles
 (a single one or a list) plus ``ya_output{t}`` / ``ya_output_target{t}``.  The batch size is
 fixed like the reference's placeholders (``main_Base.py:124-125``): a different B raises.
+
+Parity mode on several GPUs (SURVEY §8 e: "host-generated LLRs, sliced by rank"): with
+``torch.distributed`` initialised, every rank runs the same host loop (``compute_results`` with
+the same seeds, so every rank holds the same ``xa``), decodes its contiguous slice of the batch
+(``fer.shard_range``) and ``all_gather``s the APP slices, so ``sess.run`` returns the whole
+``ya_output_all`` on every rank and every rank computes the same ``Results``.  The reference
+itself runs one process per GPU with no exchange (``main_Base.py:14-15``).
 """
 from __future__ import annotations
 
@@ -33,13 +40,44 @@ def make_net_dict(T: int):
 
 class Session:
     def __init__(self, decoder: NMSDecoder, batch_size: int, T=None, loss_type: int = 2,
-                 loss_t_first=None):
+                 loss_t_first=None, group=None):
         self.decoder = decoder
         self.batch_size = int(batch_size)
         self.T = decoder.T if T is None else int(T)
         self.loss_type = loss_type
         self.loss_t_first = loss_t_first
+        self.group = group
         self.calls = 0
+
+    def _decode_app(self, X, target_bits=None):
+        """APP [T, B, bits] of the host batch X on the host: this rank's slice decoded, the
+        others gathered (one all_gather of equal-size padded slices)."""
+        import torch
+        import torch.distributed as dist
+        from .fer import shard_range
+        B = X.shape[0]
+        dist_on = dist.is_available() and dist.is_initialized()
+        world = dist.get_world_size(self.group) if dist_on else 1
+        if world == 1:
+            return self.decoder.decode(X, T=self.T, app=True, target_bits=target_bits).app.cpu().numpy()
+        rank = dist.get_rank(self.group)
+        b0, b1 = shard_range(B, rank, world)
+        nb = target_bits or self.decoder.target_bits
+        per = -(-B // world)
+        # RCCL gathers device tensors; gloo (CPU rehearsal) host tensors
+        on_dev = dist.get_backend(self.group) == "nccl"
+        dev = self.decoder.device if on_dev else torch.device("cpu")
+        part = torch.zeros((self.T, per, nb), dtype=torch.float32, device=dev)
+        if b1 > b0:
+            app = self.decoder.decode(X[b0:b1], T=self.T, app=True, target_bits=target_bits).app
+            part[:, :b1 - b0] = app.to(dev)
+        parts = [torch.empty_like(part) for _ in range(world)]
+        dist.all_gather(parts, part, group=self.group)
+        out = np.empty((self.T, B, nb), np.float32)
+        for r in range(world):
+            r0, r1 = shard_range(B, r, world)
+            out[:, r0:r1] = parts[r][:, :r1 - r0].cpu().numpy()
+        return out
 
     def run(self, fetches, feed_dict):
         single = not isinstance(fetches, (list, tuple))
@@ -52,8 +90,7 @@ class Session:
         if B != self.batch_size:
             raise ValueError(f"xa batch {B} != placeholder batch {self.batch_size} "
                              "(the reference's placeholders have a fixed batch size)")
-        res = self.decoder.decode(X.reshape(B, -1), T=self.T, app=True)
-        app = res.app.cpu().numpy()                           # [T, B, Nt*z]
+        app = self._decode_app(X.reshape(B, -1))              # [T, B, Nt*z]
         self.calls += 1
         out = []
         T = self.T
@@ -73,8 +110,7 @@ class Session:
                     out.append(app[t])
                 else:
                     if full is None:
-                        full = self.decoder.decode(X.reshape(B, -1), T=T, app=True,
-                                                   target_bits=self.decoder.n_vars).app.cpu().numpy()
+                        full = self._decode_app(X.reshape(B, -1), target_bits=self.decoder.n_vars)
                     out.append(full[t])
             else:
                 raise KeyError(f"unsupported fetch {k!r}")
@@ -82,8 +118,10 @@ class Session:
 
 
 def build_session(cfg: NMSConfig, proto=None, weights: DecoderWeights = None, device=None,
-                  kernel: str = "auto", graph_dir=None):
-    """Decoder + Session + net_dict for a reference-style config."""
+                  kernel: str = "auto", graph_dir=None, group=None):
+    """Decoder + Session + net_dict for a reference-style config (``group``: the process group
+    a multi-GPU parity run shards each batch over; default: the default group when
+    ``torch.distributed`` is initialised)."""
     import os
     from .code import default_graph_dir
     cfg.validate()
@@ -104,5 +142,5 @@ def build_session(cfg: NMSConfig, proto=None, weights: DecoderWeights = None, de
     dec.punct = (int(cfg.punct_start), int(cfg.punct_end))
     dec.short = (int(cfg.short_start), int(cfg.short_end))
     t_first = max(cfg.iters_max - cfg.iter_step - cfg.fixed_init, cfg.fixed_iter)
-    sess = Session(dec, cfg.batch_size, T, cfg.loss_type, t_first)
+    sess = Session(dec, cfg.batch_size, T, cfg.loss_type, t_first, group=group)
     return sess, make_net_dict(T)

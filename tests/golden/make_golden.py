@@ -345,6 +345,19 @@ def main():
                               fixed_iter=4)
         g_wman = decoder_case(MF, PF, "wman_111_q5", "wman_N0576_R34_z24", 24, [1, 1, 2],
                               2, 5, 10, 8, 2.0, random_weights=(0.4, 1.2), g=g_wman)
+    if want("sys_bitsliced"):
+        # systematic output (main_Base.py:83-86: target_node = N - M) on configurations the
+        # bit-sliced counters-only kernels serve: wman [3,0,3] q5 with the trained weights, and
+        # 5G BG2 [2,2,2] with puncture / shortening (row / column weights, UCN)
+        g_wman = decoder_case(MF, PF, "wman_303_sys_q5_snr2.5", "wman_N0576_R34_z24", 24,
+                              [3, 0, 3], 2, 5, 20, 24, 2.5,
+                              blocks={0: wman_blocks[0], 2: wman_blocks[2]}, target_node=18,
+                              g=g_wman)
+        _, gb = read_blocks(os.path.join(
+            REF, "Results/5G/5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640_Weight_End50.txt"))
+        decoder_case(MF, PF, "g5bg2_222_sys_q5_snr1.75",
+                     "5G_LDPC_R0.50_n_dec1280_n1024_k512_z64_s513_640", 64, [2, 2, 2], 2, 5,
+                     20, 12, 1.75, blocks=gb, target_node=10, ps=1, pe=128, ss=513, se=640)
     if want("wifi"):
         _, wb = read_blocks(os.path.join(REF, "Results/WIFI/Weights_Iter50.txt"))
         decoder_case(MF, PF, "wifi_333_q5_snr3.0", "802_11n_N648_R56_z27", 27, [3, 3, 3], 2,

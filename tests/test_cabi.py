@@ -38,7 +38,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_version_and_status_strings(lib):
-    assert lib.ldpc_abi_version() == 1
+    assert lib.ldpc_abi_version() == 2
     lib.ldpc_status_string.restype = ctypes.c_char_p
     assert lib.ldpc_status_string(0) == b"ok"
     assert b"argument" in lib.ldpc_status_string(-1)
@@ -57,6 +57,8 @@ def test_argument_validation_without_gpu(lib):
     assert lib.ldpc_ctx_destroy(None) == -1
     assert lib.ldpc_decode(None, None, 1, None, None, None) == -1
     assert lib.ldpc_ctx_create(None, 10, 10, ctypes.byref(out)) == -1
+    buf = ctypes.create_string_buffer(16)
+    assert lib.ldpc_ctx_last_kernel(None, buf, 16) == -1
     lib.ldpc_channel_awgn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                       ctypes.c_double, ctypes.c_uint64, ctypes.c_int64] + \
         [ctypes.c_int32] * 6 + [ctypes.c_float, ctypes.c_void_p]

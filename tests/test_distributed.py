@@ -112,3 +112,52 @@ def test_bench_launcher_spawns_and_propagates_failure():
     assert r.returncode != 0
     assert "rank 0: LOCAL_RANK 0" in r.stderr and "rank 1: LOCAL_RANK 1" in r.stderr
     assert "exited with status" in r.stderr
+
+
+def _session_worker(rank, world, port, q):
+    """One rank of the parity-mode FER loop: the reference's compute_results over a Session
+    that decodes this rank's slice of every host batch and gathers the rest (gloo)."""
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        from ldpc_error_floor_amd import fer
+        from ldpc_error_floor_amd.session import Session, make_net_dict
+        d = np.load(os.path.join(GOLDEN, "results_wman_303.npz"))
+        dec = _make_decoder()
+        calls = []
+        inner = dec.decode
+
+        def spy(llr, **kw):                       # record the slice sizes this rank decodes
+            calls.append(np.asarray(llr).shape[0])
+            return inner(llr, **kw)
+        dec.decode = spy
+        sess = Session(dec, batch_size=int(d["B"]))
+        wr, nr = np.random.RandomState(2044), np.random.RandomState(1076)
+        Results, _ = fer.compute_results(int(d["sample_num"]), [], [], d["sigma"], wr, nr,
+                                         int(d["B"]), 0, 24, 6, 24, True, 20, sess,
+                                         make_net_dict(20), 0, 2, 0, 0, 0, 0, 5, 20.0)
+        q.put((rank, Results.tolist(), calls))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_session_parity_mode_sharded_over_ranks():
+    """SURVEY §8 e parity mode: host-generated LLRs sliced by rank.  Two gloo ranks each decode
+    half of every 120-codeword batch and all_gather the APP; both reproduce the reference's own
+    compute_results Results (tests/golden/results_wman_303.npz) exactly."""
+    d = np.load(os.path.join(GOLDEN, "results_wman_303.npz"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_session_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (res, calls)) for r, res, calls in (q.get(timeout=600) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    B = int(d["B"])
+    for r in (0, 1):
+        np.testing.assert_array_equal(np.asarray(got[r][0], np.float32), d["Results"])
+        b0, b1 = shard_range(B, r, 2)
+        assert set(got[r][1]) == {b1 - b0}         # only its own slice, every call

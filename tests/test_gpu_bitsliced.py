@@ -32,10 +32,14 @@ def _wman(device, sharing=(3, 0, 3), q=5, T=20, seed=3):
 
 
 def _both(dec, llr):
-    out = {}
+    """Counters and flags of flood and of the fused (bit-sliced) counters-only kernel; their
+    per-iteration frame-error words must agree too."""
+    out, iw = {}, {}
     for k in ("flood", "fused"):
-        r = dec.decode(llr, app=False, counters=True, flags=True, kernel=k)
+        r = dec.decode(llr, app=False, counters=True, flags=True, kernel=k, iter_wrong=True)
         out[k] = (r.counters.cpu().numpy(), r.flags.cpu().numpy())
+        iw[k] = r.iter_wrong.cpu().numpy()
+    assert np.array_equal(iw["fused"], iw["flood"]), dec.last_kernel()
     return out
 
 

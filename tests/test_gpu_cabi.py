@@ -20,7 +20,7 @@ class Params(ctypes.Structure):
 
 class Outputs(ctypes.Structure):
     _fields_ = [("app_all", vp), ("hard_bits", vp), ("synd_bits", vp),
-                ("counters", vp), ("frame_flags", vp)]
+                ("counters", vp), ("frame_flags", vp), ("iter_wrong", vp)]
 
 
 @pytest.mark.parametrize("kernel", [1, 2])
@@ -47,7 +47,7 @@ def test_ctypes_decode_matches_reference(cuda_device, kernel):
     app = torch.empty((T, B, N * z), dtype=torch.float32, device=cuda_device)
     cnt = torch.zeros(4, dtype=torch.int64, device=cuda_device)
     p = Params(T, 2, 5, N * z, 20.0, kernel)
-    o = Outputs(app.data_ptr(), None, None, cnt.data_ptr(), None)
+    o = Outputs(app.data_ptr(), None, None, cnt.data_ptr(), None, None)
     st = lib.ldpc_decode(ctx, vp(llr.data_ptr()), ctypes.c_int64(B), ctypes.byref(p),
                          ctypes.byref(o), vp(torch.cuda.current_stream().cuda_stream))
     assert st == 0, lib.ldpc_status_string(st)
@@ -62,5 +62,41 @@ def test_ctypes_decode_matches_reference(cuda_device, kernel):
     p3 = Params(T, 2, 7, N * z, 20.0, kernel)      # invalid q_bit
     assert lib.ldpc_decode(ctx, vp(llr.data_ptr()), ctypes.c_int64(B), ctypes.byref(p3),
                            ctypes.byref(o), None) == -1
+    assert lib.ldpc_ctx_destroy(ctx) == 0
+    assert lib.ldpc_graph_destroy(g) == 0
+
+
+def test_ctypes_counters_only_per_iteration(cuda_device):
+    """The throughput path through the raw ABI: a counters-only decode (the bit-sliced kernel
+    the bench times) with the per-iteration frame-error words, and ldpc_ctx_last_kernel."""
+    import torch
+    lib = ctypes.CDLL(os.path.join(ROOT, "ldpc_error_floor_amd", "libldpc_nms.so"))
+    c = load_case("wman_303_q5_snr2.0")
+    g_ = c["g"]
+    M, N, z, T = g_.M, g_.N, c["z"], c["T"]
+    B = c["llr"].shape[0]
+    W = c["W"]
+    proto = np.ascontiguousarray(g_.proto, np.int32)
+    g = vp()
+    assert lib.ldpc_graph_create(proto.ctypes.data_as(vp), M, N, z, 0, ctypes.byref(g)) == 0
+    alpha = np.ascontiguousarray(W.alpha, np.float32)
+    beta = np.ascontiguousarray(W.beta, np.float32)
+    assert lib.ldpc_weights_set(g, T, alpha.ctypes.data_as(vp), None, beta.ctypes.data_as(vp)) == 0
+    ctx = vp()
+    assert lib.ldpc_ctx_create(g, ctypes.c_int64(B), T, ctypes.byref(ctx)) == 0
+    llr = torch.as_tensor(c["llr"], dtype=torch.float32, device=cuda_device)
+    cnt = torch.zeros(4, dtype=torch.int64, device=cuda_device)
+    iw = torch.full((T, (B + 31) // 32), -1, dtype=torch.int32, device=cuda_device)
+    p = Params(T, 2, 5, N * z, 20.0, 0)
+    o = Outputs(None, None, None, cnt.data_ptr(), None, iw.data_ptr())
+    assert lib.ldpc_decode(ctx, vp(llr.data_ptr()), ctypes.c_int64(B), ctypes.byref(p),
+                           ctypes.byref(o), vp(torch.cuda.current_stream().cuda_stream)) == 0
+    torch.cuda.synchronize()
+    name = ctypes.create_string_buffer(64)
+    assert lib.ldpc_ctx_last_kernel(ctx, name, 64) == 0
+    assert name.value.startswith(b"bsl["), name.value
+    from ldpc_error_floor_amd.decoder import unpack_bits
+    want = (c["app"] >= 0).any(axis=2)
+    assert np.array_equal(unpack_bits(iw.cpu().numpy(), B).astype(bool), want)
     assert lib.ldpc_ctx_destroy(ctx) == 0
     assert lib.ldpc_graph_destroy(g) == 0

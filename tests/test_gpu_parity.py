@@ -24,7 +24,8 @@ def _decoder(c, kernel, device):
     dec = NMSDecoder(c["g"].proto, c["z"], c["W"], c["dt"], c["q"], target_node=Nt,
                      device=device, kernel=kernel)
     if not dec.supports(kernel):
-        pytest.skip(f"{kernel} kernel does not support this configuration")
+        pytest.skip(f"{kernel} kernel does not support this configuration "
+                    f"(decoding_type {c['dt']}, q {c['q']}, graph {c['g'].M}x{c['g'].N} z={c['z']})")
     return dec
 
 
@@ -38,7 +39,7 @@ def test_extension_is_native(cuda_device):
     from ldpc_error_floor_amd import _native
     mod = _native.load()
     assert mod.__file__.startswith(os.path.join(ROOT, "ldpc_error_floor_amd"))
-    assert mod.abi_version() == 1
+    assert mod.abi_version() == 2
 
 
 @pytest.mark.parametrize("kernel", KERNEL_NAMES)

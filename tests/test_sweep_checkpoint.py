@@ -98,3 +98,53 @@ def test_collect_uncor_inputs_roundtrip(tmp_path):
     x = -np.concatenate([tr, va, te])             # files hold negated LLRs
     o = nms_oracle.decode(x, dec.proto, 24, dec.W.alpha, dec.W.alpha_ucn, dec.W.beta, 20, 2, 5)
     assert np.all(flags_from_app(o["app"]) & 1)
+
+
+def test_resume_refuses_a_different_decoder(tmp_path):
+    """The checkpoint key carries the decoder (graph + weights hash, z, mode, q, clip, T): a
+    resume with other weights or another iteration count is refused instead of adding the old
+    counters to the new run."""
+    from ldpc_error_floor_amd.weights import flat_weights
+    from ldpc_error_floor_amd.code import TannerGraph
+    dec = _make_decoder()
+    ck = str(tmp_path / "d.ckpt")
+    with pytest.raises(Stop):
+        fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=3, checkpoint=ck, checkpoint_every=1,
+                  progress=_interrupt_after(2))
+    other = _make_decoder()
+    other.W = flat_weights(TannerGraph(other.proto, 24), 20, alpha=0.7, beta=1.0)
+    with pytest.raises(ValueError, match="checkpoint is for"):
+        fer_sweep(other, SIGMAS, N_CW, BATCH, seed=3, checkpoint=ck, resume=True)
+    with pytest.raises(ValueError, match="checkpoint is for"):
+        fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=3, T=12, checkpoint=ck, resume=True)
+    # the same decoder resumes
+    full = _tuples(fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=3))
+    assert _tuples(fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=3, checkpoint=ck, resume=True)) == full
+
+
+@pytest.mark.parametrize("resume", [False, True])
+def test_fresh_start_replaces_stale_uncorrected_file(tmp_path, resume):
+    """A checkpointed sweep that starts from the beginning (no checkpoint yet, or resume off)
+    owns its uncorrected-word file: rows an earlier attempt left are not kept."""
+    dec = _make_decoder()
+    ref_path = str(tmp_path / "ref.txt")
+    fer_sweep(dec, SIGMAS[:1], N_CW, BATCH, seed=5, uncor_path=ref_path)
+    path = tmp_path / "Uncor.txt"
+    path.write_text("0.0\t0.0\tstale row from an attempt that died before its first checkpoint\n")
+    fer_sweep(dec, SIGMAS[:1], N_CW, BATCH, seed=5, uncor_path=str(path),
+              checkpoint=str(tmp_path / "n.ckpt"), resume=resume)
+    assert path.read_text() == open(ref_path).read()
+
+
+def test_point_seeds_decouple_points_from_their_position():
+    """point_seeds: a point's stream is the caller's, not its index in the list (a sweep of one
+    SNR run twice with different seeds decodes different noise; with the default seeding the
+    first point of any call would reuse seed + 0)."""
+    dec = _make_decoder()
+    a = _tuples(fer_sweep(dec, SIGMAS[1:], N_CW, BATCH, seed=1076))
+    b = _tuples(fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=1076, point_seeds=[1076, 1076]))
+    c = _tuples(fer_sweep(dec, SIGMAS[1:], N_CW, BATCH, point_seeds=[1076 + 7919]))
+    d = _tuples(fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=1076))
+    assert b[1] == a[0] and c[0] == d[1]
+    with pytest.raises(ValueError):
+        fer_sweep(dec, SIGMAS, N_CW, BATCH, point_seeds=[1])

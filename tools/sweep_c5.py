@@ -55,13 +55,20 @@ def main():
             last[0] = time.time()
             print(f"  snr {snrs_cur[si]:.2f} dB: {done}/{total} codewords", flush=True)
 
+    def point_seed(snr, stage):
+        """1076 + 7919 x (SNR in millidecibels) + a per-stage offset: a function of the SNR value
+        and the stage only (deep points do not reuse the scan's codewords either)."""
+        return 1076 + 7919 * int(round(snr * 1000)) + (0 if stage == "scan" else 104729)
+
     def run(stage, idx, n):
         global snrs_cur
         snrs_cur = [snrs[i] for i in idx]
         t0 = time.time()
+        # one Philox stream per SNR value (not per position in this call's list): the scan, the
+        # deep stage and separate --deep-snrs runs of different SNRs never share noise
         res = fer_sweep(dec, [sig[i] for i in idx], n, a.batch, seed=1076, progress=progress,
                         checkpoint=os.path.join(a.out, f"ckpt_{stage}.json"), checkpoint_every=16,
-                        resume=True)
+                        resume=True, point_seeds=[point_seed(snrs[i], stage) for i in idx])
         dt = time.time() - t0
         rows = []
         for i, c in zip(idx, res):
@@ -86,7 +93,7 @@ def main():
     n_total = a.scan * len(scan) + a.deep * len(set(deep_idx))
     out = {"workload": "C5: 5G_LDPC_R0.73_n_dec2304_n2112_k1536_z72_s1537_1584, QMS q5, T=50, "
                        "flat [3,0,3] alpha=0.75 beta=1, puncture 1-144, shorten 1537-1584, "
-                       "on-GPU Philox AWGN (seed 1076 + 7919 x SNR index), all-zero codeword",
+                       "on-GPU Philox AWGN (seed 1076 + 7919 x SNR in mdB, + 104729 in the deep stage), all-zero codeword",
            "kernel": kernel, "scan": scan, "deep": deep,
            "seconds": {"scan": round(t_scan, 1), "deep": round(t_deep, 1)},
            "codewords_total": n_total,

@@ -93,6 +93,14 @@ def display_name(prof):
     raise SystemExit("no 'kernel <name>' line in trace.log")
 
 
+def src_fingerprint():
+    """The native sources' fingerprint (ldpc_error_floor_amd.build.source_fingerprint): bench.py
+    uses this profile's PMC figures only while the sources are unchanged."""
+    sys.path.insert(0, ROOT)
+    from ldpc_error_floor_amd.build import source_fingerprint
+    return source_fingerprint()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof")
@@ -130,6 +138,7 @@ def main():
           "wait_any_frac": (round(pm["SQ_WAIT_ANY"] / pm["SQ_WAVE_CYCLES"], 4)
                             if "SQ_WAIT_ANY" in pm and pm.get("SQ_WAVE_CYCLES") else None),
           "valu_busy": valu_busy(pm, avg_ns),
+          "src_fingerprint": src_fingerprint(),
           "lds_busy": lds_busy(pm),
           "method": "2 x FETCH_SIZE + WRITE_SIZE (KiB), separate --pmc passes, gfx950 "
                     "FETCH_SIZE half-count correction (MI355X_MICROARCH.md, HBM)"}
