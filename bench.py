@@ -109,10 +109,11 @@ def _cpu_worker(proto, W, X, T, barrier, q):
         q.put(time.perf_counter() - t0)
 
 
-def cpu_baseline(proto, g, W, cp, B=120, T=20, snr=3.5):
+def cpu_baseline(proto, g, W, cp, B=480, T=20, snr=3.5):
     """Dense TF-graph-equivalent numpy decoder on the C1 sample, sharded over worker processes.
 
-    The C1 batch is split into contiguous slices (fer.shard_range), one per worker process
+    B = 480: four C1 batches (the first 480 codewords of the C1 stream), about 15 s of CPU work
+    on the GPU box's 16 cores.  The batch is split into contiguous slices (fer.shard_range), one per worker process
     (spawned: fresh interpreters, nothing inherited from this process's HIP state), each
     decoding single-threaded after all have built their dense graph; value = B / the slowest
     worker's decode time.  Workers = the host cores this process may use, capped by the box's
@@ -155,9 +156,10 @@ def cpu_baseline(proto, g, W, cp, B=120, T=20, snr=3.5):
     return {"value": round(B / dt, 3), "unit": "codewords/s", "cores": workers, "kind": "port",
             "threads": f"{workers} worker processes x 1 thread (threadpoolctl), one contiguous "
                        f"slice of the batch each; {cores} cores in this process's affinity",
-            "sample": f"C1: wman QMS q5 T={T}, B={B} host-channel codewords at {snr} dB (seeds "
-                      f"2044/1076), dense TF-graph-equivalent numpy (oracle/nms_dense.py), "
-                      f"slowest worker {dt:.1f} s (per worker: {min(times):.1f}-{dt:.1f} s)",
+            "sample": f"C1 x {B // 120}: wman QMS q5 T={T}, the first {B} host-channel codewords at "
+                      f"{snr} dB (seeds 2044/1076, compute_results order), dense TF-graph-equivalent "
+                      f"numpy (oracle/nms_dense.py), slowest worker {dt:.2f} s (per worker: "
+                      f"{min(times):.2f}-{dt:.2f} s, {sum(times):.1f} s of CPU in all)",
             "cpu_model": cpu,
             "sparse_oracle_cw_s_1thread": round(B / dt_sparse, 1)}
 

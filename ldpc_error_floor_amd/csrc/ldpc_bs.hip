@@ -138,8 +138,8 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     else p.nw = std::max((vch + k.VPL - 1) / k.VPL, (cch + k.CPL - 1) / k.CPL);
     if (p.nw > 16) return p;                       // 1024-lane workgroup
     if (k.VPL > 1 || k.CPL > 1) {
-        // spread over 16 waves (one workgroup per CU); the chunks are dealt to the SIMDs
-        p.nw = 16;
+        // spread over NW waves (one workgroup per CU); the chunks are dealt to the SIMDs
+        p.nw = k.NW;
         if (vch > k.VPL * p.nw || cch > k.CPL * p.nw) return p;
     }
     p.arows = (g.w_alpha_uniform && !ucn) ? 1 : h.M;
@@ -166,7 +166,9 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     if (k.UCN && p.off_hdz > 65535) return p;
     o = (slot_end + 15) & ~(size_t)15;
     p.off_red = (uint32_t)o;
-    o += 64 + (size_t)4 * T;                       // + the per-iteration frame-error words
+    // + the per-iteration frame-error words, rounded to 16 B: the tables after them are read
+    // with ds_read_b128 (T = 50 unrounded put them 8 B off: C3 17.8 -> 24.4 ms, C5 61 -> 81 ms)
+    o += 64 + (((size_t)4 * T + 15) & ~(size_t)15);
     p.off_alut = (uint32_t)o;
     o += (size_t)2 * (k.UCN ? 2 : 1) * p.arows * LUT_W * 4;
     p.off_blut = (uint32_t)o;
@@ -183,6 +185,8 @@ BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float cli
     if (e && atoi(e) == 0) return p;
     const char* el = getenv("LDPC_BS_LPC");          // A/B: force 2 or 4 lanes per check
     const int want_lpc = el ? atoi(el) : 0;
+    const char* ei = getenv("LDPC_BS_INST");         // A/B: force one instance (if it fits)
+    const int want_inst = ei ? atoi(ei) : -1;
     if (!bs_mode(mode)) return p;
     if (per_edge_w || !g.host || !g.w_beta_nonneg) return p;
     const host::GraphTables& h = *g.host;
@@ -191,6 +195,8 @@ BsPlan bs_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float cli
     if (min_cdeg < 2) return p;                                   // ("no other edge" rule unneeded)
     for (int i = 0; i < kBsNInst; ++i) {
         if (want_lpc != 0 && want_lpc != kBsInst[i].LPC) continue;
+        if (want_inst >= 0 && want_inst != i) continue;
+        if (want_inst < 0 && kBsInst[i].NW != 16 && (kBsInst[i].VPL > 1 || kBsInst[i].CPL > 1)) continue;   // A/B only
         BsPlan q = plan_inst(g, i, ucn, clip, min_cdeg, mode, T);
         if (q.ok) return q;
     }
@@ -218,26 +224,64 @@ const char* bs_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_
     return buf;
 }
 
-// Deal `n` chunks (costs `cost`) to nw waves with at most `cap` chunks per wave, balancing the
-// four SIMDs (wave w runs on SIMD w mod 4): heaviest chunk first, to the least-loaded SIMD that
-// has a wave with room, on that SIMD's wave with the fewest chunks.  slot[w][c] = chunk or -1.
 namespace bs {
+// Deal `n` chunks (costs `cost`) to nw waves with at most `cap` chunks per wave (slot[w][c] =
+// chunk or -1; wave w runs on SIMD w mod 4).  The chunks of one phase end at a barrier, and a
+// SIMD's last busy wave runs alone, latency-bound (a dependent chain issues every ~8.5 cycles
+// against ~2.4-4.2 with several waves), so what bounds a phase is the SIMD's total AND its
+// heaviest wave.  Chunks go heaviest first to the lightest wave with room (LPT: 5G BG2's 20
+// variable chunks on 16 waves pair the four lightest, 4 + 4 units, where the SIMD-first dealing
+// gave one wave per SIMD 11 + 4 while the others held 4-7); the waves then go heaviest first
+// to the SIMD with the smallest total and a free wave slot.  A wave's chunks are in descending
+// cost (the first place takes the heaviest: bsc's heavy-degree place).  LDPC_BS_DEAL=0: the
+// previous dealing (heaviest chunk to the least-loaded SIMD, on its emptiest wave).
 std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap) {
     const int n = (int)cost.size();
-    std::vector<int> order(n), slot((size_t)nw * cap, -1), used(nw, 0), load(4, 0);
+    std::vector<int> order(n), slot((size_t)nw * cap, -1);
     for (int c = 0; c < n; ++c) order[c] = c;
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
-    for (int c : order) {
-        int best = -1, bw = -1;
-        for (int sm = 0; sm < 4; ++sm) {
-            int w_s = -1;
-            for (int w = sm; w < nw; w += 4)
-                if (used[w] < cap && (w_s < 0 || used[w] < used[w_s])) w_s = w;
-            if (w_s >= 0 && (best < 0 || load[sm] < load[best])) { best = sm; bw = w_s; }
+    const char* e = getenv("LDPC_BS_DEAL");
+    if (e && atoi(e) == 0) {
+        std::vector<int> used(nw, 0), load(4, 0);
+        for (int c : order) {
+            int best = -1, bw = -1;
+            for (int sm = 0; sm < 4; ++sm) {
+                int w_s = -1;
+                for (int w = sm; w < nw; w += 4)
+                    if (used[w] < cap && (w_s < 0 || used[w] < used[w_s])) w_s = w;
+                if (w_s >= 0 && (best < 0 || load[sm] < load[best])) { best = sm; bw = w_s; }
+            }
+            slot[(size_t)bw * cap + used[bw]] = c;
+            ++used[bw];
+            load[best] += cost[c];
         }
-        slot[(size_t)bw * cap + used[bw]] = c;
-        ++used[bw];
-        load[best] += cost[c];
+        return slot;
+    }
+    // virtual waves by LPT
+    std::vector<std::vector<int>> vch(nw);
+    std::vector<int> vload(nw, 0);
+    for (int c : order) {
+        int best = -1;
+        for (int w = 0; w < nw; ++w)
+            if ((int)vch[w].size() < cap &&
+                (best < 0 || vload[w] < vload[best] || (vload[w] == vload[best] && vch[w].size() < vch[best].size())))
+                best = w;
+        vch[best].push_back(c);
+        vload[best] += cost[c];
+    }
+    // virtual waves to physical ones: heaviest first to the SIMD with the smallest total
+    std::vector<int> vorder(nw), sload(4, 0), next(4);
+    for (int w = 0; w < nw; ++w) vorder[w] = w;
+    std::stable_sort(vorder.begin(), vorder.end(), [&](int x, int y) { return vload[x] > vload[y]; });
+    for (int sm = 0; sm < 4; ++sm) next[sm] = sm;
+    for (int v : vorder) {
+        int sm = -1;
+        for (int q = 0; q < 4; ++q)
+            if (next[q] < nw && (sm < 0 || sload[q] < sload[sm])) sm = q;
+        const int w = next[sm];
+        next[sm] += 4;
+        sload[sm] += vload[v];
+        for (size_t u = 0; u < vch[v].size(); ++u) slot[(size_t)w * cap + u] = vch[v][u];
     }
     return slot;
 }

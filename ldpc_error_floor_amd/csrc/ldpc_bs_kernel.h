@@ -48,8 +48,9 @@ constexpr size_t BS_LDS_MAX = 160 * 1024;
 
 // kernel instances: D = check-degree bound, DV = variable-degree bound, LPC = lanes per check,
 // VPL / CPL = variables / 64-lane check chunks per lane, UCN / BIG = unsatisfied-check weights /
-// shortened bits supported, PK = 16-bit packed slot addresses, WPE = waves per SIMD (registers)
-struct BsInst { int D, DV, LPC, VPL, CPL; bool UCN, BIG, PK; int WPE; };
+// shortened bits supported, PK = 16-bit packed slot addresses, WPE = waves per SIMD (registers),
+// NW = waves of the multi-chunk instances (VPL / CPL > 1)
+struct BsInst { int D, DV, LPC, VPL, CPL; bool UCN, BIG, PK; int WPE; int NW = 16; };
 constexpr BsInst kBsInst[] = {
     {15, 6, 4, 1, 1, false, false, true, 8},     // wman (C2), LPC 4 measured 6.31 ms vs 6.73
     {16, 8, 4, 1, 1, false, false, true, 8},
@@ -58,6 +59,9 @@ constexpr BsInst kBsInst[] = {
     {10, 8, 2, 2, 2, true, true, false, 4},      // 5G BG2 (C4): 1,280 variables, 640 checks;
                                                  // 18.2 ms vs 21.2 for LPC 4 (CPL 3), same box
     {10, 8, 4, 2, 3, true, true, false, 4},      // LDPC_BS_LPC=4 A/B
+    // 5G BG2 with 10 waves (20 variable and 20 check chunks, no idle place) at up to 168 VGPRs
+    // (no spills, 2-3 waves per SIMD): LDPC_BS_INST=6 A/B
+    {10, 8, 2, 2, 2, true, true, false, 3, 10},
 };
 constexpr int kBsNInst = sizeof(kBsInst) / sizeof(kBsInst[0]);
 
@@ -286,6 +290,21 @@ __device__ __forceinline__ void lut_bit(uint32_t (&o)[NI], const uint32_t (&in)[
         o[u] = mux(in[u][3], mux(in[u][2], g[u][3], g[u][2]), mux(in[u][2], g[u][1], g[u][0]));
 }
 
+// n consecutive words src[0..n) to LDS byte address lds (a table for the next iteration),
+// global -> LDS without registers (global_load_lds_dword: lane l of the wave whose first word is
+// w0 writes word w0 + l).  Nothing waits for the loads here: the next __syncthreads (vmcnt(0))
+// retires them, before any wave reads the table.
+__device__ __forceinline__ void copy_async(uint32_t lds, const uint32_t* src, int n, int wave, int NT) {
+    // (wave-uniform loop; the lane index from mbcnt, so no thread index is kept live for it)
+    for (int w0 = wave * 64; w0 < n; w0 += NT) {
+        const int w = w0 + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        if (w < n)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + w),
+                                             (__attribute__((address_space(3))) void*)(uintptr_t)(lds + 4u * (uint32_t)w0),
+                                             4, 0, 0);
+    }
+}
+
 // lane permutation inside each group of 4 lanes (DPP quad_perm, a VALU move)
 template <int CTRL>
 __device__ __forceinline__ uint32_t qperm(uint32_t x) {
@@ -370,14 +389,40 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
 #ifndef BS_VSKIP
 #define BS_VSKIP 1
 #endif
+// lanes with several variables issue all their LLR loads before converting any (A/B switch)
+#ifndef BS_LLR_ALL
+#define BS_LLR_ALL 0
+#endif
+// LLR loads through a buffer descriptor (A/B switch; 0: 64-bit pointer loads)
+#ifndef BS_BUFLD
+#define BS_BUFLD 1
+#endif
+// fold / check-lane / table-copy tests on the wave index instead of the thread index (A/B)
+#ifndef BS_TIDFREE
+#define BS_TIDFREE 1
+#endif
+// the next iteration's weight tables copied global -> LDS asynchronously (global_load_lds: the
+// wave does not wait for the load; the barrier after the check phase retires it) instead of
+// through registers, which stalled every wave for an L2 round trip at each iteration start
+// (A/B switch)
+#ifndef BS_GLDS
+#define BS_GLDS 1
+#endif
+// UCN: a wave's alpha' table evaluation skipped when all its checks are satisfied (A/B switch;
+// the multi-chunk instances only: C4 17.96 against 18.03 ms, C3 17.54 against 17.31 without)
+#ifndef BS_USKIP
+#define BS_USKIP 1
+#endif
 
 // Register budget: the small instances run at 64 VGPRs (WPE 8: three 9-wave workgroups per CU).
 // At a 72-register budget only two were resident (the waves of a workgroup are not spread evenly
 // over the SIMDs): measured 7.56 ms (72 VGPRs) -> 6.51 ms (64) per 2^20-codeword C2 decode.
 // XP: the hard-bit export build (a.hdx: every iteration's hard decisions, for the hard_bits /
 // synd_bits outputs); the counters-only build is the one the bench and the sweeps run.
-template <int D, int DV, int LPC, int VPL, int CPL, bool UCN, bool BIG, bool PK, int WPE, bool XP>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE)))
+// LB: the workgroup size bound (64 NW for the multi-chunk instances: the register budget is
+// 512 / (waves per SIMD), which a 1024-lane bound would fix at 128)
+template <int D, int DV, int LPC, int VPL, int CPL, bool UCN, bool BIG, bool PK, int WPE, bool XP, int LB>
+__global__ void __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_bs(BsArgs a) {
     static_assert(LPC == 2 || LPC == 4, "lanes per check");
     constexpr int SB = (DV * QMAX + QMAX <= 127) ? 8 : 9;     // planes of S and of lw + S
@@ -412,8 +457,12 @@ k_bs(BsArgs a) {
 #pragma unroll
     for (int u = 0; u < VPL; ++u) {
         const uint32_t* vt = a.vn_tab + ((size_t)u * NT + tid) * VNW;
+        // (the slot addresses: loaded after the LLR prologue when the lane holds several
+        // variables, where they would only add to the registers the LLR loads hold)
+        if (!(BS_LLR_ALL && VPL > 1)) {
 #pragma unroll
-        for (int p = 0; p < VNA; ++p) va[u][p] = vt[p];
+            for (int p = 0; p < VNA; ++p) va[u][p] = vt[p];
+        }
         vv[u] = (int)vt[VNA];                                // -1: no variable (UCN: v | HD index << 16)
         dw[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave)]);
         dwmin[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave) + 1]);
@@ -428,26 +477,48 @@ k_bs(BsArgs a) {
     __syncthreads();
     uint32_t cs[VPL], cm[VPL][4], bg[VPL];
     int off = 0;
+    // all 32 loads of a variable issued before any use: one HBM round trip per workgroup
+    // prologue (with batches of 8 the LLR fetch cost 0.75 ms of a 6.5 ms C2 decode, with this
+    // 0.44 ms: the workgroups stay in step, so every pack boundary is a chip-wide HBM burst; a
+    // persistent grid prefetching the next pack during the check phases needed 6 more
+    // loop-carried registers and spilled: 7.56 ms).
+    // the pack's LLR rows through a buffer descriptor (wave-uniform base and size): each load is
+    // buffer_load_dword with the lane's 4 v in voffset and the row's 4 r nv in soffset, so no
+    // load needs a 64-bit VGPR address (with them the multi-variable lanes spilled the loaded
+    // values and waited for each load in turn); rows past the batch read 0
+    const __amdgpu_buffer_rsrc_t llr_rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.llr + b0 * nv), 0, nvalid * nv * 4, 0x00020000);
+    auto llr_at = [&](int r, int v) __attribute__((always_inline)) -> float {
+        if (BS_BUFLD)
+            return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(llr_rs, 4 * v, 4 * r * nv, 0));
+        return a.llr[(b0 + min(r, nvalid - 1)) * nv + v];
+    };
+    auto var_of = [&](int u) __attribute__((always_inline)) -> int {
+        return (UCN && vv[u] >= 0) ? (vv[u] & 0xFFFF) : vv[u];
+    };
+    // lanes with several variables (VPL > 1, one workgroup per CU: nothing else hides the fetch)
+    // issue variable u + 1's loads while converting variable u's (BS_LLR_ALL), so the fetch is
+    // one round trip without holding every variable's 32 values at once
+    float xv[VPL][PACK];
+    if (var_of(0) >= 0 && !ABL(32)) {
+#pragma unroll
+        for (int r = 0; r < PACK; ++r) xv[0][r] = llr_at(r, var_of(0));
+    }
 #pragma unroll
     for (int u = 0; u < VPL; ++u) {
         cs[u] = 0u;
         bg[u] = 0u;
 #pragma unroll
         for (int p = 0; p < 4; ++p) cm[u][p] = 0u;
-        const int v = (UCN && vv[u] >= 0) ? (vv[u] & 0xFFFF) : vv[u];
+        const int v = var_of(u);
+        const int u1 = u + 1 < VPL ? u + 1 : u;
+        const int vn = (u + 1 < VPL && !ABL(32)) ? var_of(u1) : -1;
+        const bool inter = BS_LLR_ALL && v >= 0 && vn >= 0 && !ABL(32);   // next loads interleaved
         if (v >= 0 && !ABL(32)) {
-            const float* src = a.llr + b0 * nv + v;
-            // all 32 loads issued before any use: one HBM round trip per workgroup prologue (with
-            // batches of 8 the LLR fetch cost 0.75 ms of a 6.5 ms C2 decode, with this 0.44 ms:
-            // the workgroups stay in step, so every pack boundary is a chip-wide HBM burst; a
-            // persistent grid prefetching the next pack during the check phases needed 6 more
-            // loop-carried registers and spilled: 7.56 ms)
-            float xv[PACK];
-#pragma unroll
-            for (int r = 0; r < PACK; ++r) xv[r] = src[(int64_t)min(r, nvalid - 1) * nv];
 #pragma unroll
             for (int r = 0; r < PACK; ++r) {
-                const float x = xv[r] * a.inv;
+                if (inter) xv[u1][r] = llr_at(r, vn);
+                const float x = xv[u][r] * a.inv;
                 const float xr = rintf(x);
                 const bool big = BIG && fabsf(x) == a.cu;       // a shortened bit (a.cu > qmax)
                 off |= ((xr != x || fabsf(xr) > (float)a.qmax) && !big) ? 1 : 0;
@@ -458,6 +529,10 @@ k_bs(BsArgs a) {
 #pragma unroll
                 for (int p = 0; p < 4; ++p) cm[u][p] |= ((m >> p) & 1u) << r;
             }
+        }
+        if (vn >= 0 && !inter) {
+#pragma unroll
+            for (int r = 0; r < PACK; ++r) xv[u1][r] = llr_at(r, vn);
         }
     }
     if (off) atomicOr(&RED[7], 1u);
@@ -643,6 +718,14 @@ k_bs(BsArgs a) {
         }
     };
 
+    if (BS_LLR_ALL && VPL > 1) {
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) {
+            const uint32_t* vt = a.vn_tab + ((size_t)u * NT + tid) * VNW;
+#pragma unroll
+            for (int p = 0; p < VNA; ++p) va[u][p] = vt[p];
+        }
+    }
     vn_phase(true, false, a.off_blut, 0);
     // check groups: chunk k of 64 check lanes; lane LPC c + j of it (check c = row i, index h)
     // takes edges k = LPC m + j, at slots first_i + j A_i + m z + h (a.row_lay); edges past the
@@ -677,11 +760,13 @@ k_bs(BsArgs a) {
     __syncthreads();
 
     for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
-        if (tid == 0 && t > 0) {            // fold iteration t-1's frame flags
-            // (kept in LDS for the iter_wrong export after the loop: a global pointer held
-            // through the loop cost the 64-VGPR build 17 more SGPR spill moves in it)
-            RED[16 + t - 1] = RED[0];
-            RED[1] &= RED[0];
+        if ((BS_TIDFREE ? wave == 0 : tid == 0) && t > 0) {   // fold iteration t-1's frame flags
+            // (every lane of wave 0 writes the same words: a wave-uniform branch, no thread
+            // index kept live through the loop; kept in LDS for the iter_wrong export after the
+            // loop: a global pointer held through it cost the 64-VGPR build 17 SGPR spill moves)
+            const uint32_t w0 = RED[0];
+            RED[16 + t - 1] = w0;
+            RED[1] &= w0;
             RED[0] = 0u;
         }
         const int nx = (t + 1) & 1;
@@ -692,16 +777,29 @@ k_bs(BsArgs a) {
         if (t + 1 < a.T) {
             // (the lane index made opaque per iteration: the copy addresses are recomputed here
             // rather than hoisted out of the T loop into registers the loop body spills)
-            int tl = tid;
-            asm volatile("" : "+v"(tl));
-            for (int w = tl; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
-            if (a.bcols > 1)
-                for (int w = tl; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
+            if (BS_GLDS) {
+                int cw = wave;
+                if (!BS_TIDFREE) {                  // (the wave from an opaque thread index)
+                    int tl = tid;
+                    asm volatile("" : "+v"(tl));
+                    cw = __builtin_amdgcn_readfirstlane(tl >> 6);
+                }
+                copy_async(a.off_alut + 4u * (uint32_t)(nx * AL), a.alut + (size_t)(t + 1) * AL, AL, cw, NT);
+                if (a.bcols > 1)
+                    copy_async(a.off_blut + 4u * (uint32_t)(nx * BL), a.blut + (size_t)(t + 1) * BL, BL, cw, NT);
+            } else {
+                int tl = tid;
+                asm volatile("" : "+v"(tl));
+                for (int w = tl; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
+                if (a.bcols > 1)
+                    for (int w = tl; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
+            }
         }
         // ======== check nodes ===================================================================
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
-            const bool active = (CPL == 1) ? (tid < a.cn_lanes) : (gchunk[c] >= 0);
+            const bool active = (CPL == 1) ? (BS_TIDFREE ? wave * 64 < a.cn_lanes : tid < a.cn_lanes)
+                                           : (gchunk[c] >= 0);   // (cn_lanes: 64 k)
             if (!active || ABL(1)) continue;
             uint32_t cbase = gbase[c];
             asm volatile("" : "+v"(cbase));
@@ -798,12 +896,17 @@ k_bs(BsArgs a) {
                 const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
                 const uint32_t tab = gtab[c] + (uint32_t)((t & 1) * AL * 4);
                 uint32_t qb[OB][2];
+                // alpha' is needed only where a check is unsatisfied for some codeword: a wave
+                // whose checks are all satisfied in all 32 codewords (most waves once the
+                // frames have converged) skips its table (the same messages, exactly)
+                bool any_unsat = false;
+                if constexpr (UCN) any_unsat = ucn && (!(BS_USKIP && CPL > 1) || __builtin_amdgcn_ballot_w64(syn != 0u) != 0ull);
 #pragma unroll
                 for (int b = 0; b < OB; ++b) {
                     uint32_t o[2];
                     lut_bit<2>(o, mm, tab + (uint32_t)(b * 64));
                     if constexpr (UCN) {
-                        if (ucn) {                    // alpha' where the check is unsatisfied
+                        if (any_unsat) {              // alpha' where the check is unsatisfied
                             uint32_t ou[2];
                             lut_bit<2>(ou, mm, tab + tabu + (uint32_t)(b * 64));
                             o[0] = mux(syn, ou[0], o[0]);
@@ -880,7 +983,8 @@ k_bs(BsArgs a) {
 template <int I, bool XP>
 int launch_bs_x(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     constexpr BsInst k = kBsInst[I];
-    auto* fn = &k_bs<k.D, k.DV, k.LPC, k.VPL, k.CPL, k.UCN, k.BIG, k.PK, k.WPE, XP>;
+    constexpr int LB = (k.VPL > 1 || k.CPL > 1) ? 64 * k.NW : 1024;
+    auto* fn = &k_bs<k.D, k.DV, k.LPC, k.VPL, k.CPL, k.UCN, k.BIG, k.PK, k.WPE, XP, LB>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),

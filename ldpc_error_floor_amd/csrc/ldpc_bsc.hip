@@ -29,10 +29,13 @@ namespace bs {
 // other variables, LPC lanes per check, VPL variables and CPL check chunks per lane
 // (a wman-sized instance — one variable and one check chunk per lane, 64 VGPRs — was measured
 // against bsl on C2: 61 spills, and the BG1 instance there ran 68 M cw/s against bsl's 176 M)
-struct BscInst { int D, DVH, DVL, LPC, VPL, CPL; int WPE; };
+struct BscInst { int D, DVH, DVL, LPC, VPL, CPL; int WPE; int NW = 16; };
 constexpr BscInst kBscInst[] = {
     {20, 10, 5, 4, 3, 3, 4},          // 5G BG1 (C5): degree 19 rows, degree 10 / 8 columns, 16 waves
     {20, 10, 5, 2, 3, 2, 4},          // the same with 2 lanes per check (LDPC_BS_LPC A/B)
+    // 12 waves: 36 variable chunks on 36 places, 45 check chunks on 48, up to 168 VGPRs (the
+    // 16-wave build spills 25 VGPRs at 128): LDPC_BSC_INST=2 A/B
+    {20, 10, 5, 4, 3, 4, 3, 12},
 };
 
 struct BscArgs {
@@ -77,8 +80,8 @@ __device__ __forceinline__ void lds_dput(uint32_t addr, uint32_t x, uint32_t y) 
     *reinterpret_cast<LdsD*>(addr) = v;
 }
 
-template <int D, int DVH, int DVL, int LPC, int VPL, int CPL, int WPE, bool XP>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE)))
+template <int D, int DVH, int DVL, int LPC, int VPL, int CPL, int WPE, bool XP, int LB>
+__global__ void __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_bsc(BscArgs a) {
     constexpr int SB = (DVH * QMAX + QMAX <= 127) ? 8 : 9;
     constexpr int EPL = (D + LPC - 1) / LPC;
@@ -132,10 +135,14 @@ k_bsc(BscArgs a) {
         for (int p = 0; p < 4; ++p) cm[u][p] = 0u;
         const int v = vv[u] < 0 ? -1 : (vv[u] & 0xFFFF);
         if (v >= 0) {
-            const float* src = a.llr + b0 * nv + v;
+            // (buffer loads: a wave-uniform descriptor over the pack's rows, the lane's 4 v in
+            // voffset, the row's 4 r nv in soffset: no 64-bit VGPR address per load, as bsl)
+            const __amdgpu_buffer_rsrc_t llr_rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(a.llr + b0 * nv), 0, nvalid * nv * 4, 0x00020000);
             float xv[PACK];
 #pragma unroll
-            for (int r = 0; r < PACK; ++r) xv[r] = src[(int64_t)min(r, nvalid - 1) * nv];
+            for (int r = 0; r < PACK; ++r)
+                xv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(llr_rs, 4 * v, 4 * r * nv, 0));
 #pragma unroll
             for (int r = 0; r < PACK; ++r) {
                 const float x = xv[r] * a.inv;
@@ -309,9 +316,10 @@ k_bsc(BscArgs a) {
     __syncthreads();
 
     for (int t = 0; t < a.T; ++t) {
-        if (tid == 0 && t > 0) {
-            RED[16 + t - 1] = RED[0];                 // (exported after the loop)
-            RED[1] &= RED[0];
+        if (wave == 0 && t > 0) {               // (all lanes of wave 0, the same words: bsl)
+            const uint32_t w0 = RED[0];
+            RED[16 + t - 1] = w0;                     // (exported after the loop)
+            RED[1] &= w0;
             RED[0] = 0u;
         }
         const int nx = (t + 1) & 1;
@@ -321,11 +329,17 @@ k_bsc(BscArgs a) {
         if (t + 1 < a.T) {
             // (the lane index made opaque per iteration: the copy addresses are recomputed here
             // rather than hoisted out of the T loop into registers the loop body spills)
-            int tl = tid;
-            asm volatile("" : "+v"(tl));
-            for (int w = tl; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
-            if (a.bcols > 1)
-                for (int w = tl; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
+            if (BS_GLDS) {            // (async global -> LDS, retired by the next barrier: bsl)
+                copy_async(a.off_alut + 4u * (uint32_t)(nx * AL), a.alut + (size_t)(t + 1) * AL, AL, wave, NT);
+                if (a.bcols > 1)
+                    copy_async(a.off_blut + 4u * (uint32_t)(nx * BL), a.blut + (size_t)(t + 1) * BL, BL, wave, NT);
+            } else {
+                int tl = tid;
+                asm volatile("" : "+v"(tl));
+                for (int w = tl; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
+                if (a.bcols > 1)
+                    for (int w = tl; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
+            }
         }
         // ======== check nodes ===================================================================
 #pragma unroll
@@ -529,12 +543,17 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
     const int nv = g.n_vars, nc = g.n_checks, z = h.z;
     const char* el = getenv("LDPC_BS_LPC");          // A/B: force 2 or 4 lanes per check
     const int want_lpc = el ? atoi(el) : 0;
+    const char* ei = getenv("LDPC_BSC_INST");        // A/B: force one instance (if it fits)
+    const int want_inst = ei ? atoi(ei) : -1;
     for (int i = 0; i < kBscNInst; ++i) {
         const BscInst& k = kBscInst[i];
         if (h.max_cdeg > k.D || h.max_vdeg > k.DVH) continue;
         if (want_lpc != 0 && want_lpc != k.LPC) continue;
+        if (want_inst >= 0 && want_inst != i) continue;
+        if (want_inst < 0 && k.NW != BSC_NW) continue;          // A/B-only instances
         BscPlan q;
         q.inst = i;
+        q.nw = k.NW;
         q.cn_lanes = 64 * ((k.LPC * nc + 63) / 64);
         const int vch = (nv + 63) / 64, cch = q.cn_lanes / 64;
         if (k.VPL == 1 && k.CPL == 1) q.nw = std::max(vch, cch);
@@ -576,7 +595,7 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
         o += (size_t)nv * 24;
         o = (o + 15) & ~(size_t)15;
         q.off_red = (uint32_t)o;
-        o += 64 + (size_t)4 * T;                 // + the per-iteration frame-error words
+        o += 64 + (((size_t)4 * T + 15) & ~(size_t)15);   // + the frame-error words (16 B aligned)
         q.off_alut = (uint32_t)o;
         o += (size_t)2 * q.arows * LUT_W * 4;
         q.off_blut = (uint32_t)o;
@@ -697,7 +716,7 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
 template <int I, bool XP>
 static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     constexpr BscInst k = kBscInst[I];
-    auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE, XP>;
+    auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE, XP, 64 * k.NW>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -777,6 +796,7 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
     switch (p.inst) {
         case 1: return hdx ? bsc_launch<1, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<1, false>(a, nblocks, p.nw, p.lds, s);
+        case 2: return hdx ? bsc_launch<2, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<2, false>(a, nblocks, p.nw, p.lds, s);
         default: return hdx ? bsc_launch<0, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<0, false>(a, nblocks, p.nw, p.lds, s);
     }
 }

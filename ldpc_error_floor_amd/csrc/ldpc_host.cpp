@@ -2,6 +2,7 @@
 // (see ldpc_host.h).  No HIP: built into libldpc_nms.so by hipcc and, for the sanitized check,
 // by g++ -fsanitize=address,undefined.
 #include "ldpc_host.h"
+#include "ldpc_beta_tabs.h"
 
 #include <algorithm>
 #include <climits>
@@ -67,6 +68,23 @@ int build_graph(const int32_t* proto, int32_t M, int32_t N, int32_t z, GraphTabl
     return LDPC_OK;
 }
 
+int beta_table_id(float b) {
+    if (!(b >= 0.f)) return -1;
+    uint8_t t[16];
+    for (int m = 0; m < 16; ++m)
+        t[m] = (uint8_t)std::min(15.f, std::fabs(std::nearbyint((float)m * b)));   // fp32 product, half to even
+    int lo = 0, hi = kNBetaTab;             // (the set is in ascending order of the table sums)
+    int sum = 0;
+    for (int m = 0; m < 16; ++m) sum += t[m];
+    for (int k = lo; k < hi; ++k) {
+        int s = 0;
+        for (int m = 0; m < 16; ++m) s += kBetaTab[k][m];
+        if (s != sum) continue;
+        if (std::equal(t, t + 16, kBetaTab[k])) return k;
+    }
+    return -1;
+}
+
 int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const float* alpha_ucn,
                     const float* beta, WeightInfo& w) {
     w = WeightInfo{};
@@ -109,6 +127,8 @@ int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const f
         }
         if (id) w.beta_id_mask |= (uint64_t)1 << t;
     }
+    w.beta_tid.resize((size_t)T * g.N);
+    for (size_t x = 0; x < (size_t)T * g.N; ++x) w.beta_tid[x] = beta_table_id(beta[x]);
     for (int t = 0; t < T; ++t) {
         const float a0 = alpha[(size_t)t * g.E], b0 = beta[(size_t)t * g.N];
         for (int e = 1; e < g.E && w.alpha_uniform; ++e)

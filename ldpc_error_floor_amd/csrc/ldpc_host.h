@@ -76,7 +76,13 @@ struct WeightInfo {
     // min(15, |rint(fl32(m beta))|) == m for m = 0..15 (the bit-sliced kernels skip it)
     uint64_t beta_id_mask = 0;
     std::vector<int32_t> row_merge;
+    // [T][N]: index into kBetaTab (ldpc_beta_tabs.h) of column j's q5 / q-5 channel table at
+    // iteration t, min(15, |rint(fl32(m beta))|) for m = 0..15; -1 when beta < 0 or the table is
+    // not in the set (the bit-sliced kernel then evaluates it from its table words)
+    std::vector<int32_t> beta_tid;
 };
+// kBetaTab index of beta's q5 / q-5 channel table, or -1
+int beta_table_id(float beta);
 int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const float* alpha_ucn,
                     const float* beta, WeightInfo& out);
 
