@@ -418,7 +418,7 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
     const int EPL = (k.D + LPC - 1) / LPC, HDW = (EPL + 1) / 2;
     const int nl = 64 * p.nw;
     std::vector<uint32_t> vn((size_t)k.VPL * nl * VNW, 0u);
-    std::vector<int32_t> wdeg((size_t)2 * k.VPL * p.nw, 0);
+    std::vector<int32_t> wdeg((size_t)3 * k.VPL * p.nw, 0);   // {most, fewest edges, column or -1}
     auto put = [&](uint32_t* w, int f, uint32_t addr) {
         if (k.PK) w[f >> 1] |= addr << (16 * (f & 1));
         else w[f] = addr;
@@ -465,16 +465,19 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
             const int ch = vslot[(size_t)w * k.VPL + u];
             int dmax = 0, dmin = 1 << 30;
             if (ch < 0) {                 // no chunk at this place: the kernel skips it (dw < 0)
-                wdeg[2 * ((size_t)u * p.nw + w)] = -1;
-                wdeg[2 * ((size_t)u * p.nw + w) + 1] = 0;
+                wdeg[3 * ((size_t)u * p.nw + w)] = -1;
+                wdeg[3 * ((size_t)u * p.nw + w) + 1] = 0;
+                wdeg[3 * ((size_t)u * p.nw + w) + 2] = -1;
                 continue;
             }
+            int col = -2;                 // the chunk's column (-1: several)
             std::fill(A.begin(), A.end(), p.off_zero);
             std::fill(dl.begin(), dl.end(), 0);
             for (int l = 0; l < 64; ++l) {
                 const int o = 64 * ch + l;
                 if (o >= nv) { dmin = 0; continue; }
                 const int v = order[o], j = v / z, hh = v - j * z;
+                col = (col == -2 || col == j) ? j : -1;
                 const int c0 = h.col_ptr[j], dv = h.col_ptr[j + 1] - c0;
                 for (int f = 0; f < dv; ++f) {
                     const int pe = h.col_pe[c0 + f], i = h.pe_row[pe];
@@ -499,8 +502,9 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
                 for (int f = 0; f < DV; ++f) put(q, f, A[(size_t)l * DV + f]);
                 q[VNA] = k.UCN ? ((uint32_t)order[o] | (hd_index(order[o]) << 16)) : (uint32_t)order[o];
             }
-            wdeg[2 * ((size_t)u * p.nw + w)] = dmax;
-            wdeg[2 * ((size_t)u * p.nw + w) + 1] = dmin;
+            wdeg[3 * ((size_t)u * p.nw + w)] = dmax;
+            wdeg[3 * ((size_t)u * p.nw + w) + 1] = dmin;
+            wdeg[3 * ((size_t)u * p.nw + w) + 2] = col < 0 ? -1 : col;
         }
     if (getenv("LDPC_BS_VORDER_LOG"))
         fprintf(stderr, "bsl variable-phase bank cycles per slot word: %d -> %d\n", vcost_before, vcost_after);
@@ -598,13 +602,16 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.vn_tab = gt;
     const size_t nvt = (size_t)k.VPL * 64 * p.nw * VNW;
     a.vn_wdeg = reinterpret_cast<const int32_t*>(gt + nvt);
-    a.row_lay = a.vn_wdeg + 2 * (size_t)k.VPL * p.nw;
+    a.row_lay = a.vn_wdeg + 3 * (size_t)k.VPL * p.nw;
     a.cn_chunk = a.row_lay + 2 * (size_t)g.M;
     a.cn_hd = reinterpret_cast<const uint32_t*>(a.cn_chunk + (size_t)p.nw * k.CPL);
     a.alut = alut;
     a.blut = blut;
     a.arows = p.arows;
     a.bcols = p.bcols;
+    // the fixed-set channel tables cover the grids whose magnitudes saturate at 15 (q = 5, -5)
+    a.btid = (bs_qmax(mode) == QMAX && !getenv("LDPC_BS_NOBFIX")) ? g.beta_tid : nullptr;
+    a.btid_n = g.N;
     a.counters = counters;
     a.flags = flags;
     a.bad = bad;

@@ -32,6 +32,7 @@
 #pragma once
 #include <cstdint>
 
+#include "ldpc_beta_tabs.h"
 #include "ldpc_fused.h"
 #include "ldpc_fused5_kernel.h"
 
@@ -78,12 +79,15 @@ struct BsArgs {
     const int32_t* row_lay;      // [M][2] slot layout of each proto row: first slot, j-block stride
     int z;
     const uint32_t* vn_tab;      // [VPL][64 nw][VNW]: slot byte addresses (2 per word if PK), variable (-1 idle)
-    const int32_t* vn_wdeg;      // [VPL][nw][2] most and fewest edges of a variable of each wave
+    const int32_t* vn_wdeg;      // [VPL][nw][3] most and fewest edges of a variable of each wave,
+                                 // the chunk's column when it has one (else -1)
     const int32_t* cn_chunk;     // [nw][CPL] 64-lane check chunk of each wave's group (-1 idle)
     const uint32_t* cn_hd;       // [chunks * 64][HDW] UCN: LDS byte addresses of the edges' hard decisions
     const uint32_t* alut;        // [T][AR][LUT_W]: Q(relu(alpha m step)) for m = 0..15 (AR = arows, x2 with UCN)
     const uint32_t* blut;        // [T][bcols][BLUT_W]: |Q(beta m)| for m = 0..15 (grid units), |Q(beta cu)|
     int arows, bcols;
+    const int32_t* btid;         // [T][btid_n] kBetaTab index of each column's channel table
+    int btid_n;                  // (-1: evaluate from the table words), or null
     int64_t* counters;
     uint8_t* flags;
     uint32_t* bad;               // [packs] 1: decoded by the v5 fixup instead
@@ -305,6 +309,39 @@ __device__ __forceinline__ void copy_async(uint32_t lds, const uint32_t* src, in
     }
 }
 
+// The channel-weight table |Q(beta_t ch)| (Main_Functions.py:164-177) when beta_t's table is
+// table k of the fixed set (ldpc_beta_tabs.h): each output bit j is mux(m3, f_hi(m2, m1, m0),
+// f_lo(m2, m1, m0)) with compile-time truth tables, at most three v_bitop3 with immediates —
+// against 16 leaves with SGPR operands (4.2-cycle forms) and 7 muxes per bit for a table held in
+// SGPRs.  k is wave-uniform: the wave jumps to entry k of a table of 128-byte entries
+// (s_getpc + s_setpc) and back.  (A C++ switch over the 210 tables, a binary tree of scalar
+// branches with 210 leaves, made the register allocator spill 291 VGPRs.)  The caller keeps k
+// in [0, kNBetaTab).  s40-s42 are the jump's scratch.
+__device__ __forceinline__ void beta_asm(uint32_t (&o)[4], const uint32_t (&m)[4], int k) {
+    uint32_t t0, t1;
+    asm volatile(
+        "s_getpc_b64 s[40:41]\n"
+        ".Lbpc%=:\n\t"
+        "s_lshl_b32 s42, %[k], 7\n\t"
+        "s_add_u32 s40, s40, s42\n\t"
+        "s_addc_u32 s41, s41, 0\n\t"
+        "s_add_u32 s40, s40, .Lbtab%=-.Lbpc%=\n\t"
+        "s_addc_u32 s41, s41, 0\n\t"
+        "s_setpc_b64 s[40:41]\n"
+        "\t.p2align 7\n"
+        ".Lbtab%=:\n"
+        LDPC_BETA_ASM_TABLE
+        "\t.p2align 7\n"
+        ".Lbend%=:"
+        : [o0] "=&v"(o[0]), [o1] "=&v"(o[1]), [o2] "=&v"(o[2]), [o3] "=&v"(o[3]),
+          [t0] "=&v"(t0), [t1] "=&v"(t1)
+        : [m0] "v"(m[0]), [m1] "v"(m[1]), [m2] "v"(m[2]), [m3] "v"(m[3]), [k] "s"(k)
+        : "s40", "s41", "s42", "scc");
+}
+#ifndef BS_BFIX
+#define BS_BFIX 1       // the fixed-table channel weighting (A/B switch)
+#endif
+
 // lane permutation inside each group of 4 lanes (DPP quad_perm, a VALU move)
 template <int CTRL>
 __device__ __forceinline__ uint32_t qperm(uint32_t x) {
@@ -452,7 +489,7 @@ k_bs(BsArgs a) {
 
     // ---- per-lane variables: slot addresses, variable index, degree bounds of the wave ----------
     uint32_t va[VPL][VNA];
-    int vv[VPL], dw[VPL], dwmin[VPL];
+    int vv[VPL], dw[VPL], dwmin[VPL], pcol[VPL];
     uint32_t tab_b[VPL];
 #pragma unroll
     for (int u = 0; u < VPL; ++u) {
@@ -464,8 +501,9 @@ k_bs(BsArgs a) {
             for (int p = 0; p < VNA; ++p) va[u][p] = vt[p];
         }
         vv[u] = (int)vt[VNA];                                // -1: no variable (UCN: v | HD index << 16)
-        dw[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave)]);
-        dwmin[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave) + 1]);
+        dw[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[3 * (u * nwv + wave)]);
+        dwmin[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[3 * (u * nwv + wave) + 1]);
+        pcol[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[3 * (u * nwv + wave) + 2]);
         tab_b[u] = (a.bcols > 1 && vv[u] >= 0) ? (uint32_t)(((UCN ? (vv[u] & 0xFFFF) : vv[u]) / (nv / a.bcols)) * BLUT_W * 4) : 0u;
     }
     int cn_dmin = a.cn_dmin;
@@ -577,11 +615,34 @@ k_bs(BsArgs a) {
             const uint32_t hda = UCN ? 4u * ((uint32_t)vv[u] >> 16) : 0u;     // HD slot (rotated)
             const bool counted = v >= 0 && v < a.target_bits;
             uint32_t lw[1][4];                   // |Q(beta_{t+1} ch)| (before the C->V: fewer live registers)
+            // the table's index in the fixed set (wave-uniform; -1: evaluate the table words)
+            int bk = -1;
+            if constexpr (!XP && BS_BFIX) {
+                if (!first && !last && a.btid) {
+                    const int col = (a.bcols == 1) ? 0 : pcol[u];
+                    if (col >= 0) bk = __builtin_amdgcn_readfirstlane(a.btid[(size_t)tb * a.btid_n + col]);
+                }
+            }
             if (!last) {
                 // identity table: |Q(beta ch)| = |ch| (the mask covers iterations 0..63)
                 if (ABL(2) || (tb < 64 && ((a.beta_id >> tb) & 1))) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) lw[0][i] = cm[u][i];
+                } else if (bk >= 0 && bk < kNBetaTab) {   // a table of the fixed set
+                    beta_asm(lw[0], cm[u], bk);
+                    if constexpr (BIG) {            // shortened bits: |Q(beta cu)| from the table words
+                        if (a.bcols == 1) {
+                            const ConstW* tg = (const ConstW*)(a.blut) + (size_t)tb * BLUT_W;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) lw[0][i] = mux(bg[u], tg[LUT_W + i], lw[0][i]);
+                        } else {
+                            const v4u gb = lds_q(bslice + tab_b[u] + LUT_W * 4);
+                            lw[0][0] = mux(bg[u], gb.x, lw[0][0]);
+                            lw[0][1] = mux(bg[u], gb.y, lw[0][1]);
+                            lw[0][2] = mux(bg[u], gb.z, lw[0][2]);
+                            lw[0][3] = mux(bg[u], gb.w, lw[0][3]);
+                        }
+                    }
                 } else if (a.bcols == 1) {          // one beta per iteration: table in SGPRs
                     const ConstW* tg = (const ConstW*)(a.blut) + (size_t)tb * BLUT_W;
                     lut_s(lw[0], cm[u], tg);

@@ -23,6 +23,7 @@ struct ldpc_graph {
     float* d_alpha = nullptr;
     float* d_alpha_ucn = nullptr;
     float* d_beta = nullptr;
+    int32_t* d_beta_tid = nullptr;   // [T][N] host::WeightInfo::beta_tid
 };
 
 struct ldpc_ctx {
@@ -288,6 +289,7 @@ int ldpc_graph_destroy(ldpc_graph* g) {
     dev_free(g->d_alpha);
     dev_free(g->d_alpha_ucn);
     dev_free(g->d_beta);
+    dev_free(g->d_beta_tid);
     dev_free(g->d_row_merge);
     delete g;
     return LDPC_OK;
@@ -311,18 +313,23 @@ int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* 
     dev_free(g->d_alpha);
     dev_free(g->d_alpha_ucn);
     dev_free(g->d_beta);
+    dev_free(g->d_beta_tid);
+    g->dev.beta_tid = nullptr;
     g->T_w = 0;
     const size_t ne = (size_t)T * g->h.E, nn = (size_t)T * g->h.N;
     int st = dev_alloc(&g->d_alpha, ne);
     if (st == LDPC_OK && alpha_ucn) st = dev_alloc(&g->d_alpha_ucn, ne);
     if (st == LDPC_OK) st = dev_alloc(&g->d_beta, nn);
+    if (st == LDPC_OK) st = dev_alloc(&g->d_beta_tid, nn);
     if (st != LDPC_OK) return st;
     bool ok = hipMemcpy(g->d_alpha, alpha, ne * sizeof(float), hipMemcpyHostToDevice) == hipSuccess;
     if (alpha_ucn)
         ok = ok && hipMemcpy(g->d_alpha_ucn, alpha_ucn, ne * sizeof(float),
                              hipMemcpyHostToDevice) == hipSuccess;
     ok = ok && hipMemcpy(g->d_beta, beta, nn * sizeof(float), hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMemcpy(g->d_beta_tid, wi.beta_tid.data(), nn * sizeof(int32_t), hipMemcpyHostToDevice) == hipSuccess;
     if (!ok) return LDPC_ERR_HIP;
+    g->dev.beta_tid = g->d_beta_tid;
     g->T_w = T;
     g->per_edge_w = wi.per_edge_w;
     g->row_merge = wi.row_merge;
