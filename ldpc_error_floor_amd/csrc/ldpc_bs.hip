@@ -25,7 +25,7 @@ namespace bs {
 __global__ void k_bs_tables(const float* __restrict__ alpha, const float* __restrict__ alpha_ucn,
                             const float* __restrict__ beta, const int32_t* __restrict__ row_ptr,
                             int T, int E, int N, int arows, int ar, int bcols, float step, float inv,
-                            int qmax, float cu, uint32_t* alut, uint32_t* blut) {
+                            int qmax, float cu, uint32_t* alut, uint32_t* blut, int32_t* atid) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;    // one table per thread
     const int na = T * ar, nbt = T * bcols;
     if (f >= na + nbt) return;
@@ -38,6 +38,22 @@ __global__ void k_bs_tables(const float* __restrict__ alpha, const float* __rest
         const float w = al[(size_t)t * E + row_ptr[row]];
         for (int m = 0; m < 16; ++m) g[m] = f5::q_mag5(min(m, qmax), w, step, inv, qmax);
         out = alut + (size_t)f * LUT_W;
+        // the table's index in the fixed set (ldpc_beta_tabs.h), -1 if it is not one of them:
+        // the kernels evaluate a table of the set with immediate truth tables (table_asm2)
+        int id = -1;
+        if (qmax == QMAX) {
+            int sum = 0;
+            for (int m = 0; m < 16; ++m) sum += g[m];
+            for (int k = 0; k < kNBetaTab && id < 0; ++k) {
+                bool eq = true;
+                int sk = 0;
+                for (int m = 0; m < 16; ++m) sk += kBetaTab[k][m];
+                if (sk != sum) continue;
+                for (int m = 0; m < 16; ++m) eq = eq && kBetaTab[k][m] == g[m];
+                if (eq) id = k;
+            }
+        }
+        atid[f] = id;
     } else {
         const int f2 = f - na;
         const int t = f2 / bcols, col = f2 - t * bcols;
@@ -378,9 +394,10 @@ std::vector<int> column_rotation(const host::GraphTables& h, int LPC, int EPL, i
 
 // the per-decode weight tables of both bit-sliced kernels (k_bs_tables)
 int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, int qmax,
-                   float cu, bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s) {
+                   float cu, bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s,
+                   const int32_t** atid) {
     const size_t na = (size_t)b.T * ar * LUT_W, nb = (size_t)b.T * bcols * BLUT_W;
-    const size_t bytes = (na + nb) * 4;
+    const size_t bytes = (na + nb + (size_t)b.T * ar) * 4;     // + the alpha table ids
     if (bytes > ws.bs_lut_bytes) {
         if (ws.bs_lut) (void)hipFree(ws.bs_lut);
         ws.bs_lut = nullptr;
@@ -391,6 +408,7 @@ int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcol
     }
     *alut = reinterpret_cast<uint32_t*>(ws.bs_lut);
     *blut = *alut + na;
+    if (atid) *atid = reinterpret_cast<int32_t*>(*blut + nb);
     // (skipped when these tables are already in place: same weights, T and layout)
     const uint64_t kb[4] = {g.w_version, (uint64_t)b.T << 32 | (uint32_t)(arows << 16 | ar),
                             (uint64_t)__builtin_bit_cast(uint32_t, step) << 32 | __builtin_bit_cast(uint32_t, cu),
@@ -402,7 +420,7 @@ int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcol
     const float* au = (ucn && b.alpha_ucn) ? b.alpha_ucn : b.alpha;
     hipLaunchKernelGGL(k_bs_tables, dim3((unsigned)((ntab + 127) / 128)), dim3(128), 0, s, b.alpha, au,
                        b.beta, g.row_ptr, b.T, g.E, g.N, arows, ar, bcols, step, 1.0f / step, qmax,
-                       cu, *alut, *blut);
+                       cu, *alut, *blut, reinterpret_cast<int32_t*>(*blut + nb));
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 }  // namespace bs
@@ -578,7 +596,8 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     const float step = mode_step_bs(mode);
     const int ar = (k.UCN ? 2 : 1) * p.arows;
     uint32_t *alut = nullptr, *blut = nullptr;
-    st = bs_make_tables(b, g, p.arows, ar, p.bcols, step, bs_qmax(mode), p.cu, ucn, ws, &alut, &blut, s);
+    const int32_t* atid = nullptr;
+    st = bs_make_tables(b, g, p.arows, ar, p.bcols, step, bs_qmax(mode), p.cu, ucn, ws, &alut, &blut, s, &atid);
     if (st != LDPC_OK) return st;
     const int DV = k.DV;
     const int VNW = (k.PK ? (DV + 1) / 2 : DV) + 1;
@@ -612,6 +631,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     // the fixed-set channel tables cover the grids whose magnitudes saturate at 15 (q = 5, -5)
     a.btid = (bs_qmax(mode) == QMAX && !getenv("LDPC_BS_NOBFIX")) ? g.beta_tid : nullptr;
     a.btid_n = g.N;
+    a.atid = getenv("LDPC_BS_NOAFIX") ? nullptr : atid;
     a.counters = counters;
     a.flags = flags;
     a.bad = bad;

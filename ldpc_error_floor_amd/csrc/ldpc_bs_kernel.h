@@ -86,6 +86,8 @@ struct BsArgs {
     const uint32_t* alut;        // [T][AR][LUT_W]: Q(relu(alpha m step)) for m = 0..15 (AR = arows, x2 with UCN)
     const uint32_t* blut;        // [T][bcols][BLUT_W]: |Q(beta m)| for m = 0..15 (grid units), |Q(beta cu)|
     int arows, bcols;
+    const int32_t* atid;         // [T][AR] kBetaTab index of each row's check table (-1: not in
+                                 // the set; AR = arows, x2 with UCN), or null
     const int32_t* btid;         // [T][btid_n] kBetaTab index of each column's channel table
     int btid_n;                  // (-1: evaluate from the table words), or null
     int64_t* counters;
@@ -309,37 +311,93 @@ __device__ __forceinline__ void copy_async(uint32_t lds, const uint32_t* src, in
     }
 }
 
+// Fixed-set weight tables (ldpc_beta_tabs.h) by a computed call: the wave-uniform table index k
+// selects an entry of a jump table (s_getpc + offset, s_swappc); the entry computes the output
+// planes with immediate truth tables (v_bitop3) and returns (s_setpc to s[44:45]).  With
+// BS_TAB_OOL the table of each call site is assembled into a section of its own, out of the
+// kernel's instruction stream, so the loop body stays contiguous; else it follows the call and
+// the call skips it.  s40-s45 are the call's scratch.  The caller keeps k in [0, kNBetaTab).
+// (A/B, same box, r3i: out of line C2 5.31 against 5.26 ms in line, C4 14.66 both, C3 17.00
+// against 17.07 — the instruction stream is not the bottleneck; in line is the default)
+#ifndef BS_TAB_OOL
+#define BS_TAB_OOL 0
+#endif
+#if BS_TAB_OOL
+#define LDPC_TAB_CALL(SH, AL, TABLE)                                                              \
+    "s_getpc_b64 s[40:41]\n\t"                                                                   \
+    "s_add_u32 s40, s40, .Lbtab%=@rel32@lo+4\n\t"                                                \
+    "s_addc_u32 s41, s41, .Lbtab%=@rel32@hi+12\n\t"                                              \
+    "s_lshl_b32 s42, %[k], " SH "\n\t"                                                           \
+    "s_add_u32 s40, s40, s42\n\t"                                                                \
+    "s_addc_u32 s41, s41, 0\n\t"                                                                 \
+    "s_swappc_b64 s[44:45], s[40:41]\n"                                                          \
+    "\t.pushsection .text.ldpc_tables,\"ax\",@progbits\n"                                         \
+    "\t.p2align " AL "\n"                                                                        \
+    ".Lbtab%=:\n" TABLE "\t.popsection\n"
+#else
+#define LDPC_TAB_CALL(SH, AL, TABLE)                                                              \
+    "s_getpc_b64 s[40:41]\n"                                                                      \
+    ".Lbpc%=:\n\t"                                                                                \
+    "s_lshl_b32 s42, %[k], " SH "\n\t"                                                           \
+    "s_add_u32 s40, s40, s42\n\t"                                                                \
+    "s_addc_u32 s41, s41, 0\n\t"                                                                 \
+    "s_add_u32 s40, s40, .Lbtab%=-.Lbpc%=\n\t"                                                    \
+    "s_addc_u32 s41, s41, 0\n\t"                                                                 \
+    "s_swappc_b64 s[44:45], s[40:41]\n\t"                                                        \
+    "s_branch .Lbend%=\n"                                                                        \
+    "\t.p2align " AL "\n"                                                                        \
+    ".Lbtab%=:\n" TABLE ".Lbend%=:\n"
+#endif
+
 // The channel-weight table |Q(beta_t ch)| (Main_Functions.py:164-177) when beta_t's table is
-// table k of the fixed set (ldpc_beta_tabs.h): each output bit j is mux(m3, f_hi(m2, m1, m0),
-// f_lo(m2, m1, m0)) with compile-time truth tables, at most three v_bitop3 with immediates —
-// against 16 leaves with SGPR operands (4.2-cycle forms) and 7 muxes per bit for a table held in
-// SGPRs.  k is wave-uniform: the wave jumps to entry k of a table of 128-byte entries
-// (s_getpc + s_setpc) and back.  (A C++ switch over the 210 tables, a binary tree of scalar
-// branches with 210 leaves, made the register allocator spill 291 VGPRs.)  The caller keeps k
-// in [0, kNBetaTab).  s40-s42 are the jump's scratch.
+// table k of the fixed set: each output bit j is mux(m3, f_hi(m2, m1, m0), f_lo(m2, m1, m0))
+// with compile-time truth tables, at most three v_bitop3 with immediates, against 16 leaves with
+// SGPR operands (4.2-cycle forms) and 7 muxes per bit for a table held in SGPRs.  (A C++ switch
+// over the 210 tables, a binary tree of scalar branches with 210 leaves, made the register
+// allocator spill 291 VGPRs.)
 __device__ __forceinline__ void beta_asm(uint32_t (&o)[4], const uint32_t (&m)[4], int k) {
     uint32_t t0, t1;
-    asm volatile(
-        "s_getpc_b64 s[40:41]\n"
-        ".Lbpc%=:\n\t"
-        "s_lshl_b32 s42, %[k], 7\n\t"
-        "s_add_u32 s40, s40, s42\n\t"
-        "s_addc_u32 s41, s41, 0\n\t"
-        "s_add_u32 s40, s40, .Lbtab%=-.Lbpc%=\n\t"
-        "s_addc_u32 s41, s41, 0\n\t"
-        "s_setpc_b64 s[40:41]\n"
-        "\t.p2align 7\n"
-        ".Lbtab%=:\n"
-        LDPC_BETA_ASM_TABLE
-        "\t.p2align 7\n"
-        ".Lbend%=:"
+    asm volatile(LDPC_TAB_CALL("7", "7", LDPC_BETA_ASM_TABLE)
         : [o0] "=&v"(o[0]), [o1] "=&v"(o[1]), [o2] "=&v"(o[2]), [o3] "=&v"(o[3]),
           [t0] "=&v"(t0), [t1] "=&v"(t1)
         : [m0] "v"(m[0]), [m1] "v"(m[1]), [m2] "v"(m[2]), [m3] "v"(m[3]), [k] "s"(k)
-        : "s40", "s41", "s42", "scc");
+        : "s40", "s41", "s42", "s43", "s44", "s45", "scc");
 }
 #ifndef BS_BFIX
 #define BS_BFIX 1       // the fixed-table channel weighting (A/B switch)
+#endif
+
+// The check phase's two weighted minima through table k of the fixed set, all 4 output bits of
+// both (<= 24 v_bitop3 with immediates, 256-byte entries of LDPC_BETA_ASM_TABLE2)
+__device__ __forceinline__ void table_asm2(uint32_t (&p)[4], uint32_t (&q)[4], const uint32_t (&a)[4],
+                                           const uint32_t (&b)[4], int k) {
+    uint32_t t0, t1;
+    asm volatile(LDPC_TAB_CALL("8", "8", LDPC_BETA_ASM_TABLE2)
+        : [p0] "=&v"(p[0]), [p1] "=&v"(p[1]), [p2] "=&v"(p[2]), [p3] "=&v"(p[3]),
+          [q0] "=&v"(q[0]), [q1] "=&v"(q[1]), [q2] "=&v"(q[2]), [q3] "=&v"(q[3]),
+          [t0] "=&v"(t0), [t1] "=&v"(t1)
+        : [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]),
+          [b0] "v"(b[0]), [b1] "v"(b[1]), [b2] "v"(b[2]), [b3] "v"(b[3]), [k] "s"(k)
+        : "s40", "s41", "s42", "s43", "s44", "s45", "scc");
+}
+// a chunk of check lanes whose checks lie in two rows (lanes < split: table k0, the others k1)
+__device__ __forceinline__ void alpha_fixed(uint32_t (&p)[4], uint32_t (&q)[4], const uint32_t (&a)[4],
+                                            const uint32_t (&b)[4], int k0, int k1, int split) {
+    if (k0 == k1) {
+        table_asm2(p, q, a, b, k0);
+    } else {
+        const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        if (ln < split) table_asm2(p, q, a, b, k0);
+        else table_asm2(p, q, a, b, k1);
+    }
+}
+// The fixed-table check weighting (A/B switch, off).  Measured on one box (r3g): C3 20.1
+// against 18.9 ms, C4 16.2 against 15.2, C2 5.69 against 5.71; compiled in but disabled, the
+// others ran 3-7 % slower than without it.  Not the instruction cache (the out-of-line tables
+// changed nothing, r3i): the table call holds 18 operands live at once, and the higher register
+// pressure of the whole check phase costs more than the table words and the lane exchange.
+#ifndef BS_AFIX
+#define BS_AFIX 0
 #endif
 
 // lane permutation inside each group of 4 lanes (DPP quad_perm, a VALU move)
@@ -795,6 +853,9 @@ k_bs(BsArgs a) {
     // 16 words per bit, at 64 B per bit.)
     const int cj = lane % LPC;
     int gchunk[CPL], gdeg[CPL], gm[CPL];
+    // fixed-set check tables: the chunk's first row | (first lane of the next row) << 16 (64: one
+    // row); -1: its checks span more than two rows (the table words then)
+    int grow[CPL];
     uint32_t gbase[CPL], gtab[CPL], ghd[CPL][UCN ? HDW : 1];
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
@@ -811,6 +872,13 @@ k_bs(BsArgs a) {
         gm[c] = SKIPM ? (int)__popc(wave_or((1u << ((gdeg[c] + LPC - 1) / LPC)) - 1u)) : EPL;
         gbase[c] = a.off_slots + (uint32_t)((a.row_lay[2 * ci] + cj * a.row_lay[2 * ci + 1] + (cc - ci * a.z)) * SLOT_B);
         gtab[c] = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * OB * 64);
+        {
+            const int ch = max(gchunk[c], 0), mr = a.n_checks / a.z - 1;
+            const int c0 = ch * (64 / LPC);
+            const int r0 = min(c0 / a.z, mr), r1 = min((c0 + 64 / LPC - 1) / a.z, mr);
+            const int split = (r1 == r0) ? 64 : LPC * (r1 * a.z - c0);
+            grow[c] = __builtin_amdgcn_readfirstlane(a.arows == 1 ? (64 << 16) : (r1 - r0 > 1 ? -1 : (r0 | split << 16)));
+        }
         if constexpr (UCN) {
 #pragma unroll
             for (int p = 0; p < HDW; ++p) ghd[c][p] = (ucn && gchunk[c] >= 0) ? a.cn_hd[(size_t)ql * HDW + p] : 0u;
@@ -962,6 +1030,34 @@ k_bs(BsArgs a) {
                 // frames have converged) skips its table (the same messages, exactly)
                 bool any_unsat = false;
                 if constexpr (UCN) any_unsat = ucn && (!(BS_USKIP && CPL > 1) || __builtin_amdgcn_ballot_w64(syn != 0u) != 0ull);
+                // tables of the fixed set: every lane evaluates all 4 bits of both minima with
+                // immediate truth tables (no table words, no lane exchange)
+                bool fixed = false;
+                if (BS_AFIX && a.atid && grow[c] >= 0) {
+                    const int r0 = grow[c] & 0xFFFF, split = grow[c] >> 16;
+                    const int32_t* at = a.atid + (size_t)t * AR;
+                    const int k0 = __builtin_amdgcn_readfirstlane(at[r0]);
+                    const int k1 = split < 64 ? __builtin_amdgcn_readfirstlane(at[r0 + 1]) : k0;
+                    int u0 = 0, u1 = 0;
+                    if (UCN && any_unsat) {
+                        u0 = __builtin_amdgcn_readfirstlane(at[a.arows + r0]);
+                        u1 = split < 64 ? __builtin_amdgcn_readfirstlane(at[a.arows + r0 + 1]) : u0;
+                    }
+                    fixed = min(min(k0, k1), min(u0, u1)) >= 0 && max(max(k0, k1), max(u0, u1)) < kNBetaTab;
+                    if (fixed) {
+                        alpha_fixed(q1, q2, m1, m2, k0, k1, split);
+                        if (UCN && any_unsat) {             // alpha' where the check is unsatisfied
+                            uint32_t v1[4], v2[4];
+                            alpha_fixed(v1, v2, m1, m2, u0, u1, split);
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                q1[i] = mux(syn, v1[i], q1[i]);
+                                q2[i] = mux(syn, v2[i], q2[i]);
+                            }
+                        }
+                    }
+                }
+                if (!fixed) {
 #pragma unroll
                 for (int b = 0; b < OB; ++b) {
                     uint32_t o[2];
@@ -987,6 +1083,7 @@ k_bs(BsArgs a) {
                     q1[2] = qperm<0xF5>(qb[0][0]); q1[3] = qperm<0xF5>(qb[OB - 1][0]);
                     q2[0] = qperm<0xA0>(qb[0][1]); q2[1] = qperm<0xA0>(qb[OB - 1][1]);
                     q2[2] = qperm<0xF5>(qb[0][1]); q2[3] = qperm<0xF5>(qb[OB - 1][1]);
+                }
                 }
             }
             // pass 2: an edge whose |V->C| equals the minimum gets the weighted second minimum

@@ -54,6 +54,8 @@ struct BscArgs {
     const uint32_t* alut;        // [T][arows][LUT_W]
     const uint32_t* blut;        // [T][bcols][BLUT_W]
     int arows, bcols;
+    const int32_t* atid;         // one alpha per iteration (arows 1): [T] kBetaTab index of its
+                                 // table (-1: not in the set), or null
     int64_t* counters;
     uint8_t* flags;
     uint32_t* bad;
@@ -64,6 +66,21 @@ struct BscArgs {
 };
 
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void lds_qput(uint32_t addr, const uint32_t (&x)[4]) {
+    v4u v;
+    v.x = x[0];
+    v.y = x[1];
+    v.z = x[2];
+    v.w = x[3];
+    *reinterpret_cast<LdsQ*>(addr) = v;
+}
+// the fixed-table check weighting for one alpha per iteration (A/B switch, off: C5 62.7 ms with
+// it against 59.6 without, same box (r3i), and 62.8 with it compiled in but turned off at run
+// time (LDPC_BS_NOAFIX=1) — its 18 live operands raise the register pressure of the whole check
+// phase, which costs more than the 30 table operations and 8 LDS reads it saves)
+#ifndef BSC_AFIX
+#define BSC_AFIX 0
+#endif
 
 // Check records in blocks of 16: the q1 words of records 16 b .. 16 b + 15 (256 B), then their q2
 // words (256 B), so q2 is q1 + 256 (an instruction offset) and a ds_read_b128 group of 16 lanes
@@ -427,9 +444,25 @@ k_bsc(BscArgs a) {
                 par ^= qperm<QP_X2>(par);
                 merge_lanes<QP_X2>(m1, m2);
             }
-            // weighted, quantized minima (Main_Functions.py:266-316): bit OB j.. of the table per lane
+            // weighted, quantized minima (Main_Functions.py:266-316).  One table of the fixed set
+            // for the whole iteration (uniform alpha: C5): all 4 bits of both by immediate truth
+            // tables (one entry of the jump table for all waves: no instruction-cache churn), the
+            // group's first lane writes the record
+            bool fixed = false;
+            if (BSC_AFIX && a.atid) {
+                const int k = __builtin_amdgcn_readfirstlane(a.atid[t]);
+                if (k >= 0 && k < kNBetaTab) {
+                    fixed = true;
+                    uint32_t p1[4], p2[4];
+                    table_asm2(p1, p2, m1, m2, k);
+                    if (cdeg > 0 && cj == 0) {
+                        lds_qput(grec[c], p1);
+                        lds_qput(grec[c] + REC_Q2, p2);
+                    }
+                }
+            }
             uint32_t qb[OB][2];
-            {
+            if (!fixed) {
                 const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
                 const uint32_t tab = gtab[c] + (uint32_t)((t & 1) * AL * 4);
 #pragma unroll
@@ -443,7 +476,7 @@ k_bsc(BscArgs a) {
             // the record: lane j writes planes OB j .. of q1 and q2 (the whole group has read the
             // old record above: same wave, LDS operations in program order); idle lanes past
             // the last check (degree 0) share its clamped record address and must not write
-            if (cdeg > 0) {
+            if (!fixed && cdeg > 0) {
 #pragma unroll
                 for (int b = 0; b < OB; ++b) {
                     lds_put(grec[c] + 4u * (uint32_t)(OB * cj + b), qb[b][0]);
@@ -510,7 +543,8 @@ std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap);
 std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch);
 std::vector<int> column_rotation(const host::GraphTables& h, int LPC, int EPL, int cn_lanes);
 int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, int qmax,
-                   float cu, bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s);
+                   float cu, bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s,
+                   const int32_t** atid = nullptr);
 bool bs_mode(int mode);
 float bs_step(int mode);
 int bs_qmax(int mode);
@@ -754,7 +788,8 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     const BscInst& k = kBscInst[p.inst];
     const float step = bs_step(mode);
     uint32_t *alut = nullptr, *blut = nullptr;
-    st = bs_make_tables(b, g, p.arows, p.arows, p.bcols, step, bs_qmax(mode), p.cu, false, ws, &alut, &blut, s);
+    const int32_t* atid = nullptr;
+    st = bs_make_tables(b, g, p.arows, p.arows, p.bcols, step, bs_qmax(mode), p.cu, false, ws, &alut, &blut, s, &atid);
     if (st != LDPC_OK) return st;
     const uint32_t* gt = reinterpret_cast<const uint32_t*>(ws.bs_graph);
     const int VNW = k.DVH + 1;
@@ -779,6 +814,7 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     a.cn_chunk = a.row_lay + 2 * (size_t)g.M;
     a.cn_var = reinterpret_cast<const uint32_t*>(a.cn_chunk + (size_t)p.nw * k.CPL);
     a.alut = alut;
+    a.atid = (p.arows == 1 && !getenv("LDPC_BS_NOAFIX")) ? atid : nullptr;
     a.blut = blut;
     a.arows = p.arows;
     a.bcols = p.bcols;
