@@ -85,7 +85,8 @@ constexpr auto launch_table(std::integer_sequence<int, I...>) {
 struct BsPlan {
     bool ok = false;
     int inst = -1, nw = 0, cn_lanes = 0, arows = 1, bcols = 1;
-    uint32_t off_slots = 0, off_pad = 0, off_zero = 0, off_red = 0, off_alut = 0, off_blut = 0, off_hdz = 0;
+    uint32_t off_slots = 0, off_pad = 0, off_zero = 0, off_red = 0, off_alut = 0, off_blut = 0, off_hdz = 0,
+             off_btid = 0;
     int cn_dmin = 0;
     bool ucn = false;
     float cu = 0.f;
@@ -158,7 +159,10 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
         p.nw = k.NW;
         if (vch > k.VPL * p.nw || cch > k.CPL * p.nw) return p;
     }
-    p.arows = (g.w_alpha_uniform && !ucn) ? 1 : h.M;
+    // (one alpha / alpha' per iteration: one table pair, read by every lane at the same address,
+    // a broadcast; per-row copies of it put the rows' tables in the same banks)
+    const char* eap = getenv("LDPC_BS_AROWS");
+    p.arows = ((g.w_alpha_uniform && !ucn) || (g.w_alpha_pair_uniform && !(eap && atoi(eap) == 0))) ? 1 : h.M;
     p.bcols = g.w_beta_uniform ? 1 : h.N;
     // idle check lanes: every slot is decided per lane
     p.cn_dmin = (p.cn_lanes == k.LPC * nc) ? min_cdeg : 0;
@@ -189,6 +193,8 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     o += (size_t)2 * (k.UCN ? 2 : 1) * p.arows * LUT_W * 4;
     p.off_blut = (uint32_t)o;
     o += (size_t)2 * p.bcols * BLUT_W * 4;
+    p.off_btid = (uint32_t)o;                      // the next iteration's channel-table ids
+    o += ((size_t)4 * p.bcols + 15) & ~(size_t)15;
     p.lds = (o + 15) & ~(size_t)15;
     if (p.lds > BS_LDS_MAX) return p;
     p.ok = true;
@@ -644,6 +650,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.off_alut = p.off_alut;
     a.off_blut = p.off_blut;
     a.off_hdz = p.off_hdz;
+    a.off_btid = p.off_btid;
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // -DBS_DIAG builds
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
     static const auto kLaunch = launch_table(std::make_integer_sequence<int, kBsNInst>{});

@@ -96,7 +96,7 @@ struct BsArgs {
     uint32_t* iter_wrong;        // [T][packs] per-iteration frame-error words, or null
     uint32_t* hdx;               // XP builds: [T][packs][n_vars] hard decisions (bit r = codeword
                                  // 32 pack + r), the hard-bit / syndrome export
-    uint32_t off_slots, off_pad, off_zero, off_red, off_alut, off_blut, off_hdz;   // LDS byte offsets
+    uint32_t off_slots, off_pad, off_zero, off_red, off_alut, off_blut, off_hdz, off_btid;   // LDS byte offsets
                                  // (RED: 16 words, then T words: iteration t's frame-error word)
     int ablate;   // timing diagnostics, builds with -DBS_DIAG only (LDPC_DIAG_ABLATE, wrong
                   // results): 1 no check phase, 2 no beta table, 4 no V->C pass, 8 no frame
@@ -365,6 +365,12 @@ __device__ __forceinline__ void beta_asm(uint32_t (&o)[4], const uint32_t (&m)[4
 }
 #ifndef BS_BFIX
 #define BS_BFIX 1       // the fixed-table channel weighting (A/B switch)
+#endif
+// The table ids staged in LDS per iteration (one global_load_lds by wave 0 at the iteration
+// start) instead of a global load after the barrier (A/B switch, off: same box, r3k, C3 18.29
+// against 16.60 ms, C2 5.41 against 5.26)
+#ifndef BS_BTID_LDS
+#define BS_BTID_LDS 0
 #endif
 
 // The check phase's two weighted minima through table k of the fixed set, all 4 output bits of
@@ -678,7 +684,9 @@ k_bs(BsArgs a) {
             if constexpr (!XP && BS_BFIX) {
                 if (!first && !last && a.btid) {
                     const int col = (a.bcols == 1) ? 0 : pcol[u];
-                    if (col >= 0) bk = __builtin_amdgcn_readfirstlane(a.btid[(size_t)tb * a.btid_n + col]);
+                    if (col >= 0)
+                        bk = __builtin_amdgcn_readfirstlane(BS_BTID_LDS ? (int)lds_w(a.off_btid + 4u * (uint32_t)col)
+                                                                        : a.btid[(size_t)tb * a.btid_n + col]);
                 }
             }
             if (!last) {
@@ -916,12 +924,18 @@ k_bs(BsArgs a) {
                 copy_async(a.off_alut + 4u * (uint32_t)(nx * AL), a.alut + (size_t)(t + 1) * AL, AL, cw, NT);
                 if (a.bcols > 1)
                     copy_async(a.off_blut + 4u * (uint32_t)(nx * BL), a.blut + (size_t)(t + 1) * BL, BL, cw, NT);
+                if (!XP && BS_BFIX && BS_BTID_LDS && a.btid)   // this iteration's variable phase: ids of row t + 1
+                    copy_async(a.off_btid, reinterpret_cast<const uint32_t*>(a.btid) + (size_t)(t + 1) * a.btid_n,
+                               a.bcols == 1 ? 1 : a.btid_n, cw, NT);
             } else {
                 int tl = tid;
                 asm volatile("" : "+v"(tl));
                 for (int w = tl; w < AL; w += NT) ALUT[nx * AL + w] = a.alut[(size_t)(t + 1) * AL + w];
                 if (a.bcols > 1)
                     for (int w = tl; w < BL; w += NT) BLUT[nx * BL + w] = a.blut[(size_t)(t + 1) * BL + w];
+                if (!XP && BS_BFIX && BS_BTID_LDS && a.btid)
+                    for (int w = tl; w < (a.bcols == 1 ? 1 : a.btid_n); w += NT)
+                        lds_put(a.off_btid + 4u * (uint32_t)w, (uint32_t)a.btid[(size_t)(t + 1) * a.btid_n + w]);
             }
         }
         // ======== check nodes ===================================================================

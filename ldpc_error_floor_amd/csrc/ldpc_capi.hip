@@ -345,6 +345,7 @@ int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* 
     g->dev.h_row_merge = g->row_merge.data();
     g->dev.row_merge = g->d_row_merge;
     g->dev.w_alpha_uniform = wi.alpha_uniform;
+    g->dev.w_alpha_pair_uniform = wi.alpha_pair_uniform;
     g->dev.w_beta_uniform = wi.beta_uniform;
     g->dev.w_beta_nonneg = wi.beta_nonneg;
     g->dev.w_beta_one = wi.beta_one;

@@ -113,6 +113,13 @@ int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const f
         w.row_merge[(size_t)i] = same ? 1 : 0;
     }
     w.alpha_uniform = (!w.per_edge_w && !alpha_ucn) ? 1 : 0;
+    w.alpha_pair_uniform = !w.per_edge_w ? 1 : 0;
+    for (int t = 0; t < T && w.alpha_pair_uniform; ++t) {
+        const size_t a0 = (size_t)t * g.E;
+        for (int e = 1; e < g.E && w.alpha_pair_uniform; ++e)
+            if (alpha[a0 + e] != alpha[a0] || (alpha_ucn && alpha_ucn[a0 + e] != alpha_ucn[a0]))
+                w.alpha_pair_uniform = 0;
+    }
     w.beta_uniform = 1;
     w.beta_nonneg = 1;
     w.beta_one = 1;

@@ -72,6 +72,9 @@ int build_graph(const int32_t* proto, int32_t M, int32_t N, int32_t z, GraphTabl
 struct WeightInfo {
     int per_edge_w = 0;
     int alpha_uniform = 0, beta_uniform = 0, beta_nonneg = 0, beta_one = 0;
+    // alpha and (if given) alpha_ucn each one value per iteration (UCN decoders: one table pair
+    // per iteration instead of one per row)
+    int alpha_pair_uniform = 0;
     // bit t (t < 64): every column's q5/q-5 channel table of iteration t is the identity,
     // min(15, |rint(fl32(m beta))|) == m for m = 0..15 (the bit-sliced kernels skip it)
     uint64_t beta_id_mask = 0;
