@@ -86,7 +86,7 @@ struct BsPlan {
     bool ok = false;
     int inst = -1, nw = 0, cn_lanes = 0, arows = 1, bcols = 1;
     uint32_t off_slots = 0, off_pad = 0, off_zero = 0, off_red = 0, off_alut = 0, off_blut = 0, off_hdz = 0,
-             off_btid = 0;
+             off_btid = 0, off_ch = 0;
     int cn_dmin = 0;
     bool ucn = false;
     float cu = 0.f;
@@ -195,6 +195,10 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     o += (size_t)2 * p.bcols * BLUT_W * 4;
     p.off_btid = (uint32_t)o;                      // the next iteration's channel-table ids
     o += ((size_t)4 * p.bcols + 15) & ~(size_t)15;
+    if (BS_CH_LDS) {                               // the channel planes, 16 B per (lane, variable)
+        p.off_ch = (uint32_t)o;
+        o += (size_t)16 * k.VPL * 64 * p.nw;
+    }
     p.lds = (o + 15) & ~(size_t)15;
     if (p.lds > BS_LDS_MAX) return p;
     p.ok = true;
@@ -396,6 +400,25 @@ std::vector<int> column_rotation(const host::GraphTables& h, int LPC, int EPL, i
         }
     }
     return toff;
+}
+
+// first-generation start offsets of the one-workgroup-per-CU instances (BsArgs::stagger):
+// LDPC_BS_STAGGER = the spread in microseconds (0: off)
+void bs_stagger(bool one_per_cu, int* stagger, int* stagger_n) {
+    *stagger = 0;
+    *stagger_n = 0;
+    const char* e = getenv("LDPC_BS_STAGGER");
+    const double us = e ? atof(e) : (one_per_cu ? BS_STAGGER_US : 0.0);
+    if (!(us > 0.0)) return;
+    int dev = 0, ncu = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeClockRate, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    *stagger = (int)(us * 1e-3 * (double)khz / 512.0);      // s_sleep 8 = 512 clocks
+    *stagger_n = ncu;
 }
 
 // the per-decode weight tables of both bit-sliced kernels (k_bs_tables)
@@ -643,6 +666,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.bad = bad;
     a.iter_wrong = b.iter_wrong;
     a.hdx = hdx;
+    bs_stagger(k.VPL > 1 || k.CPL > 1, &a.stagger, &a.stagger_n);
     a.off_slots = p.off_slots;
     a.off_pad = p.off_pad;
     a.off_zero = p.off_zero;
@@ -651,6 +675,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.off_blut = p.off_blut;
     a.off_hdz = p.off_hdz;
     a.off_btid = p.off_btid;
+    a.off_ch = p.off_ch;
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // -DBS_DIAG builds
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
     static const auto kLaunch = launch_table(std::make_integer_sequence<int, kBsNInst>{});

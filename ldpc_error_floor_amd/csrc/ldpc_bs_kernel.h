@@ -94,9 +94,12 @@ struct BsArgs {
     uint8_t* flags;
     uint32_t* bad;               // [packs] 1: decoded by the v5 fixup instead
     uint32_t* iter_wrong;        // [T][packs] per-iteration frame-error words, or null
+    int stagger, stagger_n;      // start offsets of workgroups 0 .. stagger_n - 1 (the first
+                                 // generation, one per CU), spread over 0 .. stagger x 512 clocks
     uint32_t* hdx;               // XP builds: [T][packs][n_vars] hard decisions (bit r = codeword
                                  // 32 pack + r), the hard-bit / syndrome export
     uint32_t off_slots, off_pad, off_zero, off_red, off_alut, off_blut, off_hdz, off_btid;   // LDS byte offsets
+    uint32_t off_ch;             // BS_CH_LDS: the channel's magnitude planes, [lane][VPL][4] words
                                  // (RED: 16 words, then T words: iteration t's frame-error word)
     int ablate;   // timing diagnostics, builds with -DBS_DIAG only (LDPC_DIAG_ABLATE, wrong
                   // results): 1 no check phase, 2 no beta table, 4 no V->C pass, 8 no frame
@@ -129,13 +132,16 @@ __device__ __forceinline__ uint32_t mux(uint32_t s, uint32_t a, uint32_t b) { re
 // two's complement of m is b sign-extended with n, plus n
 template <int SB>
 __device__ __forceinline__ void add_b(uint32_t (&S)[SB], const uint32_t (&b)[4], uint32_t n) {
+    // (the carry first: S[i]'s last use is then the instruction that redefines it, so the sum
+    // stays in S's registers; summed under a wave-uniform "edge f exists" branch, the other order
+    // left a copy of every plane at the branch's merge, 7 v_mov per edge)
     uint32_t c = n;
 #pragma unroll
     for (int i = 0; i < SB; ++i) {
         const uint32_t bi = (i < 4) ? b[i] : n;
-        const uint32_t s = B3(T_XOR3, S[i], bi, c);
-        if (i + 1 < SB) c = B3(T_MAJ, S[i], bi, c);
-        S[i] = s;
+        const uint32_t cn = (i + 1 < SB) ? B3(T_MAJ, S[i], bi, c) : 0u;
+        S[i] = B3(T_XOR3, S[i], bi, c);
+        c = cn;
     }
 }
 // S = m (same operand form), S previously zero
@@ -483,6 +489,15 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
 // 2 rounds (tools/bs_variant.sh -DBS_KEEP=k): C2 5.79 (0) / 5.70 (1) / 5.58 (2) / 5.56 (3) /
 // 5.55 (4) / 5.71 ms (6); C3 18.75 / 18.53 / 18.25 / 17.80 / 17.76 / 17.75; C4 18.15 / 17.97 /
 // 17.81 / 17.76 / 17.67 / 17.62 ms.
+// the channel's 4 magnitude planes of each variable kept in LDS (one ds_read_b128 per variable
+// and iteration) instead of 4 registers held through the whole decode (A/B switch)
+#ifndef BS_CH_LDS
+#define BS_CH_LDS 0
+#endif
+// first-generation start spread of the one-workgroup-per-CU instances, microseconds (bs_stagger)
+#ifndef BS_STAGGER_US
+#define BS_STAGGER_US 0.0
+#endif
 #ifndef BS_KEEP
 #define BS_KEEP 4
 #endif
@@ -575,6 +590,15 @@ k_bs(BsArgs a) {
     // ---- channel planes: the lane's variables for the 32 codewords of the pack ------------------
     // (no __syncthreads_or: it allocates static LDS, which would move the dynamic LDS base
     // away from 0; the flag word lives in RED)
+    // one workgroup per CU: the first generation starts in lockstep, and with every pack taking
+    // the same time, each later generation again fetches its LLR blocks in one chip-wide burst
+    // while HBM idles the rest of the pack.  Spreading the first starts over a pack's duration
+    // keeps the fetches apart for the whole grid (later workgroups inherit the offsets).
+    if (a.stagger > 0 && (int)blockIdx.x < a.stagger_n) {
+        const int n = (int)(((uint32_t)blockIdx.x * 97u % (uint32_t)a.stagger_n) * (uint32_t)a.stagger /
+                            (uint32_t)a.stagger_n);
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(8);
+    }
     if (tid == 0) RED[7] = 0u;
     __syncthreads();
     uint32_t cs[VPL], cm[VPL][4], bg[VPL];
@@ -644,6 +668,17 @@ k_bs(BsArgs a) {
         return;
     }
     if (tid == 0) a.bad[blockIdx.x] = 0u;
+    if (BS_CH_LDS) {
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) {
+            v4u c4;
+            c4.x = cm[u][0];
+            c4.y = cm[u][1];
+            c4.z = cm[u][2];
+            c4.w = cm[u][3];
+            *reinterpret_cast<LdsQ*>(a.off_ch + 16u * (uint32_t)(tid * VPL + u)) = c4;
+        }
+    }
     // PAD slot (all ones: V->C negative, magnitude 15), ZERO slot (a zero C->V), the zero hard
     // decision word of UCN padding edges, counters, iteration 0's tables
     if (tid < SLOT_W) {
@@ -677,6 +712,16 @@ k_bs(BsArgs a) {
             };
             const int v = (UCN && vv[u] >= 0) ? (vv[u] & 0xFFFF) : vv[u];
             const uint32_t hda = UCN ? 4u * ((uint32_t)vv[u] >> 16) : 0u;     // HD slot (rotated)
+            uint32_t cmu[4] = {cm[u][0], cm[u][1], cm[u][2], cm[u][3]};
+            if (BS_CH_LDS) {
+                int tl = tid;
+                asm volatile("" : "+v"(tl));
+                const v4u c4 = lds_q(a.off_ch + 16u * (uint32_t)(tl * VPL + u));
+                cmu[0] = c4.x;
+                cmu[1] = c4.y;
+                cmu[2] = c4.z;
+                cmu[3] = c4.w;
+            }
             const bool counted = v >= 0 && v < a.target_bits;
             uint32_t lw[1][4];                   // |Q(beta_{t+1} ch)| (before the C->V: fewer live registers)
             // the table's index in the fixed set (wave-uniform; -1: evaluate the table words)
@@ -693,9 +738,9 @@ k_bs(BsArgs a) {
                 // identity table: |Q(beta ch)| = |ch| (the mask covers iterations 0..63)
                 if (ABL(2) || (tb < 64 && ((a.beta_id >> tb) & 1))) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) lw[0][i] = cm[u][i];
+                    for (int i = 0; i < 4; ++i) lw[0][i] = cmu[i];
                 } else if (bk >= 0 && bk < kNBetaTab) {   // a table of the fixed set
-                    beta_asm(lw[0], cm[u], bk);
+                    beta_asm(lw[0], cmu, bk);
                     if constexpr (BIG) {            // shortened bits: |Q(beta cu)| from the table words
                         if (a.bcols == 1) {
                             const ConstW* tg = (const ConstW*)(a.blut) + (size_t)tb * BLUT_W;
@@ -711,14 +756,14 @@ k_bs(BsArgs a) {
                     }
                 } else if (a.bcols == 1) {          // one beta per iteration: table in SGPRs
                     const ConstW* tg = (const ConstW*)(a.blut) + (size_t)tb * BLUT_W;
-                    lut_s(lw[0], cm[u], tg);
+                    lut_s(lw[0], cmu, tg);
                     if constexpr (BIG) {
 #pragma unroll
                         for (int i = 0; i < 4; ++i) lw[0][i] = mux(bg[u], tg[LUT_W + i], lw[0][i]);
                     }
                 } else {
                     const uint32_t btab = bslice + tab_b[u];
-                    const uint32_t cmi[1][4] = {{cm[u][0], cm[u][1], cm[u][2], cm[u][3]}};
+                    const uint32_t cmi[1][4] = {{cmu[0], cmu[1], cmu[2], cmu[3]}};
                     lut<1>(lw, cmi, btab);
                     if constexpr (BIG) {
                         const v4u gb = lds_q(btab + LUT_W * 4);
@@ -762,7 +807,7 @@ k_bs(BsArgs a) {
                     uint32_t A[SB];
 #pragma unroll
                     for (int i = 0; i < SB; ++i) A[i] = S[i];
-                    const uint32_t cb[4] = {cm[u][0] ^ c_s, cm[u][1] ^ c_s, cm[u][2] ^ c_s, cm[u][3] ^ c_s};
+                    const uint32_t cb[4] = {cmu[0] ^ c_s, cmu[1] ^ c_s, cmu[2] ^ c_s, cmu[3] ^ c_s};
                     add_b<SB>(A, cb, c_s);
                     hd = ~A[SB - 1];
 #pragma unroll
@@ -770,7 +815,7 @@ k_bs(BsArgs a) {
                 } else {
                     uint32_t c = c_s;
 #pragma unroll
-                    for (int i = 0; i < SB - 1; ++i) c = B3(T_MAJ, S[i], i < 4 ? (cm[u][i] ^ c_s) : c_s, c);
+                    for (int i = 0; i < SB - 1; ++i) c = B3(T_MAJ, S[i], i < 4 ? (cmu[i] ^ c_s) : c_s, c);
                     hd = B3(T_XNOR3, S[SB - 1], c_s, c);
                 }
                 if (UCN && !last && ucn && v >= 0) lds_put(hda, hd);   // HD[v] (Main_Functions.py:184-188)

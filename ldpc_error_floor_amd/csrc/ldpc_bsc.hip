@@ -60,6 +60,8 @@ struct BscArgs {
     uint8_t* flags;
     uint32_t* bad;
     uint32_t* iter_wrong;        // [T][packs] per-iteration frame-error words, or null
+    int stagger, stagger_n;      // start offsets of workgroups 0 .. stagger_n - 1 (the first
+                                 // generation, one per CU), spread over 0 .. stagger x 512 clocks
     uint32_t* hdx;               // XP builds: [T][packs][n_vars] hard decisions (as bsl's)
     uint32_t off_a, off_rec, off_tv, off_red, off_alut, off_blut;   // SGN at LDS byte 0
                                  // (RED: 16 words, then T words: iteration t's frame-error word)
@@ -140,6 +142,15 @@ k_bsc(BscArgs a) {
 
     // ---- channel planes (as bsl: shortened bits = +-cu decoded here, other off-grid packs
     // flagged for the v5 fixup) --------------------------------------------------------------
+    // one workgroup per CU: the first generation starts in lockstep, and with every pack taking
+    // the same time, each later generation again fetches its LLR blocks in one chip-wide burst
+    // while HBM idles the rest of the pack.  Spreading the first starts over a pack's duration
+    // keeps the fetches apart for the whole grid (later workgroups inherit the offsets).
+    if (a.stagger > 0 && (int)blockIdx.x < a.stagger_n) {
+        const int n = (int)(((uint32_t)blockIdx.x * 97u % (uint32_t)a.stagger_n) * (uint32_t)a.stagger /
+                            (uint32_t)a.stagger_n);
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(8);
+    }
     if (tid == 0) RED[7] = 0u;
     __syncthreads();
     uint32_t cs[VPL], cm[VPL][4], bg[VPL];
@@ -542,6 +553,7 @@ std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* ns
 std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap);
 std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch);
 std::vector<int> column_rotation(const host::GraphTables& h, int LPC, int EPL, int cn_lanes);
+void bs_stagger(bool one_per_cu, int* stagger, int* stagger_n);
 int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcols, float step, int qmax,
                    float cu, bool ucn, FusedWorkspace& ws, uint32_t** alut, uint32_t** blut, hipStream_t s,
                    const int32_t** atid = nullptr);
@@ -813,6 +825,7 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     a.row_lay = a.vn_wdeg + 2 * (size_t)k.VPL * p.nw;
     a.cn_chunk = a.row_lay + 2 * (size_t)g.M;
     a.cn_var = reinterpret_cast<const uint32_t*>(a.cn_chunk + (size_t)p.nw * k.CPL);
+    bs_stagger(true, &a.stagger, &a.stagger_n);
     a.alut = alut;
     a.atid = (p.arows == 1 && !getenv("LDPC_BS_NOAFIX")) ? atid : nullptr;
     a.blut = blut;
