@@ -494,6 +494,72 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
 #ifndef BS_CH_LDS
 #define BS_CH_LDS 0
 #endif
+// The channel planes of one variable for the 32 codewords of a pack: sign cs, magnitude planes
+// cm[0..3] of Q(ch) in grid units, shortened-bit flags bg (BIG); returns 1 when a row is off the
+// grid (the pack then goes to the v5 fixup).  Per row: x = llr / step, q = clamp(rint(x), +-qmax)
+// — on the grid iff q == x, or a shortened bit (|x| == cu, decoded as +-qmax) — and q is stored
+// as the byte q + 16 (+ 32 for a shortened bit) by v_cvt_pk_u8_f32, four rows per word.  The 32
+// bytes become bit planes by four 8x8 bit-matrix transposes (three delta swaps each) and a 4x4
+// byte transpose (v_perm); offset binary q + 16 gives the sign (NOT bit 4) and, bit-sliced, the
+// magnitude (the low 4 bits, negated mod 16 where negative).  About 300 VALU per variable against
+// ~750 for a per-row insertion of each bit into each plane (2 ops per bit and plane).
+// (valid: the pack's codewords; rows past it read 0 and are masked)
+__device__ __forceinline__ void t8x8(uint32_t& lo, uint32_t& hi) {
+    uint32_t t;
+    t = B3((TA ^ TB) & TC, lo, lo >> 7, 0x00AA00AAu);
+    lo = B3(T_XOR3, lo, t, t << 7);
+    t = B3((TA ^ TB) & TC, hi, hi >> 7, 0x00AA00AAu);
+    hi = B3(T_XOR3, hi, t, t << 7);
+    t = B3((TA ^ TB) & TC, lo, lo >> 14, 0x0000CCCCu);
+    lo = B3(T_XOR3, lo, t, t << 14);
+    t = B3((TA ^ TB) & TC, hi, hi >> 14, 0x0000CCCCu);
+    hi = B3(T_XOR3, hi, t, t << 14);
+    t = B3((TA ^ TB) & TC, lo, hi << 4, 0xF0F0F0F0u);
+    lo ^= t;
+    hi ^= t >> 4;
+}
+template <bool BIG>
+__device__ __forceinline__ int pack_channel(const float (&xv)[PACK], float inv, int qmax, float cu,
+                                            uint32_t valid, uint32_t& cs, uint32_t (&cm)[4], uint32_t& bg) {
+    const float qf = (float)qmax;
+    uint32_t D[8];
+    int off = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) D[k] = 0u;
+#pragma unroll
+    for (int r = 0; r < PACK; ++r) {
+        const float x = xv[r] * inv;
+        const float q = __builtin_amdgcn_fmed3f(rintf(x), -qf, qf);
+        const bool big = BIG && fabsf(x) == cu;
+        off |= (q != x && !big) ? 1 : 0;
+        D[r >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(q + (big ? 48.f : 16.f), r & 3, D[r >> 2]);
+    }
+    uint32_t lo[4], hi[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        lo[g] = D[2 * g];
+        hi[g] = D[2 * g + 1];
+        t8x8(lo[g], hi[g]);
+    }
+    // byte p of lo[g] (p < 4) / hi[g] (p >= 4): plane p of rows 8 g .. 8 g + 7
+    const uint32_t a = __builtin_amdgcn_perm(lo[1], lo[0], 0x06020400u), b = __builtin_amdgcn_perm(lo[1], lo[0], 0x07030501u);
+    const uint32_t c = __builtin_amdgcn_perm(lo[3], lo[2], 0x06020400u), d = __builtin_amdgcn_perm(lo[3], lo[2], 0x07030501u);
+    const uint32_t L0 = __builtin_amdgcn_perm(c, a, 0x05040100u) & valid, L2 = __builtin_amdgcn_perm(c, a, 0x07060302u) & valid;
+    const uint32_t L1 = __builtin_amdgcn_perm(d, b, 0x05040100u) & valid, L3 = __builtin_amdgcn_perm(d, b, 0x07060302u) & valid;
+    const uint32_t e = __builtin_amdgcn_perm(hi[1], hi[0], 0x05010400u), f = __builtin_amdgcn_perm(hi[3], hi[2], 0x05010400u);
+    const uint32_t n = ~__builtin_amdgcn_perm(f, e, 0x05040100u) & valid;
+    bg = BIG ? (__builtin_amdgcn_perm(f, e, 0x07060302u) & valid) : 0u;
+    cs = n;
+    cm[0] = L0;
+    cm[1] = B3(T_XAND, L1, n, L0);
+    cm[2] = B3(T_XAND, L2, n, L0 | L1);
+    cm[3] = B3(T_XAND, L3, n, L0 | L1 | L2);
+    return off;
+}
+#ifndef BS_PACKT
+#define BS_PACKT 1      // pack_channel (A/B switch; 0: per-row bit insertion)
+#endif
+
 // first-generation start spread of the one-workgroup-per-CU instances, microseconds (bs_stagger)
 #ifndef BS_STAGGER_US
 #define BS_STAGGER_US 0.0
@@ -640,7 +706,13 @@ k_bs(BsArgs a) {
         const int u1 = u + 1 < VPL ? u + 1 : u;
         const int vn = (u + 1 < VPL && !ABL(32)) ? var_of(u1) : -1;
         const bool inter = BS_LLR_ALL && v >= 0 && vn >= 0 && !ABL(32);   // next loads interleaved
-        if (v >= 0 && !ABL(32)) {
+        if (BS_PACKT && v >= 0 && !ABL(32)) {
+            if (inter) {
+#pragma unroll
+                for (int r = 0; r < PACK; ++r) xv[u1][r] = llr_at(r, vn);
+            }
+            off |= pack_channel<BIG>(xv[u], a.inv, a.qmax, a.cu, valid, cs[u], cm[u], bg[u]);
+        } else if (v >= 0 && !ABL(32)) {
 #pragma unroll
             for (int r = 0; r < PACK; ++r) {
                 if (inter) xv[u1][r] = llr_at(r, vn);
