@@ -564,6 +564,12 @@ __device__ __forceinline__ int pack_channel(const float (&xv)[PACK], float inv, 
 #ifndef BS_STAGGER_US
 #define BS_STAGGER_US 0.0
 #endif
+// (A/B switch, off: C3 spill-free at 72 VGPRs with it, and slower: 17.37 against 16.07 ms on one
+// box, r3q — pass 2 then waits on its LDS reads, where the spills it removes were reloaded once
+// per iteration)
+#ifndef BS_REREAD
+#define BS_REREAD 0
+#endif
 #ifndef BS_KEEP
 #define BS_KEEP 4
 #endif
@@ -614,6 +620,9 @@ k_bs(BsArgs a) {
     constexpr int VNA = PK ? (DV + 1) / 2 : DV;                  // address words per variable
     constexpr int VNW = VNA + 1;
     constexpr int HDW = (EPL + 1) / 2;                           // packed hd addresses per check lane
+    // pass 2 reads its slots again instead of holding all EPL of them from pass 1 (wide checks:
+    // 30 registers at the check phase's peak, where the 80-register C3 build spilled)
+    constexpr bool RR = BS_REREAD && EPL >= 6;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();          // slots are LDS-absolute
     const int tid = threadIdx.x;
@@ -1093,6 +1102,10 @@ k_bs(BsArgs a) {
             uint32_t syn = 0u;
             if constexpr (UCN) {
                 if (ucn) {
+                    // (the packed addresses made opaque per iteration: unpacked per use, not
+                    // hoisted out of the T loop as EPL registers that the loop then spilled)
+#pragma unroll
+                    for (int p = 0; p < HDW; ++p) asm volatile("" : "+v"(ghd[c][p]));
 #pragma unroll
                     for (int m = 0; m < EPL; ++m) {
                         if (SKIPM && m >= gmc) continue;
@@ -1223,8 +1236,14 @@ k_bs(BsArgs a) {
             for (int m = 0; m < EPL; ++m) {
                 if (real(m)) {
                     const uint32_t addr = cbase + m * cstride;
-                    const uint32_t(&X)[4] = Xs[m];
-                    const uint32_t n = ns[m];
+                    uint32_t X[4], n;
+                    if constexpr (RR) {
+                        read_slot(n, X, addr);       // (the slot still holds this edge's V->C)
+                    } else {
+                        n = ns[m];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) X[i] = Xs[m][i];
+                    }
                     uint32_t Mg[4];
                     uint32_t ne = X[0] ^ m1[0];
 #pragma unroll
