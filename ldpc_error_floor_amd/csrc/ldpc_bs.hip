@@ -102,18 +102,18 @@ struct BsPlan {
 // one m, slots first + j A + h: with first_i = first_{i-1} + z (mod 32) the checks stay
 // consecutive mod 32 across a row boundary, and A_i is the smallest stride >= the j = 0 block
 // whose multiples j A_i (j < LPC) are at least 32 / LPC apart mod 32.
-std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* nslot) {
+std::vector<int32_t> slot_layout_rows(const host::GraphTables& h, const std::vector<int>& rl, size_t* nslot) {
     std::vector<int32_t> lay((size_t)2 * h.M, 0);
-    const int sep = 32 / LPC;
-    auto ok = [&](int A) {
-        for (int d = 1; d < LPC; ++d) {
-            const int r = (d * A) % 32;
-            if (std::min(r, 32 - r) < sep) return false;
-        }
-        return true;
-    };
     size_t cur = 0;
     for (int i = 0; i < h.M; ++i) {
+        const int LPC = rl[(size_t)i], sep = 32 / LPC;
+        auto ok = [&](int A) {
+            for (int d = 1; d < LPC; ++d) {
+                const int r = (d * A) % 32;
+                if (std::min(r, 32 - r) < sep) return false;
+            }
+            return true;
+        };
         const int deg = h.row_ptr[i + 1] - h.row_ptr[i];
         size_t first = cur;
         if (i > 0) first += (size_t)((((int64_t)lay[2 * (i - 1)] + h.z - (int64_t)cur) % 32 + 32) % 32);
@@ -126,6 +126,9 @@ std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* ns
     }
     *nslot = cur;
     return lay;
+}
+std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* nslot) {
+    return slot_layout_rows(h, std::vector<int>((size_t)h.M, LPC), nslot);
 }
 
 // The QMS grids both bit-sliced kernels decode: q = 5 (step 0.5), -5 (1), 4 (1), 3 (2), values
@@ -315,20 +318,34 @@ std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap) {
 // dealing cost of each 64-lane check chunk (LPC lanes per check): the chunk's edge positions
 // that hold a real edge for some lane (the kernels skip the rest wave-uniformly) plus the
 // per-check work that does not depend on the degree
-std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch) {
-    std::vector<int> cost(cch, 2);
+// check lane ql -> check cc | lane cj << 16 | lanes-per-check << 20 (-1: idle) of the uniform
+// layout (checks in order, LPC lanes each)
+std::vector<int32_t> uniform_lanes(const host::GraphTables& h, int LPC, int cn_lanes) {
+    std::vector<int32_t> lanes((size_t)cn_lanes, -1);
     const int nc = h.M * h.z;
+    for (int ql = 0; ql < cn_lanes; ++ql)
+        if (ql / LPC < nc) lanes[(size_t)ql] = (ql / LPC) | ((ql % LPC) << 16) | (LPC << 20);
+    return lanes;
+}
+
+// dealing cost of each 64-lane check chunk: 2 + the edge positions of its widest check
+std::vector<int> check_chunk_cost_lanes(const host::GraphTables& h, const std::vector<int32_t>& lanes) {
+    const int cch = (int)(lanes.size() / 64);
+    std::vector<int> cost(cch, 2);
     for (int ch = 0; ch < cch; ++ch) {
-        int dmax = 0;
+        int pos = 0;
         for (int l = 0; l < 64; ++l) {
-            const int cc = (64 * ch + l) / LPC;
-            if (cc >= nc) break;
-            const int i = cc / h.z;
-            dmax = std::max(dmax, h.row_ptr[i + 1] - h.row_ptr[i]);
+            const int32_t d = lanes[(size_t)64 * ch + l];
+            if (d < 0) continue;
+            const int i = (d & 0xFFFF) / h.z, L = (d >> 20) & 15;
+            pos = std::max(pos, (h.row_ptr[i + 1] - h.row_ptr[i] + L - 1) / L);
         }
-        cost[ch] += (dmax + LPC - 1) / LPC;
+        cost[ch] += pos;
     }
     return cost;
+}
+std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch) {
+    return check_chunk_cost_lanes(h, uniform_lanes(h, LPC, 64 * cch));
 }
 
 // Per-column rotation of a per-variable LDS array (bsc: Tv, 6 dwords per variable; bsl UCN: the
@@ -338,8 +355,8 @@ std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch) 
 // overlap mod 32 (the bank, for b32 reads and for b64 reads of 6-dword records alike) for most
 // column pairs; a hill climb over the toff_j (the cost of a round: the most distinct indices on
 // one bank, the sum of squared bank loads as the tie-break) spreads them.
-std::vector<int> column_rotation(const host::GraphTables& h, int LPC, int EPL, int cn_lanes) {
-    const int z = h.z, nc = h.M * h.z;
+std::vector<int> column_rotation_lanes(const host::GraphTables& h, int EPL, const std::vector<int32_t>& lanes) {
+    const int z = h.z, cn_lanes = (int)lanes.size();
     std::vector<int> toff(h.N, 0);
     {
         std::vector<std::vector<std::pair<int, int>>> grp;          // (column, hh) per round
@@ -347,9 +364,10 @@ std::vector<int> column_rotation(const host::GraphTables& h, int LPC, int EPL, i
         for (int h0 = 0; h0 < cn_lanes; h0 += 32)
             for (int m = 0; m < EPL; ++m) {
                 std::vector<std::pair<int, int>> gl;
-                for (int ql = h0; ql < h0 + 32; ++ql) {
-                    const int cc = ql / LPC, cj = ql % LPC;
-                    if (cc >= nc) continue;
+                for (int ql = h0; ql < h0 + 32 && ql < cn_lanes; ++ql) {
+                    const int32_t d = lanes[(size_t)ql];
+                    if (d < 0) continue;
+                    const int cc = d & 0xFFFF, cj = (d >> 16) & 15, LPC = (d >> 20) & 15;
                     const int i = cc / z, hc = cc - i * z, kk = LPC * m + cj;
                     if (kk >= h.row_ptr[i + 1] - h.row_ptr[i]) continue;
                     const int pe = h.row_ptr[i] + kk;
@@ -400,6 +418,9 @@ std::vector<int> column_rotation(const host::GraphTables& h, int LPC, int EPL, i
         }
     }
     return toff;
+}
+std::vector<int> column_rotation(const host::GraphTables& h, int LPC, int EPL, int cn_lanes) {
+    return column_rotation_lanes(h, EPL, uniform_lanes(h, LPC, cn_lanes));
 }
 
 // first-generation start offsets of the one-workgroup-per-CU instances (BsArgs::stagger):

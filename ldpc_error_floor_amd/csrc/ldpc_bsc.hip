@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "ldpc_bs_kernel.h"
@@ -29,13 +30,19 @@ namespace bs {
 // other variables, LPC lanes per check, VPL variables and CPL check chunks per lane
 // (a wman-sized instance — one variable and one check chunk per lane, 64 VGPRs — was measured
 // against bsl on C2: 61 spills, and the BG1 instance there ran 68 M cw/s against bsl's 176 M)
-struct BscInst { int D, DVH, DVL, LPC, VPL, CPL; int WPE; int NW = 16; };
+// MIX: rows of degree <= LPC / 2 * EPL take LPC / 2 lanes per check (their own 64-lane chunks,
+// after the LPC-lane ones): one lane merge and one more table bit per lane instead of two
+// merges and twice the lanes, for the low-degree rows
+struct BscInst { int D, DVH, DVL, LPC, VPL, CPL; int WPE; int NW = 16; bool MIX = false; };
 constexpr BscInst kBscInst[] = {
     {20, 10, 5, 4, 3, 3, 4},          // 5G BG1 (C5): degree 19 rows, degree 10 / 8 columns, 16 waves
     {20, 10, 5, 2, 3, 2, 4},          // the same with 2 lanes per check (LDPC_BS_LPC A/B)
     // 12 waves: 36 variable chunks on 36 places, 45 check chunks on 48, up to 168 VGPRs (the
     // 16-wave build spills 25 VGPRs at 128): LDPC_BSC_INST=2 A/B
     {20, 10, 5, 4, 3, 4, 3, 12},
+    // mixed lanes per check (5G BG1: four degree-19 rows at 4 lanes, six of degree 3-10 at 2)
+    {20, 10, 5, 4, 3, 3, 4, 16, true},
+    {20, 10, 5, 4, 3, 2, 4, 16, true},
 };
 
 struct BscArgs {
@@ -51,6 +58,7 @@ struct BscArgs {
     const int32_t* vn_wdeg;      // [VPL][nw][2]
     const int32_t* cn_chunk;     // [nw][CPL]
     const uint32_t* cn_var;      // [chunks * 64][CVW] variables of the lane's edges (16-bit packed)
+    const int32_t* cn_lane;      // MIX: [chunks * 64] check | lane << 16 | lanes per check << 20, -1 idle
     const uint32_t* alut;        // [T][arows][LUT_W]
     const uint32_t* blut;        // [T][bcols][BLUT_W]
     int arows, bcols;
@@ -99,12 +107,11 @@ __device__ __forceinline__ void lds_dput(uint32_t addr, uint32_t x, uint32_t y) 
     *reinterpret_cast<LdsD*>(addr) = v;
 }
 
-template <int D, int DVH, int DVL, int LPC, int VPL, int CPL, int WPE, bool XP, int LB>
+template <int D, int DVH, int DVL, int LPC, int VPL, int CPL, int WPE, bool XP, int LB, bool MIX>
 __global__ void __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_bsc(BscArgs a) {
     constexpr int SB = (DVH * QMAX + QMAX <= 127) ? 8 : 9;
     constexpr int EPL = (D + LPC - 1) / LPC;
-    constexpr int OB = 4 / LPC;
     constexpr int VNW = DVH + 1;
     constexpr int CVW = (EPL + 1) / 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -322,24 +329,35 @@ k_bsc(BscArgs a) {
 
     vn_phase(true, false, a.off_blut, 0);
     // check groups (as bsl): lane LPC c + j of a chunk takes edges k = LPC m + j of check c
-    const int cj = lane % LPC;
-    int gchunk[CPL], gdeg[CPL], gm[CPL];
+    // (MIX: each chunk's lanes per check from its lane map; lane 0 of a chunk always holds a check)
+    int gchunk[CPL], gdeg[CPL], gm[CPL], gl4[CPL];
     uint32_t gslot[CPL], grec[CPL], gtab[CPL], gvar[CPL][CVW];
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
         gchunk[c] = __builtin_amdgcn_readfirstlane(a.cn_chunk[wave * CPL + c]);
         const int ql = max(gchunk[c], 0) * 64 + lane;
-        const int cc = ql / LPC;
+        int cc, cjc, Lc = LPC;
+        gl4[c] = 1;
+        if constexpr (MIX) {
+            const int32_t d = gchunk[c] >= 0 ? a.cn_lane[ql] : -1;
+            cc = d < 0 ? a.n_checks : (d & 0xFFFF);
+            cjc = d < 0 ? 0 : ((d >> 16) & 15);
+            gl4[c] = __builtin_amdgcn_readfirstlane(d < 0 ? LPC : ((d >> 20) & 15)) == LPC ? 1 : 0;
+            Lc = gl4[c] ? LPC : LPC / 2;
+        } else {
+            cc = ql / LPC;
+            cjc = lane % LPC;
+        }
         const int ci = min(cc / a.z, a.n_checks / a.z - 1);
         gdeg[c] = (cc < a.n_checks) ? a.row_ptr[ci + 1] - a.row_ptr[ci] : 0;
         // edge positions m holding a real edge for some lane of the chunk (wave-uniform): the
         // positions past them are padding for every lane and skipped (LPC, an even count, lanes
         // of each group skip together, so the group's [V->C >= 0] parity is unchanged)
-        gm[c] = __popc(wave_or((1u << ((gdeg[c] + LPC - 1) / LPC)) - 1u));
+        gm[c] = __popc(wave_or((1u << ((gdeg[c] + Lc - 1) / Lc)) - 1u));
         (void)nwv;
-        gslot[c] = (uint32_t)(4 * (a.row_lay[2 * ci] + cj * a.row_lay[2 * ci + 1] + (cc - ci * a.z)));
+        gslot[c] = (uint32_t)(4 * (a.row_lay[2 * ci] + cjc * a.row_lay[2 * ci + 1] + (cc - ci * a.z)));
         grec[c] = a.off_rec + rec_off((uint32_t)min(cc, a.n_checks - 1));
-        gtab[c] = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * OB * 64);
+        gtab[c] = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cjc * (4 / Lc) * 64);
 #pragma unroll
         for (int p = 0; p < CVW; ++p) gvar[c][p] = gchunk[c] >= 0 ? a.cn_var[(size_t)ql * CVW + p] : 0u;
     }
@@ -377,13 +395,18 @@ k_bsc(BscArgs a) {
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             if (gchunk[c] < 0) continue;
+            // the chunk's check work at L lanes per check (MIX: L = LPC / 2 for the low-degree rows)
+            auto chunk = [&](auto LC) __attribute__((always_inline)) {
+            constexpr int L = decltype(LC)::value;
+            constexpr int OBL = 4 / L;
+            const int cjl = lane & (L - 1);
             const int cdeg = gdeg[c];
             int gmc = gm[c];
             asm volatile("" : "+s"(gmc));
             uint32_t sbase = gslot[c];
             asm volatile("" : "+v"(sbase));
             auto real = [&](int m) __attribute__((always_inline)) -> bool {
-                return LPC * m + LPC - 1 < cn_dmin || LPC * m + cj < cdeg;
+                return L * m + L - 1 < cn_dmin || L * m + cjl < cdeg;
             };
             // V->C = clamp(Tv - C->V_old, +-15) of the lane's edges (padding: negative, 15)
             v4u q1o = {0u, 0u, 0u, 0u}, q2o = {0u, 0u, 0u, 0u};
@@ -421,7 +444,7 @@ k_bsc(BscArgs a) {
                 }
                 abs_sat(Xs[m], x);
                 ns[m] = x[6];
-                if (!(LPC * m + LPC - 1 < cn_dmin) && !real(m)) {
+                if (!(L * m + L - 1 < cn_dmin) && !real(m)) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) Xs[m][i] = ~0u;
                     ns[m] = ~0u;
@@ -429,7 +452,7 @@ k_bsc(BscArgs a) {
             }
             // two minima by a tournament (sorted pairs merged, as bsl); positions past the chunk's
             // bound hold the all-ones padding, so a pair that straddles it sorts correctly and its
-            // padding sign word, XORed by all LPC lanes of the group, leaves the parity unchanged
+            // padding sign word, XORed by all L lanes of the group, leaves the parity unchanged
             uint32_t m1[4], m2[4];
             sort2(m1, m2, Xs[0], Xs[1]);
             uint32_t par = ns[0] ^ ns[1];
@@ -455,7 +478,7 @@ k_bsc(BscArgs a) {
             }
             par ^= qperm<QP_X1>(par);
             merge_lanes<QP_X1>(m1, m2);
-            if (LPC == 4) {
+            if (L == 4) {
                 par ^= qperm<QP_X2>(par);
                 merge_lanes<QP_X2>(m1, m2);
             }
@@ -470,32 +493,32 @@ k_bsc(BscArgs a) {
                     fixed = true;
                     uint32_t p1[4], p2[4];
                     table_asm2(p1, p2, m1, m2, k);
-                    if (cdeg > 0 && cj == 0) {
+                    if (cdeg > 0 && cjl == 0) {
                         lds_qput(grec[c], p1);
                         lds_qput(grec[c] + REC_Q2, p2);
                     }
                 }
             }
-            uint32_t qb[OB][2];
+            uint32_t qb[OBL][2];
             if (!fixed) {
                 const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
                 const uint32_t tab = gtab[c] + (uint32_t)((t & 1) * AL * 4);
 #pragma unroll
-                for (int b = 0; b < OB; ++b) {
+                for (int b = 0; b < OBL; ++b) {
                     uint32_t o[2];
                     lut_bit<2>(o, mm, tab + (uint32_t)(b * 64));
                     qb[b][0] = o[0];
                     qb[b][1] = o[1];
                 }
             }
-            // the record: lane j writes planes OB j .. of q1 and q2 (the whole group has read the
+            // the record: lane j writes planes OBL j .. of q1 and q2 (the whole group has read the
             // old record above: same wave, LDS operations in program order); idle lanes past
             // the last check (degree 0) share its clamped record address and must not write
             if (!fixed && cdeg > 0) {
 #pragma unroll
-                for (int b = 0; b < OB; ++b) {
-                    lds_put(grec[c] + 4u * (uint32_t)(OB * cj + b), qb[b][0]);
-                    lds_put(grec[c] + REC_Q2 + 4u * (uint32_t)(OB * cj + b), qb[b][1]);
+                for (int b = 0; b < OBL; ++b) {
+                    lds_put(grec[c] + 4u * (uint32_t)(OBL * cjl + b), qb[b][0]);
+                    lds_put(grec[c] + REC_Q2 + 4u * (uint32_t)(OBL * cjl + b), qb[b][1]);
                 }
             }
             // per edge: the C->V sign (par ^ own V->C sign, :251-254) and [|V->C| == min]
@@ -511,6 +534,9 @@ k_bsc(BscArgs a) {
                     lds_put(sa + a.off_a, ~ne);
                 }
             }
+                    };
+            if (!MIX || gl4[c]) chunk(std::integral_constant<int, LPC>{});
+            else if constexpr (MIX) chunk(std::integral_constant<int, LPC / 2>{});
         }
         __syncthreads();
         // ======== variable nodes ================================================================
@@ -554,6 +580,10 @@ namespace ldpc {
 namespace bs {
 
 std::vector<int32_t> slot_layout(const host::GraphTables& h, int LPC, size_t* nslot);
+std::vector<int32_t> slot_layout_rows(const host::GraphTables& h, const std::vector<int>& rl, size_t* nslot);
+std::vector<int32_t> uniform_lanes(const host::GraphTables& h, int LPC, int cn_lanes);
+std::vector<int> check_chunk_cost_lanes(const host::GraphTables& h, const std::vector<int32_t>& lanes);
+std::vector<int> column_rotation_lanes(const host::GraphTables& h, int EPL, const std::vector<int32_t>& lanes);
 std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap);
 std::vector<int> check_chunk_cost(const host::GraphTables& h, int LPC, int cch);
 std::vector<int> column_rotation(const host::GraphTables& h, int LPC, int EPL, int cn_lanes);
@@ -578,6 +608,8 @@ struct BscPlan {
     size_t lds = 0;
     std::vector<int32_t> lay;
     std::vector<int> vorder, vslot;      // variables by degree; chunk of each (wave, u) place
+    std::vector<int> rl;                 // lanes per check of each row
+    std::vector<int32_t> lanes;          // check lane -> check | lane << 16 | lanes per check << 20, -1 idle
 };
 
 static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T) {
@@ -595,7 +627,20 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
     const int want_lpc = el ? atoi(el) : 0;
     const char* ei = getenv("LDPC_BSC_INST");        // A/B: force one instance (if it fits)
     const int want_inst = ei ? atoi(ei) : -1;
-    for (int i = 0; i < kBscNInst; ++i) {
+    // LDPC_BSC_MIX=1: the mixed-lane instances first (fewest check chunks per wave first).  Off
+    // by default: on C5 they issue 7 % fewer VALU instructions (35.98 G against 38.68 G per
+    // launch) in the same time (56.24-56.43 against 56.34 ms, same box, r3w; PMC r3 mixprof) —
+    // the check phase there is bound by latency at four waves per SIMD, not by issue
+    const char* em = getenv("LDPC_BSC_MIX");
+    const bool mix = em && atoi(em) != 0;
+    std::vector<int> order(kBscNInst);
+    for (int i = 0; i < kBscNInst; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+        const int kx = kBscInst[x].MIX == mix ? 0 : 1, ky = kBscInst[y].MIX == mix ? 0 : 1;
+        if (kx != ky) return kx < ky;
+        return kBscInst[x].MIX && kBscInst[x].CPL < kBscInst[y].CPL;
+    });
+    for (const int i : order) {
         const BscInst& k = kBscInst[i];
         if (h.max_cdeg > k.D || h.max_vdeg > k.DVH) continue;
         if (want_lpc != 0 && want_lpc != k.LPC) continue;
@@ -604,7 +649,27 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
         BscPlan q;
         q.inst = i;
         q.nw = k.NW;
-        q.cn_lanes = 64 * ((k.LPC * nc + 63) / 64);
+        // rows and check lanes: MIX instances give the rows of degree <= LPC / 2 * EPL half the
+        // lanes, in 64-lane chunks of their own after the full-width rows' chunks
+        const int EPLk = (k.D + k.LPC - 1) / k.LPC;
+        q.rl.assign((size_t)h.M, k.LPC);
+        if (k.MIX)
+            for (int i = 0; i < h.M; ++i)
+                if (h.row_ptr[i + 1] - h.row_ptr[i] <= k.LPC / 2 * EPLk) q.rl[(size_t)i] = k.LPC / 2;
+        if (k.MIX) {
+            for (const int L : {k.LPC, k.LPC / 2}) {
+                for (int i = 0; i < h.M; ++i) {
+                    if (q.rl[(size_t)i] != L) continue;
+                    for (int hc = 0; hc < z; ++hc)
+                        for (int j = 0; j < L; ++j) q.lanes.push_back((i * z + hc) | (j << 16) | (L << 20));
+                }
+                while (q.lanes.size() % 64) q.lanes.push_back(-1);
+            }
+            q.cn_lanes = (int)q.lanes.size();
+        } else {
+            q.cn_lanes = 64 * ((k.LPC * nc + 63) / 64);
+            q.lanes = uniform_lanes(h, k.LPC, q.cn_lanes);
+        }
         const int vch = (nv + 63) / 64, cch = q.cn_lanes / 64;
         if (k.VPL == 1 && k.CPL == 1) q.nw = std::max(vch, cch);
         if (q.nw > 16 || vch > k.VPL * q.nw || cch > k.CPL * q.nw) continue;
@@ -627,10 +692,10 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
         if (!fits) continue;
         q.arows = g.w_alpha_uniform ? 1 : h.M;
         q.bcols = g.w_beta_uniform ? 1 : h.N;
-        q.cn_dmin = (q.cn_lanes == k.LPC * nc) ? min_cdeg : 0;
+        q.cn_dmin = (!k.MIX && q.cn_lanes == k.LPC * nc) ? min_cdeg : 0;
         const float cu = clip / bs_step(mode);
         q.cu = cu > (float)bs_qmax(mode) ? cu : -1.f;
-        q.lay = slot_layout(h, k.LPC, &q.nslot);
+        q.lay = slot_layout_rows(h, q.rl, &q.nslot);
         // LDS: SGN [nslot + 1] | ARG [nslot + 1] | REC [(nc + 1) / 16 blocks][2][16][4] | TV [nv][6] |
         // RED | ALUT | BLUT
         const size_t sgn = ((q.nslot + 1) * 4 + 127) & ~(size_t)127;
@@ -670,7 +735,8 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     const int VNW = k.DVH + 1, EPL = (k.D + LPC - 1) / LPC, CVW = (EPL + 1) / 2;
     const int NWp = p.nw, nl = 64 * NWp;
     auto slot_of = [&](int i, int kk, int hc) {
-        return (uint32_t)((size_t)p.lay[2 * i] + (size_t)(kk % LPC) * p.lay[2 * i + 1] + (size_t)(kk / LPC) * z + hc);
+        const int L = p.rl[(size_t)i];
+        return (uint32_t)((size_t)p.lay[2 * i] + (size_t)(kk % L) * p.lay[2 * i + 1] + (size_t)(kk / L) * z + hc);
     };
     // Tv slots: variable (column j, index hh) keeps its Tv at j z + (hh + toff_j) mod z.  The
     // check phase reads the Tv of each lane's edge m (ds_read_b64, bank = dword mod 64, 6 dwords
@@ -681,7 +747,7 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     // check pass in tools/bank_model's terms); the variable phase writes the same slot.
     const char* etv = getenv("LDPC_BSC_TVPERM");
     const std::vector<int> toff = (etv && atoi(etv) == 0) ? std::vector<int>(h.N, 0)
-                                                           : column_rotation(h, LPC, EPL, p.cn_lanes);
+                                                           : column_rotation_lanes(h, EPL, p.lanes);
     auto tv_index = [&](int v) -> uint32_t {
         const int j = v / z, hh = v - j * z;
         return (uint32_t)(j * z + (hh + toff[j]) % z);
@@ -723,23 +789,24 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     if (k.CPL == 1 && k.VPL == 1) {
         for (int w = 0; w < NWp; ++w) cchunk[w] = w < cch ? w : -1;
     } else {
-        const std::vector<int> cs = deal_chunks(check_chunk_cost(h, LPC, cch), NWp, k.CPL);
+        const std::vector<int> cs = deal_chunks(check_chunk_cost_lanes(h, p.lanes), NWp, k.CPL);
         for (size_t x = 0; x < cs.size(); ++x) cchunk[x] = cs[x];
     }
     std::vector<uint32_t> cvar((size_t)p.cn_lanes * CVW, 0u);
     for (int ql = 0; ql < p.cn_lanes; ++ql) {
-        const int cc = ql / LPC, cj = ql % LPC;
-        if (cc >= nc) continue;
+        const int32_t dl = p.lanes[(size_t)ql];
+        if (dl < 0) continue;
+        const int cc = dl & 0xFFFF, cj = (dl >> 16) & 15, L = (dl >> 20) & 15;
         const int i = cc / z, hc = cc - i * z;
         for (int m = 0; m < EPL; ++m) {
-            const int kk = LPC * m + cj;
+            const int kk = L * m + cj;
             if (kk >= h.row_ptr[i + 1] - h.row_ptr[i]) continue;
             const int pe = h.row_ptr[i] + kk;
             const uint32_t v = tv_index(h.pe_col[pe] * z + (hc + h.pe_shift[pe]) % z);
             cvar[(size_t)ql * CVW + (m >> 1)] |= v << (16 * (m & 1));
         }
     }
-    const size_t nwords = vn.size() + wdeg.size() + p.lay.size() + cchunk.size() + cvar.size();
+    const size_t nwords = vn.size() + wdeg.size() + p.lay.size() + cchunk.size() + cvar.size() + p.lanes.size();
     void* d = nullptr;
     if (hipMalloc(&d, nwords * 4) != hipSuccess) { (void)hipGetLastError(); return LDPC_ERR_OOM; }
     uint32_t* dp = reinterpret_cast<uint32_t*>(d);
@@ -754,6 +821,7 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     up(p.lay.data(), p.lay.size());
     up(cchunk.data(), cchunk.size());
     up(cvar.data(), cvar.size());
+    up(p.lanes.data(), p.lanes.size());
     if (!ok || hipStreamSynchronize(s) != hipSuccess) {
         (void)hipFree(d);
         return LDPC_ERR_HIP;
@@ -766,7 +834,7 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
 template <int I, bool XP>
 static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     constexpr BscInst k = kBscInst[I];
-    auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE, XP, 64 * k.NW>;
+    auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE, XP, 64 * k.NW, k.MIX>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -790,8 +858,8 @@ const char* bsc_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge
     const BscPlan p = bsc_plan(g, mode, ucn, per_edge_w, clip, T);
     if (!p.ok) return "";
     const BscInst& k = kBscInst[p.inst];
-    snprintf(buf, sizeof(buf), "bsc[p32,w%d,d%d,v%d/%d,l%d,x%d/%d]", p.nw, k.D, k.DVH, k.DVL, k.LPC,
-             k.VPL, k.CPL);
+    snprintf(buf, sizeof(buf), "bsc[p32,w%d,d%d,v%d/%d,l%d%s,x%d/%d]", p.nw, k.D, k.DVH, k.DVL, k.LPC,
+             k.MIX ? "/2" : "", k.VPL, k.CPL);
     return buf;
 }
 
@@ -829,6 +897,7 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     a.row_lay = a.vn_wdeg + 2 * (size_t)k.VPL * p.nw;
     a.cn_chunk = a.row_lay + 2 * (size_t)g.M;
     a.cn_var = reinterpret_cast<const uint32_t*>(a.cn_chunk + (size_t)p.nw * k.CPL);
+    a.cn_lane = reinterpret_cast<const int32_t*>(a.cn_var + (size_t)p.cn_lanes * ((((k.D + k.LPC - 1) / k.LPC) + 1) / 2));
     bs_stagger(true, &a.stagger, &a.stagger_n);
     a.alut = alut;
     a.atid = (p.arows == 1 && !getenv("LDPC_BS_NOAFIX")) ? atid : nullptr;
@@ -850,6 +919,8 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     switch (p.inst) {
         case 1: return hdx ? bsc_launch<1, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<1, false>(a, nblocks, p.nw, p.lds, s);
         case 2: return hdx ? bsc_launch<2, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<2, false>(a, nblocks, p.nw, p.lds, s);
+        case 3: return hdx ? bsc_launch<3, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<3, false>(a, nblocks, p.nw, p.lds, s);
+        case 4: return hdx ? bsc_launch<4, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<4, false>(a, nblocks, p.nw, p.lds, s);
         default: return hdx ? bsc_launch<0, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<0, false>(a, nblocks, p.nw, p.lds, s);
     }
 }

@@ -235,15 +235,18 @@ def test_bitsliced_q_minus5_large_graphs(cuda_device, cfg):
     assert np.array_equal(out["fused"][1], out["flood"][1])
 
 
-@pytest.mark.parametrize("lpc_c", ["4", "2"])
+@pytest.mark.parametrize("lpc_c", ["4", "2", "4/2"])
 def test_bitsliced_compressed_idle_check_lanes(cuda_device, lpc_c, monkeypatch):
     """bsc with a last check chunk that is only partly used (BG1 lifted by z = 60: 600 checks,
-    4 x 600 lanes = 37.5 chunks), where the idle lanes share the last check's record address."""
+    4 x 600 lanes = 37.5 chunks), where the idle lanes share the last check's record address;
+    "4/2": the mixed-lane instance (rows of degree <= 10 at two lanes per check, in chunks of
+    their own after the degree-19 rows' chunks, both segments ending in idle lanes)."""
     import bench
     from ldpc_error_floor_amd.code import TannerGraph
     from ldpc_error_floor_amd.decoder import NMSDecoder
     from ldpc_error_floor_amd.weights import flat_weights
-    monkeypatch.setenv("LDPC_BS_LPC", lpc_c)
+    monkeypatch.setenv("LDPC_BS_LPC", lpc_c.split("/")[0])
+    monkeypatch.setenv("LDPC_BSC_MIX", "1" if "/" in lpc_c else "0")
     proto = bench.load_problem(T=10, config="C5")[0]
     g = TannerGraph(proto, 60)
     dec = NMSDecoder(proto, 60, flat_weights(g, 10, alpha=0.75, beta=1.0), 2, 5, device=cuda_device)
