@@ -107,7 +107,10 @@ __device__ __forceinline__ void lds_dput(uint32_t addr, uint32_t x, uint32_t y) 
     *reinterpret_cast<LdsD*>(addr) = v;
 }
 
-template <int D, int DVH, int DVL, int LPC, int VPL, int CPL, int WPE, bool XP, int LB, bool MIX>
+// B1: every beta is 1 and one column table (a.beta_id, bcols 1: C5's flat weights), so the
+// channel term is Q(ch) itself and neither the beta table's operands nor the shortened-bit
+// planes are live (C5's instance: 124 VGPRs, no spills, against 128 and 10 spilled)
+template <int D, int DVH, int DVL, int LPC, int VPL, int CPL, int WPE, bool XP, int LB, bool MIX, bool B1>
 __global__ void __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_bsc(BscArgs a) {
     constexpr int SB = (DVH * QMAX + QMAX <= 127) ? 8 : 9;
@@ -143,7 +146,7 @@ k_bsc(BscArgs a) {
         vv[u] = (int)vt[DVH];                                // v | Tv index << 16, or -1
         dw[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave)]);
         dwmin[u] = __builtin_amdgcn_readfirstlane(a.vn_wdeg[2 * (u * nwv + wave) + 1]);
-        tab_b[u] = (a.bcols > 1 && vv[u] >= 0) ? (uint32_t)(((vv[u] & 0xFFFF) / (nv / a.bcols)) * BLUT_W * 4) : 0u;
+        tab_b[u] = (!B1 && a.bcols > 1 && vv[u] >= 0) ? (uint32_t)(((vv[u] & 0xFFFF) / (nv / a.bcols)) * BLUT_W * 4) : 0u;
     }
     (void)dwmin;
 
@@ -229,7 +232,7 @@ k_bsc(BscArgs a) {
             const bool counted = v >= 0 && v < a.target_bits;
             uint32_t lw[1][4];
             if (!last) {
-                if (a.beta_id) {
+                if (B1 || a.beta_id) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) lw[0][i] = cm[u][i];
                 } else if (a.bcols == 1) {
@@ -831,10 +834,10 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     return LDPC_OK;
 }
 
-template <int I, bool XP>
-static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
+template <int I, bool XP, bool B1>
+static int bsc_launch1(const BscArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     constexpr BscInst k = kBscInst[I];
-    auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE, XP, 64 * k.NW, k.MIX>;
+    auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE, XP, 64 * k.NW, k.MIX, B1>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -843,6 +846,13 @@ static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStre
     }
     hipLaunchKernelGGL(fn, dim3(nblocks), dim3(64 * nw), lds, s, a);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+}
+template <int I, bool XP>
+static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
+    // (LDPC_BSC_B1=0: the general channel path for a B1 decode too, an A/B switch)
+    static const bool b1_on = [] { const char* e = getenv("LDPC_BSC_B1"); return !(e && atoi(e) == 0); }();
+    if (b1_on && a.beta_id && a.bcols == 1) return bsc_launch1<I, XP, true>(a, nblocks, nw, lds, s);
+    return bsc_launch1<I, XP, false>(a, nblocks, nw, lds, s);
 }
 
 }  // namespace bs
