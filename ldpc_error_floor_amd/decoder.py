@@ -184,6 +184,12 @@ class NMSDecoder:
                          ptr(res.flags), stream.cuda_stream, ptr(res.iter_wrong))
         return res
 
+    def generates_channel_in_kernel(self, T=None, kernel=None) -> bool:
+        """Whether ``decode_awgn`` generates the LLRs inside the decoding kernel (the fused v5
+        kernel's prologue); otherwise ``ldpc_decode_awgn`` runs the channel kernel into HBM and
+        then the decoder (the bit-sliced kernels, flood, ffl)."""
+        return self.kernel_info(T, kernel)[1].startswith("fused5")
+
     def last_kernel(self) -> str:
         """The kernel that served this decoder's last decode (``ldpc_ctx_last_kernel``)."""
         return "" if self._ctx is None else self._ext.last_kernel(self._ctx)

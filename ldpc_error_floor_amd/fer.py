@@ -138,7 +138,7 @@ def decoder_fingerprint(decoder, T=None):
 def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T=None,
               punct=None, short=None, kernel=None, group=None, progress=None,
               uncor_path=None, checkpoint=None, checkpoint_every: int = 64,
-              resume: bool = False, point_seeds=None):
+              resume: bool = False, point_seeds=None, overlap: bool = False):
     """Decode ``n_codewords`` per SNR point (split across ranks) with GPU LLRs and device
     counters.  Returns a list of ``Counters`` (global totals on every rank).
 
@@ -155,7 +155,15 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
 
     ``checkpoint``: path of this sweep's checkpoint (``<path>.rank<r>`` with several ranks),
     written every ``checkpoint_every`` batches and after every SNR point; ``resume=True``
-    continues from it (a missing file starts from the beginning)."""
+    continues from it (a missing file starts from the beginning).
+
+    ``overlap``: when the decoding kernel reads its LLRs from HBM (the bit-sliced kernels: the
+    channel is a kernel of its own), generate batch j + 1 on a second stream while batch j
+    decodes (``pipelined_channel_decode``); the counters are the same either way.  Off by
+    default: measured on one MI355X (``tools/overlap_probe.py``, ``profiles/r3/overlap``), it
+    gained nothing (C2 6.36 against 6.29 ms per 2^20-codeword step, C4 / C5 equal, C3 1.6 %
+    slower) — the channel kernel is VALU-bound too and finds no idle issue slots beside the
+    decode's waves."""
     import torch
     import torch.distributed as dist
     dist_on = dist.is_available() and dist.is_initialized()
@@ -205,6 +213,29 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
         ub = (os.path.getsize(upath) if upath and os.path.exists(upath) else 0) if upath else None
         ck.save(key, si, pos, counters.cpu().tolist(), ub, done)
 
+    if fused_channel and overlap and _pipelines(decoder, T, kernel):
+        # the channel of batch j + 1 on a second stream while batch j decodes (the decoder reads
+        # its LLRs from HBM, so ldpc_decode_awgn would run the two kernels back to back)
+        jobs = [(si, pos, min(batch, end - pos)) for si in range(si0, sigmas.size)
+                for pos in range(pos0 if si == si0 else begin, end, batch)]
+        nbs = {}
+
+        def done(j, si, pos, b):
+            nbs[si] = nbs.get(si, 0) + 1
+            if ck is not None and checkpoint_every > 0 and nbs[si] % checkpoint_every == 0 and pos + b < end:
+                save(si, pos + b)
+            if progress:
+                progress(si, pos + b - begin, end - begin)
+            if pos + b >= end and ck is not None:
+                save(si + 1, begin, done=(si + 1 == sigmas.size))
+
+        pipelined_channel_decode(decoder, jobs, lambda si: (float(sigmas[si]), point_seeds[si]),
+                                 lambda si: counters[si], T=T, kernel=kernel, punct=punct,
+                                 short=short, on_done=done)
+        for si in range(si0, sigmas.size):          # points with no codewords on this rank
+            if ck is not None and si not in nbs:
+                save(si + 1, begin, done=(si + 1 == sigmas.size))
+        si0 = sigmas.size
     for si, sigma in enumerate(sigmas):
         if si < si0:
             continue
@@ -239,6 +270,68 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
     host = counters.cpu().numpy()
     return [Counters.from_array(host[i], int(n_codewords), decoder.n_vars)
             for i in range(sigmas.size)]
+
+
+def _pipelines(decoder, T, kernel) -> bool:
+    """Whether ``decoder`` runs on a GPU and ``ldpc_decode_awgn`` would generate its LLRs with
+    the channel kernel into HBM (every kernel but the fused v5, which generates in its
+    prologue)."""
+    dev = getattr(decoder, "device", None)
+    if getattr(dev, "type", None) != "cuda" or not hasattr(decoder, "generates_channel_in_kernel"):
+        return False
+    return not decoder.generates_channel_in_kernel(T, kernel)
+
+
+def pipelined_channel_decode(decoder, jobs, point, cnt, T=None, kernel=None, punct=None,
+                             short=None, on_done=None):
+    """Decode a sequence of on-GPU channel batches, the channel of batch j + 1 generated on a
+    second stream while batch j decodes on the current stream (two LLR buffers; an event orders
+    each buffer's next generation after the decode that read it).  The codewords and counters are
+    those of ``decoder.decode_awgn`` batch by batch (``ldpc_channel_awgn`` + ``ldpc_decode``).
+
+    ``jobs``: (si, pos, b) = SNR point, global offset of the batch's first codeword, batch size;
+    ``point(si)`` -> (sigma, Philox seed); ``cnt(si)`` -> the int64[4] device counters of point
+    si; ``on_done(j, si, pos, b)`` runs on the host after decode j is queued."""
+    import torch
+    jobs = list(jobs)
+    if not jobs:
+        return
+    dev = decoder.device
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    bmax = max(b for _, _, b in jobs)
+    bufs = [torch.empty((bmax, decoder.n_vars), dtype=torch.float32, device=dev) for _ in range(2)]
+    gen_ev, dec_ev = [None, None], [None, None]
+
+    def gen(j):
+        si, pos, b = jobs[j]
+        k = j % 2
+        sigma, seed = point(si)
+        if dec_ev[k] is None:
+            side.wait_stream(main)            # a fresh buffer: after the main stream's earlier work
+        else:
+            side.wait_event(dec_ev[k])        # after the decode that read this buffer
+        decoder.awgn(b, sigma, seed, offset=pos, punct=punct, short=short, out=bufs[k][:b],
+                     stream=side)
+        gen_ev[k] = torch.cuda.Event()
+        gen_ev[k].record(side)
+
+    try:
+        gen(0)
+        for j, (si, pos, b) in enumerate(jobs):
+            if j + 1 < len(jobs):
+                gen(j + 1)
+            k = j % 2
+            main.wait_event(gen_ev[k])
+            decoder.decode(bufs[k][:b], T=T, app=False, counters=cnt(si), kernel=kernel, stream=main)
+            dec_ev[k] = torch.cuda.Event()
+            dec_ev[k].record(main)
+            if on_done:
+                on_done(j, si, pos, b)
+    finally:
+        # (also when on_done raises): the buffers return to the main stream's pool only after
+        # every generation queued on the side stream
+        main.wait_stream(side)
 
 
 def collect_uncor_inputs(decoder, sigma, filename, counts=(10000, 5000, 5000), out_dir="Inputs",

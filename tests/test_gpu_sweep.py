@@ -84,6 +84,26 @@ def test_sweep_resume_on_gpu(cuda_device, tmp_path):
     assert key(res) == key(full)
 
 
+@pytest.mark.parametrize("cfg", ["C2", "C5"])
+def test_sweep_overlapped_channel_equals_inline(cuda_device, cfg):
+    """fer_sweep's pipelined path (batch j + 1's channel kernel on a second stream while batch j
+    decodes, for the kernels that read their LLRs from HBM) decodes exactly the codewords of the
+    in-line path: several SNR points and a ragged last batch."""
+    import bench
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    from ldpc_error_floor_amd.fer import fer_sweep, _pipelines
+    c = bench.CONFIGS[cfg]
+    proto, g, W, cp = bench.load_problem(T=12, config=cfg)
+    dec = NMSDecoder(proto, c["z"], W, 2, 5, device=cuda_device)
+    dec.punct, dec.short = c.get("punct", (0, 0)), c.get("short", (0, 0))
+    assert _pipelines(dec, None, None) and dec.kernel_info()[1].startswith(("bsl[", "bsc["))
+    sig = [float(cp.sigma(c["snr"] - 1.0)), float(cp.sigma(c["snr"] - 0.5))]
+    key = lambda rs: [(r.bit_err_last, r.frame_err_last, r.frame_err_all, r.loss2) for r in rs]  # noqa: E731
+    inline = key(fer_sweep(dec, sig, 9000, 2048, seed=4))
+    assert key(fer_sweep(dec, sig, 9000, 2048, seed=4, overlap=True)) == inline
+    assert inline[0][1] > 0
+
+
 def test_off_grid_clip_selects_flood(cuda_device):
     """clip_LLR = 19.7 is not a multiple of the q=5 step: the fused kernel cannot clip in its
     integer domain, so AUTO must pick flood (and 'fused' is reported unsupported)."""
