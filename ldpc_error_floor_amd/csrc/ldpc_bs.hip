@@ -89,10 +89,24 @@ struct BsPlan {
              off_btid = 0, off_ch = 0;
     int cn_dmin = 0;
     bool ucn = false;
+    bool colalign = false;         // variable lanes: each column on a half-wave of its own
     float cu = 0.f;
     size_t lds = 0;
     std::vector<int32_t> lay;      // [M][2] first slot of proto row i, stride A_i of its j-blocks
 };
+
+// Column-aligned variable lanes (the one-chunk instances, z <= 32): the variables of each column
+// start a 32-lane half-wave of their own (32 - z idle lanes after them).  Edge f of the z
+// variables of one column reads the slots first + (k mod LPC) A + (k div LPC) z + (hh - shift)
+// mod z: z consecutive slots, distinct mod 32, so every half-wave slot read of the variable phase
+// is free of bank conflicts; packed, a half-wave holds the tail of one column and the head of
+// the next, whose runs overlap mod 32 (802.11n, z = 27: 143 bank cycles per slot word in the
+// bank model against a floor of 78, tools/bank_model.py).  Taken when it costs at most one more
+// wave than the packed lanes (802.11n: 12 waves against 11; wman, z = 24, would need 12 against
+// 9).  LDPC_BS_COLALIGN=0/1 forces it off / on where it fits.
+static bool colalign_fits(const host::GraphTables& h, int nw_packed) {
+    return h.z <= 32 && 32 * h.N <= 64 * 16 && (32 * h.N + 63) / 64 <= nw_packed + 1;
+}
 
 // Slot layout: edge k of check (row i, index h) is slot first_i + (k mod LPC) A_i +
 // (k div LPC) z + h.  LDS banking (MI355X_MICROARCH.md, LDS): ds_read_b32 / ds_read2_b32 /
@@ -153,7 +167,13 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     p.ucn = ucn;
     const int nv = g.n_vars, nc = g.n_checks;
     p.cn_lanes = 64 * ((k.LPC * nc + 63) / 64);
-    const int vch = (nv + 63) / 64, cch = p.cn_lanes / 64;
+    int vch = (nv + 63) / 64;
+    const int cch = p.cn_lanes / 64;
+    if (k.VPL == 1 && k.CPL == 1) {
+        static const int eca = [] { const char* e = getenv("LDPC_BS_COLALIGN"); return e ? atoi(e) : BS_COLALIGN; }();
+        p.colalign = eca != 0 && colalign_fits(h, std::max(vch, cch));
+        if (p.colalign) vch = (32 * h.N + 63) / 64;
+    }
     if (k.VPL == 1 && k.CPL == 1) p.nw = std::max(vch, cch);
     else p.nw = std::max((vch + k.VPL - 1) / k.VPL, (cch + k.CPL - 1) / k.CPL);
     if (p.nw > 16) return p;                       // 1024-lane workgroup
@@ -503,7 +523,16 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
     for (int v = 0; v < nv; ++v) order[v] = v;
     auto vdeg = [&](int v) { const int j = v / z; return h.col_ptr[j + 1] - h.col_ptr[j]; };
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return vdeg(x) > vdeg(y); });
-    const int nch = (nv + 63) / 64;
+    if (p.colalign) {               // each column's z variables, then 32 - z idle lanes (-1)
+        std::vector<int> pad;
+        for (int o = 0; o < nv; o += z) {
+            pad.insert(pad.end(), order.begin() + o, order.begin() + o + z);
+            pad.insert(pad.end(), (size_t)(32 - z), -1);
+        }
+        order.swap(pad);
+    }
+    const int nvo = (int)order.size();
+    const int nch = (nvo + 63) / 64;
     std::vector<int> vcost(nch);
     for (int ch = 0; ch < nch; ++ch) vcost[ch] = 3 + vdeg(order[64 * ch]);
     const std::vector<int> vslot = deal_chunks(vcost, p.nw, k.VPL);
@@ -543,7 +572,7 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
             std::fill(dl.begin(), dl.end(), 0);
             for (int l = 0; l < 64; ++l) {
                 const int o = 64 * ch + l;
-                if (o >= nv) { dmin = 0; continue; }
+                if (o >= nvo || order[o] < 0) { dmin = 0; continue; }
                 const int v = order[o], j = v / z, hh = v - j * z;
                 col = (col == -2 || col == j) ? j : -1;
                 const int c0 = h.col_ptr[j], dv = h.col_ptr[j + 1] - c0;
@@ -564,7 +593,7 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
             }
             for (int l = 0; l < 64; ++l) {
                 const int o = 64 * ch + l;
-                if (o >= nv) continue;
+                if (o >= nvo || order[o] < 0) continue;
                 uint32_t* q = &vn[((size_t)u * nl + 64 * w + l) * VNW];
                 for (int pw = 0; pw < VNA; ++pw) q[pw] = 0u;
                 for (int f = 0; f < DV; ++f) put(q, f, A[(size_t)l * DV + f]);

@@ -564,6 +564,10 @@ __device__ __forceinline__ int pack_channel(const float (&xv)[PACK], float inv, 
 #ifndef BS_STAGGER_US
 #define BS_STAGGER_US 0.0
 #endif
+// column-aligned variable lanes (ldpc_bs.hip, colalign_fits): 1 on where it fits
+#ifndef BS_COLALIGN
+#define BS_COLALIGN 1
+#endif
 // (A/B switch, off: C3 spill-free at 72 VGPRs with it, and slower: 17.37 against 16.07 ms on one
 // box, r3q — pass 2 then waits on its LDS reads, where the spills it removes were reloaded once
 // per iteration)
