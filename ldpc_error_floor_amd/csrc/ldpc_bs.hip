@@ -216,6 +216,7 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     o += (size_t)2 * (k.UCN ? 2 : 1) * p.arows * LUT_W * 4;
     p.off_blut = (uint32_t)o;
     o += (size_t)2 * p.bcols * BLUT_W * 4;
+    if (k.PK && k.CPL == 1 && o > 65535) return p;  // 16-bit alpha-table addresses (BS_PKG)
     p.off_btid = (uint32_t)o;                      // the next iteration's channel-table ids
     o += ((size_t)4 * p.bcols + 15) & ~(size_t)15;
     if (BS_CH_LDS) {                               // the channel planes, 16 B per (lane, variable)

@@ -564,6 +564,11 @@ __device__ __forceinline__ int pack_channel(const float (&xv)[PACK], float inv, 
 #ifndef BS_STAGGER_US
 #define BS_STAGGER_US 0.0
 #endif
+// the check lane's slot base and alpha-table address packed in one register (16-bit-address
+// one-chunk instances; ldpc_bs.hip checks that the tables end below 64 KB)
+#ifndef BS_PKG
+#define BS_PKG 1
+#endif
 // column-aligned variable lanes (ldpc_bs.hip, colalign_fits): 1 on where it fits
 #ifndef BS_COLALIGN
 #define BS_COLALIGN 1
@@ -624,6 +629,7 @@ k_bs(BsArgs a) {
     constexpr int VNA = PK ? (DV + 1) / 2 : DV;                  // address words per variable
     constexpr int VNW = VNA + 1;
     constexpr int HDW = (EPL + 1) / 2;                           // packed hd addresses per check lane
+    constexpr bool PKG = PK && CPL == 1 && BS_PKG;               // slot base | alpha table << 16
     // pass 2 reads its slots again instead of holding all EPL of them from pass 1 (wide checks:
     // 30 registers at the check phase's peak, where the 80-register C3 build spilled)
     constexpr bool RR = BS_REREAD && EPL >= 6;
@@ -1010,6 +1016,9 @@ k_bs(BsArgs a) {
         gm[c] = SKIPM ? (int)__popc(wave_or((1u << ((gdeg[c] + LPC - 1) / LPC)) - 1u)) : EPL;
         gbase[c] = a.off_slots + (uint32_t)((a.row_lay[2 * ci] + cj * a.row_lay[2 * ci + 1] + (cc - ci * a.z)) * SLOT_B);
         gtab[c] = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cj * OB * 64);
+        // (16-bit LDS addresses: the slot base and the alpha-table address share one register
+        // through the T loop, unpacked per iteration)
+        if constexpr (PKG) gbase[c] |= gtab[c] << 16;
         {
             const int ch = max(gchunk[c], 0), mr = a.n_checks / a.z - 1;
             const int c0 = ch * (64 / LPC);
@@ -1076,6 +1085,8 @@ k_bs(BsArgs a) {
             if (!active || ABL(1)) continue;
             uint32_t cbase = gbase[c];
             asm volatile("" : "+v"(cbase));
+            uint32_t ctab = PKG ? (cbase >> 16) : gtab[c];
+            if constexpr (PKG) cbase &= 0xFFFFu;
             const int cdeg = gdeg[c];
             int gmc = gm[c];
             asm volatile("" : "+s"(gmc));
@@ -1171,7 +1182,7 @@ k_bs(BsArgs a) {
             uint32_t q1[4], q2[4];
             {
                 const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
-                const uint32_t tab = gtab[c] + (uint32_t)((t & 1) * AL * 4);
+                const uint32_t tab = ctab + (uint32_t)((t & 1) * AL * 4);
                 uint32_t qb[OB][2];
                 // alpha' is needed only where a check is unsatisfied for some codeword: a wave
                 // whose checks are all satisfied in all 32 codewords (most waves once the
