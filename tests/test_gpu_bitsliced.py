@@ -125,6 +125,10 @@ def test_bitsliced_large_and_ucn(cuda_device, cfg, T, B, lpc, monkeypatch):
     dec, cp, c = _config(cuda_device, cfg, T)
     name = dec.kernel_info()[1]
     assert name.startswith("bsl") and ",ucn" in name, name
+    if cfg == "C3":
+        # 802.11n (z = 27): column-aligned variable lanes, each column on a half-wave of its own
+        # (648 variables on 12 waves instead of 11 packed ones; ldpc_bs.hip colalign_fits)
+        assert name.startswith("bsl[p32,w12,"), name
     llr = dec.awgn(B, float(cp.sigma(c["snr"] - 0.75)), seed=5, offset=77)
     out = _both(dec, llr)
     assert np.array_equal(out["fused"][0], out["flood"][0]), (out["fused"][0], out["flood"][0])
