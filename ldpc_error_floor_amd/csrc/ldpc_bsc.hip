@@ -630,12 +630,14 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
     const int want_lpc = el ? atoi(el) : 0;
     const char* ei = getenv("LDPC_BSC_INST");        // A/B: force one instance (if it fits)
     const int want_inst = ei ? atoi(ei) : -1;
-    // LDPC_BSC_MIX=1: the mixed-lane instances first (fewest check chunks per wave first).  Off
-    // by default: on C5 they issue 7 % fewer VALU instructions (35.98 G against 38.68 G per
-    // launch) in the same time (56.24-56.43 against 56.34 ms, same box, r3w; PMC r3 mixprof) —
-    // the check phase there is bound by latency at four waves per SIMD, not by issue
+    // the mixed-lane instances first (fewest check chunks per wave first) when the decode takes
+    // the beta = 1 build (every beta 1, one column table: bsc_launch's B1), where they run without
+    // spills: C5 53.86 -> 52.44 ms (r3zd).  With a beta table they spill 11-19 VGPRs and issue 7 %
+    // fewer VALU instructions in the same time as the uniform ones (56.24-56.43 against 56.34 ms,
+    // r3w; PMC r3 mixprof): the uniform instances stay the default there.  LDPC_BSC_MIX=0/1
+    // forces either.
     const char* em = getenv("LDPC_BSC_MIX");
-    const bool mix = em && atoi(em) != 0;
+    const bool mix = em ? atoi(em) != 0 : (g.w_beta_one && g.w_beta_uniform);
     std::vector<int> order(kBscNInst);
     for (int i = 0; i < kBscNInst; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
