@@ -561,8 +561,10 @@ __device__ __forceinline__ int pack_channel(const float (&xv)[PACK], float inv, 
 #endif
 
 // first-generation start spread of the one-workgroup-per-CU instances, microseconds (bs_stagger)
+// (bsl's one-workgroup-per-CU instances: 5G BG2 (C4) 13.93 -> 13.78 ms at 100 us, 50 / 200 us
+// in between, same box, r3ze; bsc: no effect, so it passes one_per_cu = false and starts at 0)
 #ifndef BS_STAGGER_US
-#define BS_STAGGER_US 0.0
+#define BS_STAGGER_US 100.0
 #endif
 // the check lane's slot base and alpha-table address packed in one register (16-bit-address
 // one-chunk instances; ldpc_bs.hip checks that the tables end below 64 KB)

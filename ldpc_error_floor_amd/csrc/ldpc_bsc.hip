@@ -910,7 +910,7 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     a.cn_chunk = a.row_lay + 2 * (size_t)g.M;
     a.cn_var = reinterpret_cast<const uint32_t*>(a.cn_chunk + (size_t)p.nw * k.CPL);
     a.cn_lane = reinterpret_cast<const int32_t*>(a.cn_var + (size_t)p.cn_lanes * ((((k.D + k.LPC - 1) / k.LPC) + 1) / 2));
-    bs_stagger(true, &a.stagger, &a.stagger_n);
+    bs_stagger(false, &a.stagger, &a.stagger_n);     // (LDPC_BS_STAGGER still applies; C5: no gain)
     a.alut = alut;
     a.atid = (p.arows == 1 && !getenv("LDPC_BS_NOAFIX")) ? atid : nullptr;
     a.blut = blut;
