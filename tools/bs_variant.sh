@@ -13,7 +13,7 @@ W=$(mktemp -d /tmp/ldpc_bsvar.XXXX)
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -Ildpc_error_floor_amd/csrc -mllvm -pragma-unroll-threshold=500000 $*"
 N=$(ls $B/ldpc_bs_i*.o | wc -l)
 for i in $(seq 0 $((N - 1))); do
-  /opt/rocm/bin/hipcc $FLAGS -DBS_INST=$i -c ldpc_error_floor_amd/csrc/ldpc_bs_inst.hip -o "$W/bs_i$i.o" &
+  /opt/rocm/bin/hipcc $FLAGS -mllvm -amdgpu-use-amdgpu-trackers -DBS_INST=$i -c ldpc_error_floor_amd/csrc/ldpc_bs_inst.hip -o "$W/bs_i$i.o" &
 done
 /opt/rocm/bin/hipcc $FLAGS -c ldpc_error_floor_amd/csrc/ldpc_bsc.hip -o "$W/bsc.o" &
 /opt/rocm/bin/hipcc $FLAGS -c ldpc_error_floor_amd/csrc/ldpc_bs.hip -o "$W/bsh.o" &
