@@ -122,7 +122,7 @@ def build(force=False, jobs=4, verbose=False):
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, obj)
         objs.append(o)
-        if force or _newer(o, [s] + hdrs):
+        if force or _newer(o, [s] + hdrs + [os.path.abspath(__file__)]):   # (flags live here)
             jobs_list.append([hipcc] + flags + defs + ["-c", s, "-o", o])
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         for r in ex.map(_run, jobs_list):
