@@ -11,6 +11,9 @@ and resumes from it when rerun with the same arguments.  Writes ``<out>/sweep_c5
 
   python tools/sweep_c5.py --out gpurun_out/sweep_c5 [--scan 4194304] [--deep 1073741824]
   python tools/sweep_c5.py --out gpurun_out/c5_deep --deep-snrs 15.0 --deep 10737418240
+
+``--config C2|C3|C4`` sweeps another SURVEY §8 d workload the same way (its trained weights and
+channel ranges, bench.CONFIGS); the output is then ``<out>/sweep_<config>.json``.
 """
 import argparse
 import json
@@ -25,6 +28,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/sweep_c5")
+    ap.add_argument("--config", default="C5", choices=["C2", "C3", "C4", "C5"])
     ap.add_argument("--snrs", default="2.5,3.0,3.25,3.5,3.75,4.0,4.25,4.5,5.0")
     ap.add_argument("--scan", type=int, default=1 << 22)
     ap.add_argument("--deep", type=int, default=1 << 30)
@@ -40,11 +44,11 @@ def main():
     from ldpc_error_floor_amd.fer import fer_sweep
 
     os.makedirs(a.out, exist_ok=True)
-    cfg = bench.CONFIGS["C5"]
-    proto, g, W, cp = bench.load_problem(config="C5")
+    cfg = bench.CONFIGS[a.config]
+    proto, g, W, cp = bench.load_problem(config=a.config)
     dev = torch.device("cuda", 0)
     dec = NMSDecoder(proto, cfg["z"], W, 2, 5, device=dev, B_max=a.batch)
-    dec.punct, dec.short = cfg["punct"], cfg["short"]
+    dec.punct, dec.short = cfg.get("punct", (0, 0)), cfg.get("short", (0, 0))
     kernel = dec.kernel_info()[1]
     snrs = [float(x) for x in (a.deep_snrs or a.snrs).split(",")]
     sig = [float(x) for x in cp.sigma(np.asarray(snrs))]
@@ -91,9 +95,17 @@ def main():
             deep_idx.append(zero[0])
     deep, t_deep = run("deep", sorted(set(deep_idx)), a.deep) if deep_idx else ([], 0.0)
     n_total = a.scan * len(scan) + a.deep * len(set(deep_idx))
-    out = {"workload": "C5: 5G_LDPC_R0.73_n_dec2304_n2112_k1536_z72_s1537_1584, QMS q5, T=50, "
-                       "flat [3,0,3] alpha=0.75 beta=1, puncture 1-144, shorten 1537-1584, "
-                       "on-GPU Philox AWGN (seed 1076 + 7919 x SNR in mdB, + 104729 in the deep stage), all-zero codeword",
+    if a.config == "C5":
+        wl = ("C5: 5G_LDPC_R0.73_n_dec2304_n2112_k1536_z72_s1537_1584, QMS q5, T=50, "
+              "flat [3,0,3] alpha=0.75 beta=1, puncture 1-144, shorten 1537-1584")
+    else:
+        sh = ",".join(str(x) for x in cfg["sharing"])
+        wl = (f"{a.config}: {cfg['graph']}, QMS q5, T={cfg['T']}, sharing [{sh}] trained weights "
+              f"({os.path.basename(cfg['weights'])})"
+              + (f", puncture {cfg['punct'][0]}-{cfg['punct'][1]}" if "punct" in cfg else "")
+              + (f", shorten {cfg['short'][0]}-{cfg['short'][1]}" if "short" in cfg else ""))
+    out = {"workload": wl + ", on-GPU Philox AWGN (seed 1076 + 7919 x SNR in mdB, + 104729 in the "
+                            "deep stage), all-zero codeword",
            "kernel": kernel, "scan": scan, "deep": deep,
            "seconds": {"scan": round(t_scan, 1), "deep": round(t_deep, 1)},
            "codewords_total": n_total,
@@ -101,7 +113,7 @@ def main():
            "note": "FER counters from fer_sweep (device int64 counters, calc_ber_fer "
                    "semantics: fer_last = frames wrong at the last iteration, fer = frames "
                    "wrong at every iteration); e2e includes the channel kernel"}
-    with open(os.path.join(a.out, "sweep_c5.json"), "w") as f:
+    with open(os.path.join(a.out, f"sweep_{a.config.lower()}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: out[k] for k in ("kernel", "codewords_total", "codewords_per_s")}))
 
