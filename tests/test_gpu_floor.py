@@ -1,5 +1,5 @@
-"""Error-floor events of the timed kernel (GPU only); the C4 high-SNR flare at the end.  At 6 dB the wman decoder (C2: QMS q5,
-T=20, trained [3,0,3] weights) fails about 4e-7 of its frames (`profiles/r3/sweep_c2/`: 3,475
+"""Error-floor events of the timed kernel (GPU only), and the C4 high-SNR flare at the end.  At
+6 dB the wman decoder (C2: QMS q5, T=20, trained [3,0,3] weights) fails about 4e-7 of its frames (`profiles/r3/sweep_c2/`: 3,475
 frames in 8.6e9 codewords).  The 2^20-codeword parity tests see none of these frames, so here
 2^27 codewords at that SNR go through the bit-sliced kernel and through flood (both pinned on the
 reference's fixtures) batch by batch: counters and per-frame flags must agree, there must be
