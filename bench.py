@@ -36,8 +36,6 @@ import argparse
 import json
 import os
 import platform
-import socket
-import subprocess
 import sys
 import time
 
@@ -164,42 +162,10 @@ def cpu_baseline(proto, g, W, cp, B=480, T=20, snr=3.5):
             "sparse_oracle_cw_s_1thread": round(B / dt_sparse, 1)}
 
 
-def _free_port():
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        return sk.getsockname()[1]
-
-
 def launch_ranks(n):
-    """Start ranks 0..n-1 of this command as fresh child processes (one per GPU; RANK,
-    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT as torch.distributed.run would set them) and wait.
-    The parent never initialises HIP and never execs.  Rank 0 prints the JSON line (the
-    children share this stdout).  Returns 0, or the status of the first rank that failed (the
-    others are then terminated)."""
-    port = _free_port()
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
-                                      env=env))
-    status = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            rc = p.poll()
-            if rc is None:
-                continue
-            live.remove(p)
-            if rc != 0 and status == 0:
-                status = rc if rc > 0 else 128 - rc
-                print(f"bench.py: rank {procs.index(p)} exited with status {rc}; stopping the "
-                      f"other ranks", file=sys.stderr, flush=True)
-                for q in live:
-                    q.terminate()
-        time.sleep(0.05)
-    return status
+    """Ranks 0..n-1 of this command as fresh child processes (ldpc_error_floor_amd.launch)."""
+    from ldpc_error_floor_amd.launch import launch_ranks as _launch
+    return _launch(__file__, sys.argv[1:], n, tag="bench.py")
 
 
 def main():

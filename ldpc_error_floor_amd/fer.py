@@ -75,15 +75,18 @@ def shard_range(total: int, rank: int, world: int):
     return begin, begin + per + (1 if rank < rem else 0)
 
 
-CKPT_VERSION = 1
+CKPT_VERSION = 2        # 2: key holds point_seeds and the decoder fingerprint; rank 0's file
+                        # is <path> at every world size
 
 
 class SweepCheckpoint:
     """One rank's sweep state as a small JSON file, replaced atomically (write + rename).
 
     ``key`` holds everything that fixes the codeword stream and its partition (seed, sigmas,
-    total codewords, batch, T, puncture/shorten, rank/world); a resume against a different key
-    is refused.  ``si`` / ``pos`` = the SNR index and global codeword index to decode next,
+    total codewords, batch, T, puncture/shorten, rank/world, the decoder's fingerprint); a
+    resume against a different key is refused.  Rank 0 keeps ``<path>`` at every world size
+    (rank r > 0: ``<path>.rank<r>``), so a resume at another world size finds rank 0's file
+    and is refused by its key instead of silently starting over.  ``si`` / ``pos`` = the SNR index and global codeword index to decode next,
     ``counters`` = this rank's (not yet all-reduced) int64 counter block, ``uncor_bytes`` = the
     length of the uncorrected-word file at that point (truncated back to it on resume, so rows
     written after the checkpoint are not duplicated)."""
@@ -188,21 +191,29 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
     ck = None
     si0, pos0 = 0, begin
     if checkpoint is not None:
-        ck = SweepCheckpoint(checkpoint if world == 1 else f"{checkpoint}.rank{rank}")
+        ck = SweepCheckpoint(checkpoint if rank == 0 else f"{checkpoint}.rank{rank}")
         key = {"seed": int(seed), "point_seeds": point_seeds, "sigmas": [float(x) for x in sigmas],
                "n_codewords": int(n_codewords), "batch": int(batch),
                "T": None if T is None else int(T), "punct": list(punct), "short": list(short),
                "rank": rank, "world": world, "uncor": upath is not None,
                "decoder": decoder_fingerprint(decoder, T)}
-        st = ck.load() if resume else None
-        if st is None and upath is not None and os.path.exists(upath):
-            # a sweep that starts from the beginning owns its uncorrected-word file: rows left by
-            # an earlier attempt (e.g. one that died before its first checkpoint) would be
-            # written again
-            os.remove(upath)
+        err = ""
+        try:
+            st = ck.load() if resume else None
+            if st is not None and st["key"] != key:
+                err = f"{ck.path}: checkpoint is for {st['key']}, this sweep is {key}"
+        except ValueError as e:
+            st, err = None, str(e)
+        if dist_on:
+            # every rank raises together (one failing rank alone would leave the others waiting
+            # in the final all_reduce)
+            flag = torch.tensor([1 if err else 0], dtype=torch.int64, device=counters.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+            if int(flag.item()) and not err:
+                err = "another rank refused its checkpoint"
+        if err:
+            raise ValueError(err)
         if st is not None:
-            if st["key"] != key:
-                raise ValueError(f"{ck.path}: checkpoint is for {st['key']}, this sweep is {key}")
             si0, pos0 = st["si"], st["pos"]
             counters.copy_(torch.tensor(st["counters"], dtype=torch.int64))
             if upath is not None and st.get("uncor_bytes") is not None and os.path.exists(upath):
@@ -212,6 +223,12 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
     def save(si, pos, done=False):
         ub = (os.path.getsize(upath) if upath and os.path.exists(upath) else 0) if upath else None
         ck.save(key, si, pos, counters.cpu().tolist(), ub, done)
+
+    if ck is not None and st is None:
+        # a fresh start records the uncorrected-word file's current length at once: a resume
+        # truncates back to it (rows of an attempt that died before its first checkpoint go),
+        # and rows earlier sweeps appended to a shared file stay (Print_Functions.py:122 appends)
+        save(si0, pos0)
 
     if fused_channel and overlap and _pipelines(decoder, T, kernel):
         # the channel of batch j + 1 on a second stream while batch j decodes (the decoder reads

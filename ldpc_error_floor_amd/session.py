@@ -8,12 +8,16 @@ X, net_dict['ya']: Y, net_dict['etha']: e, net_dict['learn_rate']: 0})``
 (a single one or a list) plus ``ya_output{t}`` / ``ya_output_target{t}``.  The batch size is
 fixed like the reference's placeholders (``main_Base.py:124-125``): a different B raises.
 
-Parity mode on several GPUs (SURVEY §8 e: "host-generated LLRs, sliced by rank"): with
-``torch.distributed`` initialised, every rank runs the same host loop (``compute_results`` with
-the same seeds, so every rank holds the same ``xa``), decodes its contiguous slice of the batch
+Parity mode on several GPUs (SURVEY §8 e: "host-generated LLRs, sliced by rank"), opt-in
+with ``shard=True``: every rank runs the same host loop (``compute_results`` with the same
+seeds, so every rank holds the same ``xa``), decodes its contiguous slice of the batch
 (``fer.shard_range``) and ``all_gather``s the APP slices, so ``sess.run`` returns the whole
-``ya_output_all`` on every rank and every rank computes the same ``Results``.  The reference
-itself runs one process per GPU with no exchange (``main_Base.py:14-15``).
+``ya_output_all`` on every rank and every rank computes the same ``Results``.  Each call first
+checks (one all_reduce MIN/MAX of a checksum of ``xa``) that every rank fed the same batch and
+raises otherwise.  Every rank must make the same sequence of ``run`` calls.  Without
+``shard`` a Session never communicates, whatever ``torch.distributed`` holds: the reference
+itself runs one process per GPU with no exchange (``main_Base.py:14-15``), and ranks under
+torchrun may evaluate different configs or seeds.
 """
 from __future__ import annotations
 
@@ -40,23 +44,25 @@ def make_net_dict(T: int):
 
 class Session:
     def __init__(self, decoder: NMSDecoder, batch_size: int, T=None, loss_type: int = 2,
-                 loss_t_first=None, group=None):
+                 loss_t_first=None, group=None, shard: bool = False):
         self.decoder = decoder
         self.batch_size = int(batch_size)
         self.T = decoder.T if T is None else int(T)
         self.loss_type = loss_type
         self.loss_t_first = loss_t_first
         self.group = group
+        self.shard = bool(shard)
         self.calls = 0
 
     def _decode_app(self, X, target_bits=None):
-        """APP [T, B, bits] of the host batch X on the host: this rank's slice decoded, the
-        others gathered (one all_gather of equal-size padded slices)."""
+        """APP [T, B, bits] of the host batch X on the host.  Sharded (``shard=True`` with
+        more than one rank): this rank's slice decoded, the others gathered (one all_gather of
+        equal-size padded slices)."""
         import torch
         import torch.distributed as dist
         from .fer import shard_range
         B = X.shape[0]
-        dist_on = dist.is_available() and dist.is_initialized()
+        dist_on = self.shard and dist.is_available() and dist.is_initialized()
         world = dist.get_world_size(self.group) if dist_on else 1
         if world == 1:
             return self.decoder.decode(X, T=self.T, app=True, target_bits=target_bits).app.cpu().numpy()
@@ -67,6 +73,7 @@ class Session:
         # RCCL gathers device tensors; gloo (CPU rehearsal) host tensors
         on_dev = dist.get_backend(self.group) == "nccl"
         dev = self.decoder.device if on_dev else torch.device("cpu")
+        self._check_same_batch(X, dev)
         part = torch.zeros((self.T, per, nb), dtype=torch.float32, device=dev)
         if b1 > b0:
             app = self.decoder.decode(X[b0:b1], T=self.T, app=True, target_bits=target_bits).app
@@ -78,6 +85,22 @@ class Session:
             r0, r1 = shard_range(B, r, world)
             out[:, r0:r1] = parts[r][:, :r1 - r0].cpu().numpy()
         return out
+
+    def _check_same_batch(self, X, dev):
+        """Raise unless every rank of the group fed the same ``xa`` (a sharded Session gathers
+        the other ranks' APP rows, which are only this rank's answer if they decoded this
+        rank's batch)."""
+        import hashlib
+        import torch
+        import torch.distributed as dist
+        h = hashlib.blake2b(np.ascontiguousarray(X).tobytes(), digest_size=7).digest()
+        v = int.from_bytes(h, "little")                  # < 2^56: exact in int64
+        lo = torch.tensor([v, -v], dtype=torch.int64, device=dev)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+        if int(lo[0]) != v or int(lo[1]) != -v:
+            raise RuntimeError("Session(shard=True): the ranks fed different xa batches to "
+                               "sess.run; a sharded parity run needs the same host stream on "
+                               "every rank")
 
     def run(self, fetches, feed_dict):
         single = not isinstance(fetches, (list, tuple))
@@ -118,10 +141,10 @@ class Session:
 
 
 def build_session(cfg: NMSConfig, proto=None, weights: DecoderWeights = None, device=None,
-                  kernel: str = "auto", graph_dir=None, group=None):
-    """Decoder + Session + net_dict for a reference-style config (``group``: the process group
-    a multi-GPU parity run shards each batch over; default: the default group when
-    ``torch.distributed`` is initialised)."""
+                  kernel: str = "auto", graph_dir=None, group=None, shard: bool = False):
+    """Decoder + Session + net_dict for a reference-style config.  ``shard=True``: a
+    multi-GPU parity run that splits each batch over the ranks of ``group`` (default: the
+    default group); off by default, so every rank decodes its own batches alone."""
     import os
     from .code import default_graph_dir
     cfg.validate()
@@ -142,5 +165,5 @@ def build_session(cfg: NMSConfig, proto=None, weights: DecoderWeights = None, de
     dec.punct = (int(cfg.punct_start), int(cfg.punct_end))
     dec.short = (int(cfg.short_start), int(cfg.short_end))
     t_first = max(cfg.iters_max - cfg.iter_step - cfg.fixed_init, cfg.fixed_iter)
-    sess = Session(dec, cfg.batch_size, T, cfg.loss_type, t_first, group=group)
+    sess = Session(dec, cfg.batch_size, T, cfg.loss_type, t_first, group=group, shard=shard)
     return sess, make_net_dict(T)

@@ -114,9 +114,11 @@ def test_bench_launcher_spawns_and_propagates_failure():
     assert "exited with status" in r.stderr
 
 
-def _session_worker(rank, world, port, q):
+def _session_worker(rank, world, port, q, shard=True, seed_per_rank=False):
     """One rank of the parity-mode FER loop: the reference's compute_results over a Session
-    that decodes this rank's slice of every host batch and gathers the rest (gloo)."""
+    that decodes this rank's slice of every host batch and gathers the rest (gloo).
+    ``shard=False``: a plain Session under the same process group (no communication);
+    ``seed_per_rank``: rank r draws its noise from seed 1076 + r (a sharded Session refuses)."""
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     try:
@@ -131,14 +133,34 @@ def _session_worker(rank, world, port, q):
             calls.append(np.asarray(llr).shape[0])
             return inner(llr, **kw)
         dec.decode = spy
-        sess = Session(dec, batch_size=int(d["B"]))
-        wr, nr = np.random.RandomState(2044), np.random.RandomState(1076)
-        Results, _ = fer.compute_results(int(d["sample_num"]), [], [], d["sigma"], wr, nr,
-                                         int(d["B"]), 0, 24, 6, 24, True, 20, sess,
-                                         make_net_dict(20), 0, 2, 0, 0, 0, 0, 5, 20.0)
+        sess = Session(dec, batch_size=int(d["B"]), shard=shard)
+        wr = np.random.RandomState(2044)
+        nr = np.random.RandomState(1076 + (rank if seed_per_rank else 0))
+        try:
+            Results, _ = fer.compute_results(int(d["sample_num"]), [], [], d["sigma"], wr, nr,
+                                             int(d["B"]), 0, 24, 6, 24, True, 20, sess,
+                                             make_net_dict(20), 0, 2, 0, 0, 0, 0, 5, 20.0)
+        except RuntimeError as e:
+            q.put((rank, str(e), calls))
+            return
         q.put((rank, Results.tolist(), calls))
     finally:
         dist.destroy_process_group()
+
+
+def _run_session_ranks(**kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_session_worker, args=(r, 2, port, q), kwargs=kw)
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (res, calls)) for r, res, calls in (q.get(timeout=600) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
 
 
 def test_session_parity_mode_sharded_over_ranks():
@@ -146,18 +168,31 @@ def test_session_parity_mode_sharded_over_ranks():
     half of every 120-codeword batch and all_gather the APP; both reproduce the reference's own
     compute_results Results (tests/golden/results_wman_303.npz) exactly."""
     d = np.load(os.path.join(GOLDEN, "results_wman_303.npz"))
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_session_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    got = dict((r, (res, calls)) for r, res, calls in (q.get(timeout=600) for _ in procs))
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    got = _run_session_ranks(shard=True)
     B = int(d["B"])
     for r in (0, 1):
         np.testing.assert_array_equal(np.asarray(got[r][0], np.float32), d["Results"])
         b0, b1 = shard_range(B, r, 2)
         assert set(got[r][1]) == {b1 - b0}         # only its own slice, every call
+
+
+def test_session_unsharded_under_process_group_decodes_whole_batches():
+    """Without shard=True a Session under an initialised process group never communicates:
+    each rank decodes its whole batches (the reference's one-process-per-GPU model,
+    main_Base.py:14-15), here with a different noise seed per rank."""
+    d = np.load(os.path.join(GOLDEN, "results_wman_303.npz"))
+    got = _run_session_ranks(shard=False, seed_per_rank=True)
+    B = int(d["B"])
+    np.testing.assert_array_equal(np.asarray(got[0][0], np.float32), d["Results"])
+    assert not np.array_equal(np.asarray(got[1][0], np.float32), d["Results"])
+    for r in (0, 1):
+        assert set(got[r][1]) == {B}
+
+
+def test_session_sharded_refuses_different_batches():
+    """A sharded Session whose ranks feed different xa raises on every rank instead of
+    returning APP rows other ranks decoded from their own batches."""
+    got = _run_session_ranks(shard=True, seed_per_rank=True)
+    for r in (0, 1):
+        assert isinstance(got[r][0], str) and "different xa" in got[r][0]
+        assert got[r][1] == []

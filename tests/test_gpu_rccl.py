@@ -29,6 +29,7 @@ def _rank_env():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", LOCAL_WORLD_SIZE="1",
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
     env.pop("LDPC_BENCH_BACKEND", None)          # the default backend: nccl (RCCL)
+    env.pop("LDPC_SWEEP_BACKEND", None)
     return env
 
 
@@ -88,3 +89,26 @@ def test_fer_sweep_over_rccl_group(cuda_device):
     assert out["backend"] == "nccl"
     assert out["grouped"] == out["plain"]
     assert out["plain"][0][1] > 0
+
+
+def test_sweep_tool_world1_over_rccl(tmp_path):
+    """tools/sweep_c5.py (the configs[4] multi-GPU sweep entry point) as an RCCL world-1 rank
+    gives the counters of the same sweep run without a process group."""
+    args = [sys.executable, os.path.join(ROOT, "tools", "sweep_c5.py"), "--config", "C2",
+            "--snrs", "2.0,4.0", "--scan", "65536", "--deep", "98304", "--batch", "32768",
+            "--deep-below", "0.5"]
+    plain_env = {k: v for k, v in os.environ.items()
+                 if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LDPC_SWEEP_BACKEND")}
+    outs = {}
+    for name, env in (("plain", plain_env), ("rccl", _rank_env())):
+        out = str(tmp_path / name)
+        r = subprocess.run(args + ["--out", out], env=env, capture_output=True, text=True,
+                           timeout=300, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        with open(os.path.join(out, "sweep_c2.json")) as f:
+            outs[name] = json.load(f)
+    assert outs["plain"]["process_group"] is None
+    assert outs["rccl"]["process_group"] == {"backend": "nccl", "world": 1}
+    strip = lambda j: [{k: v for k, v in r.items()} for r in j["scan"] + j["deep"]]  # noqa: E731
+    assert strip(outs["rccl"]) == strip(outs["plain"])
+    assert outs["plain"]["scan"][0]["frame_err_last"] > 0 and outs["plain"]["deep"]

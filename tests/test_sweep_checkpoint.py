@@ -122,18 +122,40 @@ def test_resume_refuses_a_different_decoder(tmp_path):
     assert _tuples(fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=3, checkpoint=ck, resume=True)) == full
 
 
-@pytest.mark.parametrize("resume", [False, True])
-def test_fresh_start_replaces_stale_uncorrected_file(tmp_path, resume):
-    """A checkpointed sweep that starts from the beginning (no checkpoint yet, or resume off)
-    owns its uncorrected-word file: rows an earlier attempt left are not kept."""
+def test_fresh_start_keeps_earlier_rows_and_resume_drops_its_own(tmp_path):
+    """A checkpointed sweep appends to its uncorrected-word file like the reference
+    (Print_Functions.py:122) and like an un-checkpointed sweep: rows earlier sweeps wrote stay.
+    Its fresh start records the file's length in the checkpoint at once, so an attempt that
+    dies before its first periodic checkpoint and is resumed leaves no duplicated rows."""
     dec = _make_decoder()
     ref_path = str(tmp_path / "ref.txt")
     fer_sweep(dec, SIGMAS[:1], N_CW, BATCH, seed=5, uncor_path=ref_path)
+    ref = open(ref_path).read()
+    assert ref
+    prior = "0.0\t0.0\t0.0\trow of an earlier SNR point's sweep\n"
     path = tmp_path / "Uncor.txt"
-    path.write_text("0.0\t0.0\tstale row from an attempt that died before its first checkpoint\n")
+    path.write_text(prior)
     fer_sweep(dec, SIGMAS[:1], N_CW, BATCH, seed=5, uncor_path=str(path),
-              checkpoint=str(tmp_path / "n.ckpt"), resume=resume)
-    assert path.read_text() == open(ref_path).read()
+              checkpoint=str(tmp_path / "a.ckpt"))
+    assert path.read_text() == prior + ref
+    # dies after 4 of 6 batches, before any periodic checkpoint (every 64 batches)
+    path.write_text(prior)
+    ck = str(tmp_path / "b.ckpt")
+    with pytest.raises(Stop):
+        fer_sweep(dec, SIGMAS[:1], N_CW, BATCH, seed=5, uncor_path=str(path), checkpoint=ck,
+                  progress=_interrupt_after(4))
+    st = json.load(open(ck))
+    assert (st["si"], st["pos"], st["uncor_bytes"]) == (0, 0, len(prior))
+    fer_sweep(dec, SIGMAS[:1], N_CW, BATCH, seed=5, uncor_path=str(path), checkpoint=ck,
+              resume=True)
+    assert path.read_text() == prior + ref
+
+
+def test_old_checkpoint_version_refused(tmp_path):
+    ck = tmp_path / "old.ckpt"
+    ck.write_text(json.dumps({"version": 1, "key": {}, "si": 0, "pos": 0, "counters": []}))
+    with pytest.raises(ValueError, match="checkpoint version 1"):
+        fer_sweep(_make_decoder(), SIGMAS, N_CW, BATCH, checkpoint=str(ck), resume=True)
 
 
 def test_point_seeds_decouple_points_from_their_position():
