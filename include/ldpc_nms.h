@@ -29,7 +29,8 @@
 extern "C" {
 #endif
 
-#define LDPC_NMS_ABI_VERSION 2     /* 2: ldpc_decode_outputs.iter_wrong, ldpc_ctx_last_kernel */
+#define LDPC_NMS_ABI_VERSION 3     /* 2: ldpc_decode_outputs.iter_wrong, ldpc_ctx_last_kernel;
+                                      3: ldpc_decode_params.outputs_size */
 
 typedef struct ldpc_graph ldpc_graph;
 typedef struct ldpc_ctx ldpc_ctx;
@@ -63,7 +64,12 @@ typedef struct ldpc_decode_params {
     int32_t target_bits;        /* Nt*z: width of app_all and of the FER/BER bit range */
     float clip_llr;             /* clip_LLR (20.0 in the reference) */
     int32_t kernel;             /* ldpc_kernel */
-    int32_t reserved[2];
+    int32_t outputs_size;       /* sizeof(ldpc_decode_outputs) the caller was built with: 0 = the
+                                   ABI-1 struct (five pointers, no iter_wrong; ABI-1 callers zeroed
+                                   this word as reserved), sizeof(ldpc_decode_outputs) = this
+                                   header's struct; any other value -> LDPC_ERR_ARG.  The library
+                                   never reads past the size the caller declares. */
+    int32_t reserved;
 } ldpc_decode_params;
 
 typedef struct ldpc_decode_outputs {
@@ -78,7 +84,8 @@ typedef struct ldpc_decode_outputs {
                                    decision 1 among the target bits at iteration t (the per-iteration
                                    frame error of calc_ber_fer, Print_Functions.py:100-118; the
                                    all-zero codeword), bits past B zero; or NULL.  Every kernel
-                                   serves it, the counters-only ones included. */
+                                   serves it, the counters-only ones included.  Read only when
+                                   ldpc_decode_params.outputs_size declares it (ABI 3). */
 } ldpc_decode_outputs;
 
 int ldpc_abi_version(void);

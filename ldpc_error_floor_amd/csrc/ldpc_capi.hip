@@ -478,8 +478,21 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     int mode = -1;
     const int chk = host::check_decode(g->h, B, c->B_max, c->T_max, g->T_w, p, &mode);
     if (chk != LDPC_OK) return chk;
-    ldpc_decode_outputs none{};
-    const ldpc_decode_outputs& out = o ? *o : none;
+    // the caller's outputs struct, never read past the size it declares (ABI 1: five pointers)
+    ldpc_decode_outputs out{};
+    if (o) {
+        if (p->outputs_size == (int32_t)sizeof(ldpc_decode_outputs)) {
+            out = *o;
+        } else if (p->outputs_size == 0) {
+            out.app_all = o->app_all;
+            out.hard_bits = o->hard_bits;
+            out.synd_bits = o->synd_bits;
+            out.counters = o->counters;
+            out.frame_flags = o->frame_flags;
+        } else {
+            return LDPC_ERR_ARG;
+        }
+    }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     DeviceGuard dg(g->device);
     const bool ucn = g->d_alpha_ucn != nullptr;

@@ -95,7 +95,11 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
             }
             ws.hd_elems = (int64_t)elems;
         }
-        if (hipMemsetAsync(ws.hd, 0, (size_t)(b.T + 1) * b.ntiles * g.n_vars * 4 * sizeof(uint64_t), s) != hipSuccess)
+        // the v5 export ORs its bits into a zeroed buffer; a bit-sliced decode reads the tile
+        // buffer only for the packs its v5 fixup decodes, and the fixup clears those blocks'
+        // bits itself (f5_block), so the (T + 1) x tiles x n_vars x 32 B memset is skipped
+        if (!bs &&
+            hipMemsetAsync(ws.hd, 0, (size_t)(b.T + 1) * b.ntiles * g.n_vars * 4 * sizeof(uint64_t), s) != hipSuccess)
             return LDPC_ERR_HIP;
         hd_out = ws.hd;
     }

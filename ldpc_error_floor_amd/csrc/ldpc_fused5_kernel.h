@@ -279,6 +279,27 @@ f5_block(const F5Args& a, const float* __restrict__ alpha, const float* __restri
     const float inv = a.inv, step = a.step;
     const int z = a.z;
 
+    if (a.only && a.hd_out) {
+        // bit-sliced fixup with a hard-bit export: nobody zeroed the tile buffer (the host
+        // skips that memset for bit-sliced decodes), so clear this block's codeword bits of the
+        // iterations the export reads (slots t + 1, t < T) before the VN phases OR them in.
+        // Other blocks of the same tile own other bits of the same words: atomicAnd only.
+        const int64_t tile = b0 / TILE;
+        const int bl0 = (int)(b0 - tile * TILE);          // CW divides TILE: one tile per block
+        const int n = a.T * nv * 4;
+        for (int i = tid; i < n; i += NT) {
+            const int w = i & 3;
+            const int v = (i >> 2) % nv;
+            const int t = (i >> 2) / nv;
+            const int kmin = (bl0 - w + 3) >> 2, kmax = (bl0 + (int)nvalid - 1 - w) >> 2;
+            if (kmax < kmin) continue;
+            const unsigned long long m = ((kmax - kmin == 63) ? ~0ull : ((2ull << (kmax - kmin)) - 1)) << kmin;
+            atomicAnd(reinterpret_cast<unsigned long long*>(
+                          a.hd_out + ((((size_t)(t + 1) * a.ntiles + tile) * nv + v) * 4) + w), ~m);
+        }
+        __syncthreads();
+    }
+
     F5_STAMP(0);
     // ---- prologue: coalesced LLR block -> padded scratch -> CH[v][cw]; beta; W = Tv_0 | hd ----
     {

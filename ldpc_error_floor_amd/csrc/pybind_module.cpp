@@ -78,6 +78,7 @@ static ldpc_decode_params make_params(int T, int decoding_type, int q_bit, int t
     p.target_bits = target_bits;
     p.clip_llr = clip;
     p.kernel = kernel;
+    p.outputs_size = (int32_t)sizeof(ldpc_decode_outputs);
     return p;
 }
 

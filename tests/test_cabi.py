@@ -38,7 +38,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_version_and_status_strings(lib):
-    assert lib.ldpc_abi_version() == 2
+    assert lib.ldpc_abi_version() == 3
     lib.ldpc_status_string.restype = ctypes.c_char_p
     assert lib.ldpc_status_string(0) == b"ok"
     assert b"argument" in lib.ldpc_status_string(-1)

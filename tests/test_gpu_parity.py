@@ -39,7 +39,7 @@ def test_extension_is_native(cuda_device):
     from ldpc_error_floor_amd import _native
     mod = _native.load()
     assert mod.__file__.startswith(os.path.join(ROOT, "ldpc_error_floor_amd"))
-    assert mod.abi_version() == 2
+    assert mod.abi_version() == 3
 
 
 @pytest.mark.parametrize("kernel", KERNEL_NAMES)

@@ -108,6 +108,9 @@ def test_bitsliced_export_off_grid_packs(cuda_device):
     llr = dec.awgn(200, float(cp.sigma(2.0)), seed=3)
     llr[40, 3] += 0.1                 # pack 1 off the grid
     llr[199, 0] = 25.0                # the last (ragged) pack out of range
+    # first fill the context's tile buffer with another batch's bits (a v5 APP + hard-bit
+    # export): the bit-sliced export does not zero it, its fixup clears the blocks it decodes
+    dec.decode(dec.awgn(200, float(cp.sigma(0.5)), seed=4), app=True, hard=True, kernel="fused")
     res = {}
     for k in ("flood", "fused"):
         r = dec.decode(llr, app=False, hard=True, synd=True, iter_wrong=True, kernel=k)
