@@ -1,16 +1,29 @@
-// ldpc_awgn.h — the on-GPU AWGN LLR generator shared by ldpc_channel_awgn (ldpc_channel.hip)
-// and the fused decoder's in-prologue channel (ldpc_fused5.hip), so that generating inside the
-// decoder is bit-identical to generating into HBM and decoding.
+// ldpc_awgn.h — the on-GPU AWGN LLR generator shared by ldpc_channel_awgn (ldpc_channel.hip),
+// ldpc_decode_awgn's byte channel for the bit-sliced kernels and the fused v5 decoder's
+// in-prologue channel (ldpc_fused5.hip), so that generating inside the decoder is bit-identical
+// to generating into HBM and decoding.
 //
 // Channel model of create_mix_epoch (Print_Functions.py:29-72) for the all-zero word:
 //   y = sigma * n - 1 (BPSK 0 -> -1),  LLR = 2 y / sigma^2 (log p1/p0);  QMS: Cal_MSA_Q
 //   (round half to even + clip); punctured bits -> 0 (0.001 for sum-product); shortened bits
 //   -> -clip_LLR (after quantization).
-// Noise: counter-based Philox4x32-10 keyed by the 64-bit seed, counter = (pair index, global
-// codeword index, tag), so any shard generated with its global codeword offset draws exactly
-// the numbers one GPU would.  Box-Muller on (u1, u2): u1 takes 53 random bits and is converted
-// to fp32 only at the logarithm — fp32's exponent range reaches 2^-54, so |n| goes to ~8.6
-// sigma and the tails that matter at FER ~1e-9 are kept — everything else is fp32.
+// Noise: counter-based Philox4x32-10 keyed by the 64-bit seed, so any shard generated with its
+// global codeword offset draws exactly the numbers one GPU would.  Two samplers:
+//  * float modes (SP, MS): Box-Muller per (codeword, element pair), counter = (pair index,
+//    global codeword index, tag).  u1 takes 53 random bits and is converted to fp32 only at the
+//    logarithm — fp32's exponent range reaches 2^-54, so |n| goes to ~8.6 sigma — everything
+//    else is fp32.
+//  * QMS (every q_bit): the quantized LLR is one of at most 33 levels, and level j is taken
+//    with probability Phi(n_j) - Phi(n_{j-1}), n_j the noise value of the j-th rounding
+//    boundary of Cal_MSA_Q (computed on the host in float64 from erfc, as a 64-bit fixed-point
+//    CDF threshold T_j = P(level <= j) 2^64).  Element (b, v) compares a 64-bit uniform U with
+//    the thresholds: level = #{j : U >= T_j}.  U's high word is word (b mod 4) of
+//    Philox(v, b / 4, tag 'LDQ4') — one Philox call serves four codewords of one variable, and
+//    punctured / shortened variables draw nothing — and its low word (word b mod 4 of
+//    Philox(v, b / 4, tag 'LDQR')) is drawn only when the high word equals a threshold's (about
+//    once per 2^27 elements).  This is the reference's distribution exactly (to 2^-64 per
+//    level, against fp32 Box-Muller's ulp-level boundary errors and its ~8.6 sigma tail cut),
+//    with no logarithm, square root or sine: about a third of the Box-Muller VALU per element.
 // It is NOT the numpy RandomState stream: host-generated LLRs remain the seed-parity path.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -42,6 +55,10 @@ struct Philox {
     }
 };
 
+constexpr int AWGN_NB_MAX = 32;        // rounding boundaries of the widest quantizer (q = 6)
+constexpr uint32_t AWGN_TAG_Q = 0x4C445134u;   // 'LDQ4': high words of the QMS uniforms
+constexpr uint32_t AWGN_TAG_R = 0x4C445152u;   // 'LDQR': their low words (rarely drawn)
+
 struct AwgnParams {
     uint32_t k0, k1;        // Philox key (seed low / high word)
     int64_t offset;         // global index of the batch's first codeword
@@ -49,28 +66,22 @@ struct AwgnParams {
     float clip;
     int decoding_type, q_bit;
     int ps, pe, ss, se;     // 1-based inclusive puncture / shorten ranges (0: none)
+    // QMS level sampler (make_awgn fills it when decoding_type is QMS)
+    int nb;                 // boundaries; levels 0 .. nb
+    int kmin;               // grid index of level 0 (value / grid step), for the byte output
+    uint32_t thr_hi[AWGN_NB_MAX], thr_lo[AWGN_NB_MAX];   // T_j, ascending
+    float val[AWGN_NB_MAX + 1];                           // LLR value of level j
 };
 
-// host: parameters from the C-ABI arguments (ldpc_channel.hip)
+// host: parameters from the C-ABI arguments, with the QMS level thresholds (ldpc_channel.hip)
 AwgnParams make_awgn(double sigma, uint64_t seed, int64_t offset, int decoding_type, int q_bit,
                      int ps, int pe, int ss, int se, float clip);
+// ldpc_decode_awgn's byte channel for the bit-sliced kernels: q8 = [ceil(B/32)][n_vars][8] words
+// (k_awgn_q8; qmax: the grid's largest magnitude, for the shortened-bit byte)
+int channel_q8(uint32_t* q8, int64_t B, int n_vars, const AwgnParams& a, int qmax, hipStream_t s);
 
-__device__ __forceinline__ float awgn_quant(float x, int q_bit) {
-    switch (q_bit) {
-        case 6: return fminf(fmaxf(rintf(x), -15.5f), 15.5f);
-        case 5: return fminf(fmaxf(rintf(x * 2.0f) * 0.5f, -7.5f), 7.5f);
-        case -5: return fminf(fmaxf(rintf(x), -15.0f), 15.0f);
-        case 4: return fminf(fmaxf(rintf(x), -7.0f), 7.0f);
-        default: return fminf(fmaxf(rintf(x * 0.5f) * 2.0f, -6.0f), 6.0f);
-    }
-}
-
-// LLRs of elements 2*pr and 2*pr+1 of codeword `b` (batch-relative) into l[0], l[1].
-// QB: the quantizer, fixed at compile time (0 = none, i.e. a float mode; else the q_bit), or
-// AWGN_QRT to take decoding_type / q_bit from `a` at run time (the runtime switch compiles to
-// all five quantizers and selects)
-constexpr int AWGN_QRT = 99;
-template <int QB = AWGN_QRT>
+// float modes (SP, MS): LLRs of elements 2*pr and 2*pr+1 of codeword `b` (batch-relative)
+// into l[0], l[1] by Box-Muller (QMS uses the level sampler below)
 __device__ __forceinline__ void awgn_pair(const AwgnParams& a, int64_t b, int pr, float (&l)[2]) {
     const uint64_t gcw = (uint64_t)(a.offset + b);
     uint32_t c[4] = {(uint32_t)pr, (uint32_t)gcw, (uint32_t)(gcw >> 32), 0x4C445043u};
@@ -86,15 +97,96 @@ __device__ __forceinline__ void awgn_pair(const AwgnParams& a, int64_t b, int pr
     for (int h = 0; h < 2; ++h) {
         const int bit = 2 * pr + h + 1;                                  // 1-based like the reference
         float llr = (nz[h] * a.sigma - 1.0f) * a.inv;
-        if constexpr (QB == AWGN_QRT) {
-            if (a.decoding_type == LDPC_DEC_QMS) llr = awgn_quant(llr, a.q_bit);
-        } else if constexpr (QB != 0) {
-            llr = awgn_quant(llr, QB);
-        }
         if (a.ps > 0 && bit >= a.ps && bit <= a.pe) llr = (a.decoding_type == 0) ? 0.001f : 0.0f;
         if (a.ss > 0 && bit >= a.ss && bit <= a.se) llr = -a.clip;
         l[h] = llr;
     }
+}
+
+// ---- QMS level sampler -------------------------------------------------------------------------
+// Level of each of the four codewords 4 gq + j (global quad gq) at variable v (0-based), from the
+// high words hw (Philox(v, gq, 'LDQ4')).  bucket / thi / tlo: the bucket table (awgn_bucket_fill)
+// and thresholds, in LDS or global memory.  A bucket holds base | count << 8: U's top AWGN_KB
+// bits fix every threshold but the `count` ones starting at `base`, compared one by one.
+constexpr int AWGN_KB = 10;                 // bucket bits (1024 buckets, 2 KB of LDS)
+template <typename P16, typename P32>
+__device__ __forceinline__ int awgn_level(const AwgnParams& a, P16 bucket, P32 thi, P32 tlo,
+                                          uint32_t u, uint32_t v, uint64_t gq, int j) {
+    const uint32_t e = bucket[u >> (32 - AWGN_KB)];
+    int lv = (int)(e & 0xFFu);
+    const int cnt = (int)(e >> 8);
+    for (int i = 0; i < cnt; ++i) {
+        const uint32_t th = thi[lv];
+        if (u < th) break;                       // thresholds ascend: the rest are above U too
+        if (u == th) {                           // the high words tie: compare the low words
+            uint32_t c[4] = {v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_R};
+            Philox::gen(c, a.k0, a.k1);
+            if (c[j] < tlo[lv]) break;
+        }
+        ++lv;
+    }
+    return lv;
+}
+
+// the bucket table of a's thresholds, built by the threads of a workgroup (tid < n) into LDS
+__device__ __forceinline__ void awgn_bucket_fill(const AwgnParams& a, uint16_t* bucket, uint32_t* thi,
+                                                 uint32_t* tlo, int tid, int n) {
+    for (int i = tid; i < a.nb; i += n) {
+        thi[i] = a.thr_hi[i];
+        tlo[i] = a.thr_lo[i];
+    }
+    for (int b = tid; b < (1 << AWGN_KB); b += n) {
+        int base = 0, cnt = 0;
+        for (int i = 0; i < a.nb; ++i) {
+            const uint32_t tb = a.thr_hi[i] >> (32 - AWGN_KB);
+            base += tb < (uint32_t)b ? 1 : 0;
+            cnt += tb == (uint32_t)b ? 1 : 0;
+        }
+        bucket[b] = (uint16_t)(base | cnt << 8);
+    }
+}
+
+// the levels of codewords 4 gq .. 4 gq + 3 at variable v (0-based; punctured / shortened
+// variables are the caller's): level indices 0 .. a.nb
+template <typename P16, typename P32>
+__device__ __forceinline__ void awgn_levels4(const AwgnParams& a, P16 bucket, P32 thi, P32 tlo,
+                                             uint32_t v, uint64_t gq, int (&lv)[4]) {
+    uint32_t c[4] = {v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_Q};
+    Philox::gen(c, a.k0, a.k1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lv[j] = awgn_level(a, bucket, thi, tlo, c[j], v, gq, j);
+}
+
+// what a QMS element at 1-based bit `bit` is: 0 random, 1 punctured (LLR 0), 2 shortened (-clip)
+__device__ __forceinline__ int awgn_fixed(const AwgnParams& a, int bit) {
+    if (a.ss > 0 && bit >= a.ss && bit <= a.se) return 2;
+    if (a.ps > 0 && bit >= a.ps && bit <= a.pe) return 1;
+    return 0;
+}
+
+// one QMS element (codeword at global index gb, variable v) by a linear threshold scan over a's
+// own tables: the fused v5 kernel's in-prologue channel for batches whose offset is not a
+// multiple of 4 (same stream as awgn_levels4)
+__device__ __forceinline__ float awgn_qms_elem(const AwgnParams& a, uint64_t gb, int v) {
+    const int fx = awgn_fixed(a, v + 1);
+    if (fx == 1) return 0.0f;
+    if (fx == 2) return -a.clip;
+    const uint64_t gq = gb >> 2;
+    const int j = (int)(gb & 3);
+    uint32_t c[4] = {(uint32_t)v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_Q};
+    Philox::gen(c, a.k0, a.k1);
+    const uint32_t u = c[j];
+    int lv = 0;
+    for (int i = 0; i < a.nb; ++i) {
+        if (u < a.thr_hi[i]) break;
+        if (u == a.thr_hi[i]) {
+            uint32_t r[4] = {(uint32_t)v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_R};
+            Philox::gen(r, a.k0, a.k1);
+            if (r[j] < a.thr_lo[i]) break;
+        }
+        ++lv;
+    }
+    return a.val[lv];
 }
 
 }  // namespace ldpc

@@ -76,7 +76,7 @@ __global__ void k_bs_tables(const float* __restrict__ alpha, const float* __rest
 }
 
 // ---- host: planning, graph tables, launch -------------------------------------------------
-typedef int (*LaunchFn)(const BsArgs&, int, int, size_t, hipStream_t);
+typedef int (*LaunchFn)(const BsArgs&, int, int, size_t, hipStream_t, bool);
 template <int... I>
 constexpr auto launch_table(std::integer_sequence<int, I...>) {
     return std::array<LaunchFn, sizeof...(I)>{&bs_launch<I>...};
@@ -662,6 +662,12 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
     return LDPC_OK;
 }
 
+bool bs_q8_ok(const DevGraph& g, int mode, bool ucn, float clip, int T, bool has_short) {
+    const BsPlan p = bs_plan(g, mode, ucn, false, clip, T);
+    if (!p.ok) return bsc_q8_ok(g, mode, ucn, clip, T, has_short);
+    return !has_short || p.cu > 0.f;
+}
+
 int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
               bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, uint32_t* hdx, hipStream_t s) {
     const BsPlan p = bs_plan(g, mode, ucn, false, b.clip, b.T);
@@ -683,7 +689,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     const int VNW = (k.PK ? (DV + 1) / 2 : DV) + 1;
     const uint32_t* gt = reinterpret_cast<const uint32_t*>(ws.bs_graph);
     BsArgs a{};
-    a.llr = llr;
+    a.llr = b.q8 ? reinterpret_cast<const float*>(b.q8) : llr;
     a.B = b.B;
     a.n_vars = g.n_vars;
     a.n_checks = g.n_checks;
@@ -730,7 +736,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // -DBS_DIAG builds
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
     static const auto kLaunch = launch_table(std::make_integer_sequence<int, kBsNInst>{});
-    return kLaunch[p.inst](a, nblocks, p.nw, p.lds, s);
+    return kLaunch[p.inst](a, nblocks, p.nw, p.lds, s, b.q8 != nullptr);
 }
 
 }  // namespace ldpc

@@ -11,8 +11,8 @@ namespace ldpc {
 namespace bs {
 
 template <>
-int bs_launch<BS_INST>(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
-    return launch_bs<BS_INST>(a, nblocks, nw, lds, s);
+int bs_launch<BS_INST>(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s, bool q8) {
+    return launch_bs<BS_INST>(a, nblocks, nw, lds, s, q8);
 }
 
 }  // namespace bs

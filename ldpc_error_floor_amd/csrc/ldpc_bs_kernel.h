@@ -67,7 +67,8 @@ constexpr BsInst kBsInst[] = {
 constexpr int kBsNInst = sizeof(kBsInst) / sizeof(kBsInst[0]);
 
 struct BsArgs {
-    const float* llr;
+    const float* llr;            // (Q8 builds: the channel as bytes [packs][n_vars][8] words,
+                                 // pack_channel_q8; the field keeps the kernarg layout of the others)
     int64_t B;
     int n_vars, n_checks, T, target_bits, cn_lanes, cn_dmin;
     float inv;
@@ -518,22 +519,11 @@ __device__ __forceinline__ void t8x8(uint32_t& lo, uint32_t& hi) {
     lo ^= t;
     hi ^= t >> 4;
 }
+// the 32 bytes (byte r of D[r / 4]: q + 16, + 32 on a shortened bit) -> sign / magnitude /
+// shortened planes
 template <bool BIG>
-__device__ __forceinline__ int pack_channel(const float (&xv)[PACK], float inv, int qmax, float cu,
-                                            uint32_t valid, uint32_t& cs, uint32_t (&cm)[4], uint32_t& bg) {
-    const float qf = (float)qmax;
-    uint32_t D[8];
-    int off = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) D[k] = 0u;
-#pragma unroll
-    for (int r = 0; r < PACK; ++r) {
-        const float x = xv[r] * inv;
-        const float q = __builtin_amdgcn_fmed3f(rintf(x), -qf, qf);
-        const bool big = BIG && fabsf(x) == cu;
-        off |= (q != x && !big) ? 1 : 0;
-        D[r >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(q + (big ? 48.f : 16.f), r & 3, D[r >> 2]);
-    }
+__device__ __forceinline__ void pack_bytes(const uint32_t (&D)[8], uint32_t valid, uint32_t& cs,
+                                           uint32_t (&cm)[4], uint32_t& bg) {
     uint32_t lo[4], hi[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -554,7 +544,35 @@ __device__ __forceinline__ int pack_channel(const float (&xv)[PACK], float inv, 
     cm[1] = B3(T_XAND, L1, n, L0);
     cm[2] = B3(T_XAND, L2, n, L0 | L1);
     cm[3] = B3(T_XAND, L3, n, L0 | L1 | L2);
+}
+template <bool BIG>
+__device__ __forceinline__ int pack_channel(const float (&xv)[PACK], float inv, int qmax, float cu,
+                                            uint32_t valid, uint32_t& cs, uint32_t (&cm)[4], uint32_t& bg) {
+    const float qf = (float)qmax;
+    uint32_t D[8];
+    int off = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) D[k] = 0u;
+#pragma unroll
+    for (int r = 0; r < PACK; ++r) {
+        const float x = xv[r] * inv;
+        const float q = __builtin_amdgcn_fmed3f(rintf(x), -qf, qf);
+        const bool big = BIG && fabsf(x) == cu;
+        off |= (q != x && !big) ? 1 : 0;
+        D[r >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(q + (big ? 48.f : 16.f), r & 3, D[r >> 2]);
+    }
+    pack_bytes<BIG>(D, valid, cs, cm, bg);
     return off;
+}
+// the channel already as those bytes (ldpc_decode_awgn's byte channel, k_awgn_q8): q8 =
+// [packs][n_vars][8] words; always on the grid
+template <bool BIG>
+__device__ __forceinline__ void pack_channel_q8(const uint32_t* __restrict__ q8, int64_t pk, int nv, int v,
+                                                uint32_t valid, uint32_t& cs, uint32_t (&cm)[4], uint32_t& bg) {
+    const uint4* src = reinterpret_cast<const uint4*>(q8 + ((size_t)pk * nv + v) * 8);
+    const uint4 x0 = src[0], x1 = src[1];
+    const uint32_t D[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    pack_bytes<BIG>(D, valid, cs, cm, bg);
 }
 #ifndef BS_PACKT
 #define BS_PACKT 1      // pack_channel (A/B switch; 0: per-row bit insertion)
@@ -620,7 +638,10 @@ __device__ __forceinline__ int pack_channel(const float (&xv)[PACK], float inv, 
 // synd_bits outputs); the counters-only build is the one the bench and the sweeps run.
 // LB: the workgroup size bound (64 NW for the multi-chunk instances: the register budget is
 // 512 / (waves per SIMD), which a 1024-lane bound would fix at 128)
-template <int D, int DV, int LPC, int VPL, int CPL, bool UCN, bool BIG, bool PK, int WPE, bool XP, int LB>
+// Q8: the channel as bytes (in a.llr: ldpc_decode_awgn's byte channel) instead of float LLRs; a
+// build of its own (a run-time branch moved the register allocation of the whole kernel: C3's
+// spills 5 -> 9 VGPRs)
+template <int D, int DV, int LPC, int VPL, int CPL, bool UCN, bool BIG, bool PK, int WPE, bool XP, int LB, bool Q8>
 __global__ void __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_bs(BsArgs a) {
     static_assert(LPC == 2 || LPC == 4, "lanes per check");
@@ -713,6 +734,21 @@ k_bs(BsArgs a) {
     // issue variable u + 1's loads while converting variable u's (BS_LLR_ALL), so the fetch is
     // one round trip without holding every variable's 32 values at once
     float xv[VPL][PACK];
+    if constexpr (Q8) {
+        // byte channel (ldpc_decode_awgn): two 16-byte loads per variable, no conversion, never
+        // off the grid
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) {
+            cs[u] = 0u;
+            bg[u] = 0u;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) cm[u][p] = 0u;
+            const int v = var_of(u);
+            if (v >= 0 && !ABL(32))
+                pack_channel_q8<BIG>(reinterpret_cast<const uint32_t*>(a.llr), blockIdx.x, nv, v, valid, cs[u],
+                                     cm[u], bg[u]);
+        }
+    } else {
     if (var_of(0) >= 0 && !ABL(32)) {
 #pragma unroll
         for (int r = 0; r < PACK; ++r) xv[0][r] = llr_at(r, var_of(0));
@@ -753,6 +789,7 @@ k_bs(BsArgs a) {
 #pragma unroll
             for (int r = 0; r < PACK; ++r) xv[u1][r] = llr_at(r, vn);
         }
+    }
     }
     if (off) atomicOr(&RED[7], 1u);
     __syncthreads();
@@ -1307,11 +1344,11 @@ k_bs(BsArgs a) {
     }
 }
 
-template <int I, bool XP>
+template <int I, bool XP, bool Q8>
 int launch_bs_x(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     constexpr BsInst k = kBsInst[I];
     constexpr int LB = (k.VPL > 1 || k.CPL > 1) ? 64 * k.NW : 1024;
-    auto* fn = &k_bs<k.D, k.DV, k.LPC, k.VPL, k.CPL, k.UCN, k.BIG, k.PK, k.WPE, XP, LB>;
+    auto* fn = &k_bs<k.D, k.DV, k.LPC, k.VPL, k.CPL, k.UCN, k.BIG, k.PK, k.WPE, XP, LB, Q8>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -1322,13 +1359,15 @@ int launch_bs_x(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s)
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 template <int I>
-int launch_bs(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
-    return a.hdx ? launch_bs_x<I, true>(a, nblocks, nw, lds, s) : launch_bs_x<I, false>(a, nblocks, nw, lds, s);
+int launch_bs(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s, bool q8) {
+    // (the byte channel comes from ldpc_decode_awgn, which exports no hard bits)
+    if (a.hdx) return q8 ? LDPC_ERR_UNSUPPORTED : launch_bs_x<I, true, false>(a, nblocks, nw, lds, s);
+    return q8 ? launch_bs_x<I, false, true>(a, nblocks, nw, lds, s) : launch_bs_x<I, false, false>(a, nblocks, nw, lds, s);
 }
 
 // per-instance translation units (ldpc_bs_inst.hip, -DBS_INST=i)
 template <int I>
-int bs_launch(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s);
+int bs_launch(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s, bool q8);
 
 }  // namespace bs
 }  // namespace ldpc

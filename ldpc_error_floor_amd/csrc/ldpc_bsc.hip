@@ -46,7 +46,7 @@ constexpr BscInst kBscInst[] = {
 };
 
 struct BscArgs {
-    const float* llr;
+    const float* llr;            // (Q8 builds: the byte channel, as bsl's)
     int64_t B;
     int n_vars, n_checks, T, target_bits, cn_dmin, z;
     float inv, cu;
@@ -110,7 +110,7 @@ __device__ __forceinline__ void lds_dput(uint32_t addr, uint32_t x, uint32_t y) 
 // B1: every beta is 1 and one column table (a.beta_id, bcols 1: C5's flat weights), so the
 // channel term is Q(ch) itself and neither the beta table's operands nor the shortened-bit
 // planes are live (C5's instance: 124 VGPRs, no spills, against 128 and 10 spilled)
-template <int D, int DVH, int DVL, int LPC, int VPL, int CPL, int WPE, bool XP, int LB, bool MIX, bool B1>
+template <int D, int DVH, int DVL, int LPC, int VPL, int CPL, int WPE, bool XP, int LB, bool MIX, bool B1, bool Q8>
 __global__ void __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_bsc(BscArgs a) {
     constexpr int SB = (DVH * QMAX + QMAX <= 127) ? 8 : 9;
@@ -172,7 +172,10 @@ k_bsc(BscArgs a) {
 #pragma unroll
         for (int p = 0; p < 4; ++p) cm[u][p] = 0u;
         const int v = vv[u] < 0 ? -1 : (vv[u] & 0xFFFF);
-        if (v >= 0) {
+        if (Q8 && v >= 0) {                        // byte channel (ldpc_decode_awgn), a build of its own
+            pack_channel_q8<true>(reinterpret_cast<const uint32_t*>(a.llr), blockIdx.x, nv, v, valid, cs[u],
+                                  cm[u], bg[u]);
+        } else if (v >= 0) {
             // (buffer loads: a wave-uniform descriptor over the pack's rows, the lane's 4 v in
             // voffset, the row's 4 r nv in soffset: no 64-bit VGPR address per load, as bsl)
             const __amdgpu_buffer_rsrc_t llr_rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -836,10 +839,10 @@ static int bsc_tables(const DevGraph& g, const BscPlan& p, FusedWorkspace& ws, h
     return LDPC_OK;
 }
 
-template <int I, bool XP, bool B1>
+template <int I, bool XP, bool B1, bool Q8>
 static int bsc_launch1(const BscArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
     constexpr BscInst k = kBscInst[I];
-    auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE, XP, 64 * k.NW, k.MIX, B1>;
+    auto* fn = &k_bsc<k.D, k.DVH, k.DVL, k.LPC, k.VPL, k.CPL, k.WPE, XP, 64 * k.NW, k.MIX, B1, Q8>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -850,16 +853,29 @@ static int bsc_launch1(const BscArgs& a, int nblocks, int nw, size_t lds, hipStr
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 template <int I, bool XP>
-static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStream_t s) {
+static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStream_t s, bool q8) {
     // (LDPC_BSC_B1=0: the general channel path for a B1 decode too, an A/B switch)
     static const bool b1_on = [] { const char* e = getenv("LDPC_BSC_B1"); return !(e && atoi(e) == 0); }();
-    if (b1_on && a.beta_id && a.bcols == 1) return bsc_launch1<I, XP, true>(a, nblocks, nw, lds, s);
-    return bsc_launch1<I, XP, false>(a, nblocks, nw, lds, s);
+    const bool b1 = b1_on && a.beta_id && a.bcols == 1;
+    if constexpr (XP) {
+        // (the byte channel comes from ldpc_decode_awgn, which exports no hard bits)
+        if (q8) return LDPC_ERR_UNSUPPORTED;
+    } else {
+        if (q8) return b1 ? bsc_launch1<I, false, true, true>(a, nblocks, nw, lds, s)
+                            : bsc_launch1<I, false, false, true>(a, nblocks, nw, lds, s);
+    }
+    if (b1) return bsc_launch1<I, XP, true, false>(a, nblocks, nw, lds, s);
+    return bsc_launch1<I, XP, false, false>(a, nblocks, nw, lds, s);
 }
 
 }  // namespace bs
 
 using namespace bs;
+
+bool bsc_q8_ok(const DevGraph& g, int mode, bool ucn, float clip, int T, bool has_short) {
+    const BscPlan p = bsc_plan(g, mode, ucn, false, clip, T);
+    return p.ok && (!has_short || p.cu > 0.f);
+}
 
 bool bsc_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T) {
     return bsc_plan(g, mode, ucn, per_edge_w, clip, T).ok;
@@ -890,7 +906,8 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     const uint32_t* gt = reinterpret_cast<const uint32_t*>(ws.bs_graph);
     const int VNW = k.DVH + 1;
     BscArgs a{};
-    a.llr = llr;
+    const bool q8 = b.q8 != nullptr;
+    a.llr = q8 ? reinterpret_cast<const float*>(b.q8) : llr;
     a.B = b.B;
     a.n_vars = g.n_vars;
     a.n_checks = g.n_checks;
@@ -929,11 +946,11 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     a.off_blut = p.off_blut;
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
     switch (p.inst) {
-        case 1: return hdx ? bsc_launch<1, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<1, false>(a, nblocks, p.nw, p.lds, s);
-        case 2: return hdx ? bsc_launch<2, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<2, false>(a, nblocks, p.nw, p.lds, s);
-        case 3: return hdx ? bsc_launch<3, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<3, false>(a, nblocks, p.nw, p.lds, s);
-        case 4: return hdx ? bsc_launch<4, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<4, false>(a, nblocks, p.nw, p.lds, s);
-        default: return hdx ? bsc_launch<0, true>(a, nblocks, p.nw, p.lds, s) : bsc_launch<0, false>(a, nblocks, p.nw, p.lds, s);
+        case 1: return hdx ? bsc_launch<1, true>(a, nblocks, p.nw, p.lds, s, q8) : bsc_launch<1, false>(a, nblocks, p.nw, p.lds, s, q8);
+        case 2: return hdx ? bsc_launch<2, true>(a, nblocks, p.nw, p.lds, s, q8) : bsc_launch<2, false>(a, nblocks, p.nw, p.lds, s, q8);
+        case 3: return hdx ? bsc_launch<3, true>(a, nblocks, p.nw, p.lds, s, q8) : bsc_launch<3, false>(a, nblocks, p.nw, p.lds, s, q8);
+        case 4: return hdx ? bsc_launch<4, true>(a, nblocks, p.nw, p.lds, s, q8) : bsc_launch<4, false>(a, nblocks, p.nw, p.lds, s, q8);
+        default: return hdx ? bsc_launch<0, true>(a, nblocks, p.nw, p.lds, s, q8) : bsc_launch<0, false>(a, nblocks, p.nw, p.lds, s, q8);
     }
 }
 

@@ -45,6 +45,9 @@ struct ldpc_ctx {
     // LLR buffer for ldpc_decode_awgn when the kernel cannot generate in its prologue
     float* llr_scratch = nullptr;
     int64_t llr_scratch_n = 0;
+    // byte channel for the bit-sliced kernels ([packs][n_vars][32] u8, k_awgn_q8)
+    uint32_t* q8_scratch = nullptr;
+    int64_t q8_scratch_n = 0;
     char last_kernel[64] = {0};   // ldpc_ctx_last_kernel
 };
 
@@ -378,12 +381,14 @@ int ldpc_ctx_destroy(ldpc_ctx* c) {
     dev_free(c->wrong); dev_free(c->anypos); dev_free(c->biterr);
     fused_free(c->fused);
     if (c->llr_scratch) (void)hipFree(c->llr_scratch);
+    if (c->q8_scratch) (void)hipFree(c->q8_scratch);
     delete c;
     return LDPC_OK;
 }
 
 static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
-                       const ldpc_decode_outputs* o, void* stream, const AwgnParams* gen);
+                       const ldpc_decode_outputs* o, void* stream, const AwgnParams* gen,
+                       const uint32_t* q8 = nullptr);
 
 // LDPC_KERNEL_AUTO takes the fused kernel when it serves the request, except for sum-product:
 // its check update is bound by the tanh / atanh / divide VALU work, which flood's four codewords
@@ -406,8 +411,37 @@ int ldpc_decode_awgn(ldpc_ctx* c, int64_t B, const ldpc_decode_params* p,
                                    p->clip_llr);
     int st = decode_impl(c, nullptr, B, p, o, stream, &a);
     if (st != LDPC_ERR_UNSUPPORTED) return st;
-    // this kernel reads its LLRs: generate them into the context's buffer, then decode
     ldpc_graph* g = c->g;
+    // counters-only QMS decodes the bit-sliced kernels serve: the byte channel (k_awgn_q8, one
+    // byte per LLR in the layout the kernels' prologue packs into planes) instead of float LLRs
+    const int mode = mode_of(p->decoding_type, p->q_bit);
+    static const bool q8_on = [] { const char* e = getenv("LDPC_AWGN_Q8"); return !(e && atoi(e) == 0); }();
+    if (q8_on && p->decoding_type == LDPC_DEC_QMS && (!o || !o->app_all) && p->kernel != LDPC_KERNEL_FLOOD &&
+        fused_q8_ok(g->dev, mode, p->T, p->clip_llr, g->d_alpha_ucn != nullptr, g->per_edge_w != 0,
+                    ch->short_start > 0)) {
+        const int64_t nb = (B + 31) / 32 * 32 * (int64_t)g->h.N * g->h.z;       // bytes
+        if (c->q8_scratch_n < nb) {
+            DeviceGuard dg(g->device);
+            if (c->q8_scratch) (void)hipFree(c->q8_scratch);
+            c->q8_scratch = nullptr;
+            c->q8_scratch_n = 0;
+            if (hipMalloc(reinterpret_cast<void**>(&c->q8_scratch), (size_t)nb) != hipSuccess) {
+                (void)hipGetLastError();
+                return LDPC_ERR_OOM;
+            }
+            c->q8_scratch_n = nb;
+        }
+        {
+            DeviceGuard dg(g->device);
+            st = channel_q8(c->q8_scratch, B, g->h.N * g->h.z, a,
+                            mode == MODE_Q4 ? 7 : mode == MODE_Q3 ? 3 : 15,
+                            reinterpret_cast<hipStream_t>(stream));
+        }
+        if (st != LDPC_OK) return st;
+        st = decode_impl(c, nullptr, B, p, o, stream, nullptr, c->q8_scratch);
+        if (st != LDPC_ERR_UNSUPPORTED) return st;
+    }
+    // this kernel reads its LLRs: generate them into the context's buffer, then decode
     const int64_t n = c->B_max * (int64_t)g->h.N * g->h.z;
     if (c->llr_scratch_n < n) {
         DeviceGuard dg(g->device);
@@ -471,8 +505,9 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
 }
 
 static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
-                       const ldpc_decode_outputs* o, void* stream, const AwgnParams* gen) {
-    if (!c || !p || (!llr_dev && !gen)) return LDPC_ERR_ARG;
+                       const ldpc_decode_outputs* o, void* stream, const AwgnParams* gen,
+                       const uint32_t* q8) {
+    if (!c || !p || (!llr_dev && !gen && !q8)) return LDPC_ERR_ARG;
     ldpc_graph* g = c->g;
     if (!g->d_alpha || !g->d_beta) return LDPC_ERR_STATE;
     int mode = -1;
@@ -508,6 +543,7 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     if (kern != LDPC_KERNEL_FLOOD && kern != LDPC_KERNEL_FUSED) return LDPC_ERR_ARG;
     if (kern == LDPC_KERNEL_FUSED && !fok) return LDPC_ERR_UNSUPPORTED;
     if (gen && (kern != LDPC_KERNEL_FUSED || fl)) return LDPC_ERR_UNSUPPORTED;   // caller falls back
+    if (q8 && (kern != LDPC_KERNEL_FUSED || fl)) return LDPC_ERR_UNSUPPORTED;
 
     const int ntiles = (int)((B + TILE - 1) / TILE);
     const bool count = out.counters || out.frame_flags || out.iter_wrong;
@@ -528,6 +564,7 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     b.biterr = c->biterr;
     b.awgn = gen;
     b.iter_wrong = out.iter_wrong;
+    b.q8 = q8;
     if (out.iter_wrong &&
         hipMemsetAsync(out.iter_wrong, 0, (size_t)p->T * ((B + 31) / 32) * sizeof(uint32_t), s) != hipSuccess)
         return LDPC_ERR_HIP;

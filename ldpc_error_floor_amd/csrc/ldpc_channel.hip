@@ -2,17 +2,16 @@
 // The generator itself (model, Philox stream, precision) is ldpc_awgn.h, shared with the
 // fused decoder's in-prologue channel.
 #include <algorithm>
-#include <type_traits>
 
 #include "ldpc_awgn.h"
 #include "ldpc_internal.h"
 
 namespace ldpc {
 
-// one (codeword, element pair) per thread, grid-strided.  The index -> (codeword, pair) split is
+// float modes: one (codeword, element pair) per thread, grid-strided.  The index -> (codeword, pair) split is
 // a 32-bit division whenever the batch has fewer than 2^32 pairs (a 64-bit one is a long
 // emulated sequence), and an even row length stores the pair as one 8-byte write.
-template <bool WIDE, int QB>
+template <bool WIDE>
 __global__ void __launch_bounds__(256) k_awgn(float* __restrict__ out, int64_t B, int n_vars,
                                               AwgnParams a, int pairs8) {
     const int npairs = (n_vars + 1) / 2;
@@ -31,7 +30,7 @@ __global__ void __launch_bounds__(256) k_awgn(float* __restrict__ out, int64_t B
             pr = (int)((uint32_t)id - q * (uint32_t)npairs);
         }
         float l[2];
-        awgn_pair<QB>(a, b, pr, l);
+        awgn_pair(a, b, pr, l);
         float* row = out + b * n_vars;
         if (even) {
             *reinterpret_cast<float2*>(row + 2 * pr) = make_float2(l[0], l[1]);
@@ -39,6 +38,98 @@ __global__ void __launch_bounds__(256) k_awgn(float* __restrict__ out, int64_t B
             row[2 * pr] = l[0];
             if (2 * pr + 1 < n_vars) row[2 * pr + 1] = l[1];
         }
+    }
+}
+
+// QMS: Box-Muller's replacement.  One thread per (global codeword quad, variable); variable
+// fastest, so each of the four row stores is coalesced across the wave.  The bucket table and
+// thresholds are built in LDS by each workgroup (awgn_bucket_fill, ~2 KB).
+template <bool WIDE>
+__global__ void __launch_bounds__(256) k_awgn_qf(float* __restrict__ out, int64_t B, int n_vars,
+                                                 AwgnParams a) {
+    __shared__ uint16_t bucket[1 << AWGN_KB];
+    __shared__ uint32_t thi[AWGN_NB_MAX], tlo[AWGN_NB_MAX];
+    __shared__ float val[AWGN_NB_MAX + 1];
+    awgn_bucket_fill(a, bucket, thi, tlo, threadIdx.x, blockDim.x);
+    if (threadIdx.x <= (unsigned)a.nb) val[threadIdx.x] = a.val[threadIdx.x];
+    __syncthreads();
+    const uint64_t g0 = (uint64_t)a.offset;
+    const uint64_t q0 = g0 >> 2;
+    const int64_t nq = (int64_t)(((g0 + (uint64_t)B - 1) >> 2) - q0 + 1);
+    const int64_t total = nq * n_vars;
+    for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
+         id += (int64_t)gridDim.x * blockDim.x) {
+        int64_t m;
+        int v;
+        if (WIDE) {
+            m = id / n_vars;
+            v = (int)(id - m * n_vars);
+        } else {
+            const uint32_t q = (uint32_t)id / (uint32_t)n_vars;
+            m = q;
+            v = (int)((uint32_t)id - q * (uint32_t)n_vars);
+        }
+        const uint64_t gq = q0 + (uint64_t)m;
+        const int64_t bq = (int64_t)(gq * 4 - g0);          // batch index of the quad's word 0
+        const int fx = awgn_fixed(a, v + 1);
+        float l[4];
+        if (fx == 0) {
+            int lv[4];
+            awgn_levels4(a, bucket, thi, tlo, (uint32_t)v, gq, lv);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) l[j] = val[lv[j]];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) l[j] = fx == 1 ? 0.0f : -a.clip;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (bq + j >= 0 && bq + j < B) out[(bq + j) * n_vars + v] = l[j];
+    }
+}
+
+// QMS bytes for the bit-sliced decoders (ldpc_decode_awgn): [packs][n_vars][32] u8, byte r of
+// (pack, v) = grid value + 16 of codeword 32 pack + r (+ 32 on a shortened bit: the BIG
+// instances' marker, pack_channel) — the bytes pack_channel builds from float LLRs, 576 B per
+// wman codeword instead of 2,304.  One thread per (pack, variable, codeword quad), the quad
+// index fastest: a wave stores 8 variables x 32 bytes, contiguous.  Rows past B are generated
+// too (the decoder masks them).
+__global__ void __launch_bounds__(256) k_awgn_q8(uint32_t* __restrict__ out, int64_t npk, int n_vars,
+                                                 AwgnParams a, int qmax) {
+    __shared__ uint16_t bucket[1 << AWGN_KB];
+    __shared__ uint32_t thi[AWGN_NB_MAX], tlo[AWGN_NB_MAX];
+    awgn_bucket_fill(a, bucket, thi, tlo, threadIdx.x, blockDim.x);
+    __syncthreads();
+    const uint64_t g0 = (uint64_t)a.offset;
+    const int sh = (int)(g0 & 3);                            // the batch's first quad offset
+    const int64_t total = npk * n_vars * 8;
+    const uint32_t boff = (uint32_t)(16 + a.kmin);           // byte of level 0
+    for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
+         id += (int64_t)gridDim.x * blockDim.x) {
+        const int i = (int)(id & 7);
+        const int64_t pv = id >> 3;
+        const int64_t pk = pv / n_vars;
+        const int v = (int)(pv - pk * n_vars);
+        const int fx = awgn_fixed(a, v + 1);
+        uint32_t w;
+        if (fx == 1) {
+            w = 0x10101010u;
+        } else if (fx == 2) {
+            w = (uint32_t)(48 - qmax) * 0x01010101u;
+        } else {
+            const uint64_t gb = g0 + (uint64_t)(pk * 32 + 4 * i);
+            int la[4], lb[4];
+            awgn_levels4(a, bucket, thi, tlo, (uint32_t)v, gb >> 2, la);
+            if (sh) awgn_levels4(a, bucket, thi, tlo, (uint32_t)v, (gb >> 2) + 1, lb);
+            w = 0u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int x = sh + k;
+                const int lv = x < 4 ? la[x & 3] : lb[x & 3];
+                w |= ((uint32_t)lv + boff) << (8 * k);
+            }
+        }
+        out[id] = w;
     }
 }
 
@@ -57,6 +148,7 @@ AwgnParams make_awgn(double sigma, uint64_t seed, int64_t offset, int decoding_t
     a.pe = pe;
     a.ss = ss;
     a.se = se;
+    if (decoding_type == LDPC_DEC_QMS) host::awgn_qms_levels(sigma, q_bit, &a.nb, &a.kmin, a.thr_hi, a.thr_lo, a.val);
     return a;
 }
 
@@ -72,28 +164,42 @@ extern "C" int ldpc_channel_awgn(float* llr_dev, int64_t B, int32_t n_vars, doub
                                               punct_start, punct_end, short_start, short_end,
                                               clip_llr);
     if (chk != LDPC_OK) return chk;
-    const int64_t total = B * ((n_vars + 1) / 2);
-    const unsigned grid = (unsigned)std::min<int64_t>(8192, (total + 255) / 256);
     const ldpc::AwgnParams a = ldpc::make_awgn(sigma, seed, offset, decoding_type, q_bit,
                                                punct_start, punct_end, short_start, short_end,
                                                clip_llr);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (decoding_type == LDPC_DEC_QMS) {
+        // the level sampler (ldpc_awgn.h): one thread per (codeword quad, variable)
+        const int64_t nq = (int64_t)((((uint64_t)offset + (uint64_t)B - 1) >> 2) - ((uint64_t)offset >> 2) + 1);
+        const int64_t total = nq * n_vars;
+        const unsigned grid = (unsigned)std::min<int64_t>(8192, (total + 255) / 256);
+        if (total + (int64_t)grid * 256 >= ((int64_t)1 << 32))
+            hipLaunchKernelGGL((ldpc::k_awgn_qf<true>), dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a);
+        else
+            hipLaunchKernelGGL((ldpc::k_awgn_qf<false>), dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a);
+        return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+    }
+    // float modes: Box-Muller per element pair
+    const int64_t total = B * ((n_vars + 1) / 2);
+    const unsigned grid = (unsigned)std::min<int64_t>(8192, (total + 255) / 256);
     // 8-byte pair stores: even rows in an 8-byte aligned buffer
     const int pairs8 = ((n_vars & 1) == 0 && (reinterpret_cast<uintptr_t>(llr_dev) & 7) == 0) ? 1 : 0;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const bool wide = total + (int64_t)grid * 256 >= ((int64_t)1 << 32);
-    const int qb = decoding_type == LDPC_DEC_QMS ? q_bit : 0;
-    auto go = [&](auto qc) {
-        constexpr int Q = decltype(qc)::value;
-        if (wide) hipLaunchKernelGGL((ldpc::k_awgn<true, Q>), dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a, pairs8);
-        else hipLaunchKernelGGL((ldpc::k_awgn<false, Q>), dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a, pairs8);
-    };
-    switch (qb) {       // one build per quantizer (check_channel has validated q_bit)
-        case 6: go(std::integral_constant<int, 6>{}); break;
-        case 5: go(std::integral_constant<int, 5>{}); break;
-        case -5: go(std::integral_constant<int, -5>{}); break;
-        case 4: go(std::integral_constant<int, 4>{}); break;
-        case 3: go(std::integral_constant<int, 3>{}); break;
-        default: go(std::integral_constant<int, 0>{}); break;
-    }
+    if (wide) hipLaunchKernelGGL(ldpc::k_awgn<true>, dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a, pairs8);
+    else hipLaunchKernelGGL(ldpc::k_awgn<false>, dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a, pairs8);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
+
+namespace ldpc {
+
+// ldpc_decode_awgn's byte channel: q8 [ceil(B/32)][n_vars][8] words (k_awgn_q8)
+int channel_q8(uint32_t* q8, int64_t B, int n_vars, const AwgnParams& a, int qmax, hipStream_t s) {
+    if (a.decoding_type != LDPC_DEC_QMS || a.nb <= 0) return LDPC_ERR_ARG;
+    const int64_t npk = (B + 31) / 32;
+    const int64_t total = npk * n_vars * 8;
+    const unsigned grid = (unsigned)std::min<int64_t>(8192, (total + 255) / 256);
+    hipLaunchKernelGGL(k_awgn_q8, dim3(grid), dim3(256), 0, s, q8, npk, n_vars, a, qmax);
+    return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+}
+
+}  // namespace ldpc

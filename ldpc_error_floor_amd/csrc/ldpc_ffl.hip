@@ -306,7 +306,6 @@ template <int CW, bool UCN>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(8)))
 k_ffs(FflArgs a) {
     constexpr int G = 64 / CW;
-    constexpr float SP_EPS = 1.0f - 1e-7f;               // as flood (Main_Functions.py:243)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* TV = reinterpret_cast<float*>(smem + a.off_tv);
     float* C2V = reinterpret_cast<float*>(smem + a.off_rec);
@@ -361,7 +360,6 @@ k_ffs(FflArgs a) {
             const bool act = h < z;
             const int hh = act ? h : z - 1;
             const int r0 = a.row_ptr[i], deg = a.row_ptr[i + 1] - r0;
-            float P = 1.f, L = 0.f;
             uint32_t syn = 0u;
             for (int k0 = 0; k0 < deg; k0 += 4) {
                 float tv[4], cv[4];
@@ -380,11 +378,7 @@ k_ffs(FflArgs a) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     if (k0 + u < deg) {
-                        const float x = fminf(fmaxf(tv[u] - cv[u], -a.clip), a.clip);      // :227
-                        float y = tanhf(-0.5f * x);
-                        y = (fabsf(y) > 0.f) ? y : 1.f;                                   // :240
-                        P *= y;
-                        L += logf(fabsf(y));
+                        const float y = sp_t(fminf(fmaxf(tv[u] - cv[u], -a.clip), a.clip));   // :227
                         if (act) C2V[((r0 + k0 + u) * z + hh) * CW + w] = y;
                         if (UCN) syn ^= hdv[u];
                     }
@@ -392,20 +386,15 @@ k_ffs(FflArgs a) {
             }
             const float* at = a.alpha + (size_t)t * a.E + r0;
             const float* au = UCN ? a.alpha_ucn + (size_t)t * a.E + r0 : nullptr;
-            const bool big = fabsf(P) >= 1.17549435e-38f;
+            // edge k's product over the others in the oracle's order (as flood's cn_update_sp)
+            float pre = 1.f;
             for (int k = 0; k < deg; ++k) {
                 const int slot = ((r0 + k) * z + hh) * CW + w;
                 const float y = act ? C2V[slot] : 1.f;
-                float others;
-                if (big) {
-                    others = P / y;
-                } else {                                   // product underflowed: log domain
-                    const bool neg = (P < 0.f) != (y < 0.f);
-                    const float m = expf(L - logf(fabsf(y)));
-                    others = neg ? -m : m;
-                }
-                others = fminf(fmaxf(others, -SP_EPS), SP_EPS);                         // :243
-                const float o = -2.0f * atanhf(others);                                // :244
+                float others = pre;
+                for (int j = k + 1; j < deg; ++j) others *= act ? C2V[((r0 + j) * z + hh) * CW + w] : 1.f;
+                pre *= y;
+                const float o = sp_o(others);
                 const float wt = (UCN && (syn & 1u)) ? au[k] : at[k];
                 float x = fabsf(o) * wt;
                 x = (x > 0.f) ? x : 0.f;                                               // :308

@@ -81,21 +81,17 @@ __global__ void __launch_bounds__(256) k_prologue(DevGraph g, Bufs p, const floa
 // ----------------------------------------------------------------------------------------
 // check-node update (Main_Functions.py:213-316)
 // Sum-product check update (decoding_type 0, Main_Functions.py:238-245), 4 codewords per
-// lane like the min-sum path.  t_k = tanh(-x_k/2) with t == 0 -> 1 (the reference's masking
-// also swallows exact-zero messages); the product over the other edges is P / t_k, with P the
-// product over all edges, or exp(sum of the others' log|t|) when P is not a normal float;
-// o = -2 atanh(clip(., +-(1 - 1e-7))); then weight, relu, clip and sign as the min-sum path.
-// Pass 1 parks t_k in the edge's C->V slot (after reading the old message there).
+// lane like the min-sum path, in the oracle's float32 order (sp_t / sp_o, ldpc_internal.h):
+// pass 1 parks t_k in the edge's C->V slot (after reading the old message there); pass 2 takes
+// edge k's product over the others as (t_0 ... t_{k-1}) t_{k+1} ... t_{d-1} left to right
+// (the running prefix, then the later slots, which still hold t), writes its message into slot
+// k, then extends the prefix with t_k; then weight, relu, clip and sign as the min-sum path.
 template <bool UCN>
 __device__ __forceinline__ void cn_update_sp(const DevGraph& g, const Bufs& p, int t, int64_t tile,
                                              int c, int lane, int i, int h, int r0, int deg,
                                              const float* Tt, float* Ct) {
     (void)c; (void)i;
-    constexpr float SP_EPS = 1.0f - 1e-7f;            // float32(1 - 1e-7) = 0.99999988
-    float P[4], L[4];
     uint32_t syn = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { P[q] = 1.f; L[q] = 0.f; }
     for (int k = 0; k < deg; ++k) {
         const int pe = r0 + k;
         const int s = h + g.pe_shift[pe];
@@ -104,14 +100,8 @@ __device__ __forceinline__ void cn_update_sp(const DevGraph& g, const Bufs& p, i
         const float4 cv = (t == 0) ? make_float4(0.f, 0.f, 0.f, 0.f) : ld4(Ct + (size_t)k * TILE);
         float th[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float x = fminf(fmaxf(f4(tv, q) - f4(cv, q), -p.clip), p.clip);   // :227
-            float y = tanhf(-0.5f * x);
-            y = (fabsf(y) > 0.f) ? y : 1.f;                                        // :240
-            th[q] = y;
-            P[q] *= y;
-            L[q] += logf(fabsf(y));
-        }
+        for (int q = 0; q < 4; ++q)
+            th[q] = sp_t(fminf(fmaxf(f4(tv, q) - f4(cv, q), -p.clip), p.clip));   // :227
         st4(Ct + (size_t)k * TILE, make_float4(th[0], th[1], th[2], th[3]));
         if (UCN) {
             const uint64_t* hw = p.hd + hd_index(p, t - 1, tile, v);
@@ -121,29 +111,27 @@ __device__ __forceinline__ void cn_update_sp(const DevGraph& g, const Bufs& p, i
     }
     const float* at = p.alpha + (size_t)t * g.E;
     const float* au = UCN ? p.alpha_ucn + (size_t)t * g.E : nullptr;
+    float pre[4] = {1.f, 1.f, 1.f, 1.f};
     for (int k = 0; k < deg; ++k) {
         const float a = at[r0 + k];
         const float u = UCN ? au[r0 + k] : 0.f;
         const float4 tk = ld4(Ct + (size_t)k * TILE);
+        float others[4] = {pre[0], pre[1], pre[2], pre[3]};
+        for (int j = k + 1; j < deg; ++j) {
+            const float4 tj = ld4(Ct + (size_t)j * TILE);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) others[q] *= f4(tj, q);
+        }
         float r[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const float y = f4(tk, q);
-            float others;
-            if (fabsf(P[q]) >= 1.17549435e-38f) {
-                others = P[q] / y;
-            } else {                                   // product underflowed: log domain
-                const bool neg = (P[q] < 0.f) != (y < 0.f);
-                const float m = expf(L[q] - logf(fabsf(y)));
-                others = neg ? -m : m;
-            }
-            others = fminf(fmaxf(others, -SP_EPS), SP_EPS);                        // :243
-            const float o = -2.0f * atanhf(others);                               // :244
+            const float o = sp_o(others[q]);
             const float w = (UCN && ((syn >> q) & 1)) ? u : a;
             float x = fabsf(o) * w;
             x = (x > 0.f) ? x : 0.f;                                              // :308
             x = fminf(fmaxf(x, -p.clip), p.clip);                                 // :313
             r[q] = (o > 0.f) ? x : ((o < 0.f) ? -x : 0.f);                        // :316
+            pre[q] *= f4(tk, q);
         }
         st4(Ct + (size_t)k * TILE, make_float4(r[0], r[1], r[2], r[3]));
     }

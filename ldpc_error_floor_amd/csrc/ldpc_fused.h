@@ -59,6 +59,12 @@ const char* bs_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_
 // word (t, pack, v) = codeword 32 pack + r; the export build of the kernel)
 int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
               bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, uint32_t* hdx, hipStream_t s);
+// the byte channel (Bufs::q8) serves this counters-only decode: the bit-sliced kernel applies and,
+// with shortened bits in the channel, has the shortened-bit marker (a BIG instance)
+bool bs_q8_ok(const DevGraph& g, int mode, bool ucn, float clip, int T, bool has_short);
+bool bsc_q8_ok(const DevGraph& g, int mode, bool ucn, float clip, int T, bool has_short);
+// (fused_decode with it: the bit-sliced kernel or LDPC_ERR_UNSUPPORTED)
+bool fused_q8_ok(const DevGraph& g, int mode, int T, float clip, bool ucn, bool per_edge_w, bool has_short);
 // compressed bit-sliced kernel (ldpc_bsc.hip): the graphs whose per-edge slots exceed the LDS
 bool bsc_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T);
 const char* bsc_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T);

@@ -61,6 +61,11 @@ const char* fused_kernel_name(const DevGraph& g, int mode, int T, float clip_llr
     return fused5_shape_name(g, T);
 }
 
+bool fused_q8_ok(const DevGraph& g, int mode, int T, float clip, bool ucn, bool per_edge_w, bool has_short) {
+    return fused_supported(g, mode, T, clip) && use_bs(g, mode, T, ucn, per_edge_w, clip) &&
+           bs_q8_ok(g, mode, ucn, clip, T, has_short);
+}
+
 int64_t fused_bytes_per_cw(const DevGraph& g, int T) {
     (void)T;
     // compulsory: the channel LLRs are read once; outputs are counters only
@@ -82,6 +87,8 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
     // counters / frame flags / bit exports without APP: the bit-sliced kernel when it applies
     // (its export build stores every iteration's hard decisions, bit-sliced, in ws.hdx)
     const bool bs = !b.app_out && !b.awgn && use_bs(g, mode, b.T, ucn, per_edge_w != 0, b.clip);
+    if (b.q8 && !bs) return LDPC_ERR_UNSUPPORTED;          // the byte channel is the bit-sliced kernels'
+
     ws.bits_packed = false;
     if (want_bits) {
         const size_t elems = (size_t)(T_max + 1) * ntiles_max * g.n_vars * 4;
@@ -136,6 +143,7 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
         if (st != LDPC_OK) return st;
         ws.last_kernel = fused_kernel_name(g, mode, b.T, b.clip, ucn, per_edge_w != 0);
         ws.bits_packed = want_bits;
+        if (b.q8) return LDPC_OK;      // byte channel: every pack is on the grid, nothing to fix up
         // test hook: LDPC_BS_FIXUP=0 skips the v5 fixup, so a test can tell that a batch was
         // decoded by the bit-sliced kernel alone (flagged packs then contribute nothing).  Read
         // per decode (a test sets it after other decodes ran in the same process).

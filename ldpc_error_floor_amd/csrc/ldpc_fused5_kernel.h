@@ -306,14 +306,37 @@ f5_block(const F5Args& a, const float* __restrict__ alpha, const float* __restri
         float* scr = reinterpret_cast<float*>(W);            // [CW][nv+1]
         const int rl = nv + 1;
         if (a.gen) {
-            // in-kernel channel: the same generator as ldpc_channel_awgn (ldpc_awgn.h)
-            const int npairs = (nv + 1) >> 1;
-            for (int i = tid; i < CW * npairs; i += NT) {
-                const int r = i / npairs, pr = i - r * npairs;
-                float l[2] = {0.f, 0.f};
-                if (r < nvalid) awgn_pair(a.awgn, b0 + r, pr, l);
-                scr[r * rl + 2 * pr] = l[0];
-                if (2 * pr + 1 < nv) scr[r * rl + 2 * pr + 1] = l[1];
+            // in-kernel channel: the same QMS level sampler as ldpc_channel_awgn (ldpc_awgn.h),
+            // its bucket table in the CH region (written only after the scratch is consumed)
+            const AwgnParams& g = a.awgn;
+            const uint64_t g0 = (uint64_t)g.offset + (uint64_t)b0;    // global index of row 0
+            if ((size_t)total * 4 >= (2u << AWGN_KB) + (3 * AWGN_NB_MAX + 1) * 4) {
+                uint16_t* bk = reinterpret_cast<uint16_t*>(CH);
+                uint32_t* th = reinterpret_cast<uint32_t*>(CH) + (1 << AWGN_KB) / 2;
+                uint32_t* tl = th + AWGN_NB_MAX;
+                float* vl = reinterpret_cast<float*>(tl + AWGN_NB_MAX);
+                awgn_bucket_fill(g, bk, th, tl, tid, NT);
+                if (tid <= g.nb) vl[tid] = g.val[tid];
+                __syncthreads();
+                const int sh = (int)(g0 & 3);
+                const int nq = (CW + sh + 3) >> 2;                     // quads covering the rows
+                for (int i = tid; i < nq * nv; i += NT) {
+                    const int m = i / nv, v = i - m * nv;
+                    const int fx = awgn_fixed(g, v + 1);
+                    int lv[4] = {0, 0, 0, 0};
+                    if (fx == 0) awgn_levels4(g, bk, th, tl, (uint32_t)v, (g0 >> 2) + (uint64_t)m, lv);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int r = 4 * m + j - sh;
+                        if (r < 0 || r >= CW) continue;
+                        scr[r * rl + v] = r >= nvalid ? 0.f : fx == 0 ? vl[lv[j]] : fx == 1 ? 0.f : -g.clip;
+                    }
+                }
+            } else {                   // tiny graphs: a threshold scan per element
+                for (int i = tid; i < CW * nv; i += NT) {
+                    const int r = i / nv, v = i - r * nv;
+                    scr[r * rl + v] = r < nvalid ? awgn_qms_elem(g, g0 + (uint64_t)r, v) : 0.f;
+                }
             }
         } else
         for (int v0 = 0; v0 < nv; v0 += NT) {

@@ -230,5 +230,40 @@ std::pair<int, int> order_variable_edges(std::vector<uint32_t>& A, const std::ve
     return {before, after};
 }
 
+void awgn_qms_levels(double sigma, int q_bit, int* nb, int* kmin, uint32_t* thr_hi, uint32_t* thr_lo,
+                     float* val) {
+    double u, cmax;                       // grid step and clip of Cal_MSA_Q
+    switch (q_bit) {
+        case 6: u = 1.0; cmax = 15.5; break;
+        case 5: u = 0.5; cmax = 7.5; break;
+        case -5: u = 1.0; cmax = 15.0; break;
+        case 4: u = 1.0; cmax = 7.0; break;
+        default: u = 2.0; cmax = 6.0; break;
+    }
+    const int K = (int)std::ceil(cmax / u) + 1;
+    auto Q = [&](int k) { return std::min(std::max(k * u, -cmax), cmax); };
+    int n = 0;
+    val[0] = (float)Q(-K);
+    const double s2 = sigma * sigma;
+    for (int k = -K + 1; k <= K; ++k) {
+        if (Q(k) == Q(k - 1)) continue;
+        const double x = (k - 0.5) * u;                       // rounding boundary, LLR units
+        const double nz = (x * s2 * 0.5 + 1.0) / sigma;       // noise value at the boundary
+        uint64_t T;
+        if (nz < 0.0) {
+            T = (uint64_t)std::ldexp(0.5 * std::erfc(-nz * 0.7071067811865476), 64);
+        } else {
+            const uint64_t tail = (uint64_t)std::ldexp(0.5 * std::erfc(nz * 0.7071067811865476), 64);
+            T = tail == 0 ? ~(uint64_t)0 : (uint64_t)0 - tail;
+        }
+        thr_hi[n] = (uint32_t)(T >> 32);
+        thr_lo[n] = (uint32_t)T;
+        ++n;
+        val[n] = (float)Q(k);
+    }
+    *nb = n;
+    *kmin = q_bit == 6 ? 0 : (int)std::lround(-cmax / u);
+}
+
 }  // namespace host
 }  // namespace ldpc

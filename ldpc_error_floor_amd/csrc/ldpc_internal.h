@@ -58,7 +58,27 @@ struct Bufs {
                                // prologue instead of reading them (fused v5 only), or null
     uint32_t* iter_wrong;      // [T][ceil(B/32)] per-iteration frame-error words, or null
                                // (ldpc_decode_outputs::iter_wrong; zeroed before the decode)
+    const uint32_t* q8;        // the channel as bytes [packs][n_vars][8] words (k_awgn_q8) for the
+                               // bit-sliced kernels, instead of float LLRs, or null
 };
+
+// Sum-product check update pieces (decoding_type 0, Main_Functions.py:238-245) shared by flood
+// and the fused SP kernel, in the oracle's float32 arithmetic (oracle/nms_oracle.py _sp_check):
+// t = fl32(tanh(fl32(-x / 2))) with t == 0 -> 1 (the reference's masking also swallows exact-
+// zero messages), the product over the other edges in edge order in float32 (the caller's
+// prefix x later edges), o = -2 fl32(atanh(clip(product, +-fl32(1 - 1e-7)))).  tanh and atanh
+// are evaluated in float64 and rounded once, so they are the correctly rounded float32 values
+// (the float32 library functions were a few ulps off, which atanh near the clip amplified to
+// differences up to ~0.7 in an APP against the oracle).
+__device__ __forceinline__ float sp_t(float x) {
+    const float y = (float)tanh((double)(-0.5f * x));
+    return (y != 0.f) ? y : 1.f;                                               // :240
+}
+__device__ __forceinline__ float sp_o(float others) {
+    constexpr float SP_EPS = 1.0f - 1e-7f;            // float32(1 - 1e-7) = 0.99999988
+    others = fminf(fmaxf(others, -SP_EPS), SP_EPS);                            // :243
+    return -2.0f * (float)atanh((double)others);                               // :244
+}
 
 // per-iteration frame-error words (ldpc_decode_outputs::iter_wrong) of one block of codewords
 // b0 .. b0 + CW - 1 (CW a power of two <= 64, b0 a multiple of CW) at iteration t: `m` holds

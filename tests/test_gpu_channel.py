@@ -1,9 +1,10 @@
 """The on-GPU AWGN channel (ldpc_channel_awgn / ldpc_decode_awgn, csrc/ldpc_awgn.h) against
 its CPU restatement oracle/philox_oracle.py (GPU only).  The oracle's Philox is pinned by the
-Random123 known-answer vectors (tests/test_philox_oracle.py); this pins the device stream to
-it: quantized LLRs bit-exact (except within ulps of a grid rounding boundary, where the device
-logf / sincospif may round the other way), float LLRs within a few ulps, puncture / shorten
-exact, and the in-decoder generation equal to decoding the oracle's LLRs."""
+Random123 known-answer vectors and its QMS level probabilities by the channel model
+(tests/test_philox_oracle.py); this pins the device streams to it: QMS LLRs (the level
+sampler) bit-exact for every q_bit and offset, float LLRs (Box-Muller) within a few ulps,
+puncture / shorten exact, and every in-decoder generation (v5 prologue, the bit-sliced
+kernels' byte channel) equal to decoding the oracle's LLRs."""
 import os
 
 import numpy as np
@@ -11,7 +12,7 @@ import pytest
 
 from conftest import ROOT
 from oracle import nms_oracle
-from oracle.philox_oracle import awgn_llr, near_boundary
+from oracle.philox_oracle import awgn_llr
 
 pytestmark = pytest.mark.gpu
 DATA = os.path.join(ROOT, "ldpc_error_floor_amd", "data")
@@ -28,17 +29,22 @@ def _decoder(device, graph, z, dt, q, T=8):
 
 
 @pytest.mark.parametrize("q", [5, 6, -5, 4, 3])
-def test_qms_channel_bit_exact(cuda_device, q):
+@pytest.mark.parametrize("off", [123456, 123457])
+def test_qms_channel_bit_exact(cuda_device, q, off):
     dec = _decoder(cuda_device, "wman_N0576_R34_z24", 24, 2, q)
-    B, off, seed, sigma = 4096, 123457, (1 << 33) + 1076, 0.61
+    B, seed, sigma = 4099, (1 << 33) + 1076, 0.61
     got = dec.awgn(B, sigma, seed, offset=off).cpu().numpy()
-    ref, raw = awgn_llr(B, dec.n_vars, sigma, seed, off, decoding_type=2, q_bit=q)
-    edge = near_boundary(raw, q)
-    assert edge.mean() < 1e-3
-    assert np.array_equal(got[~edge], ref[~edge])
-    # at a boundary the two roundings are adjacent grid values
-    step = {6: 1.0, 5: 0.5, -5: 1.0, 4: 1.0, 3: 2.0}[q]
-    assert np.all(np.abs(got[edge] - ref[edge]) <= step)
+    ref, _ = awgn_llr(B, dec.n_vars, sigma, seed, off, decoding_type=2, q_bit=q)
+    assert np.array_equal(got, ref)
+
+
+def test_qms_channel_puncture_shorten_bit_exact(cuda_device):
+    dec = _decoder(cuda_device, G5, 64, 2, 5)
+    B, off, seed, sigma = 1000, 77, 9, 0.7943282
+    got = dec.awgn(B, sigma, seed, offset=off, punct=(1, 128), short=(513, 640)).cpu().numpy()
+    ref, _ = awgn_llr(B, dec.n_vars, sigma, seed, off, decoding_type=2, q_bit=5, punct=(1, 128),
+                      short=(513, 640))
+    assert np.array_equal(got, ref)
 
 
 @pytest.mark.parametrize("dt", [1, 0])
@@ -57,24 +63,59 @@ def test_float_channel_within_ulps_puncture_shorten(cuda_device, dt):
 
 
 def test_decode_awgn_equals_decoding_oracle_llrs(cuda_device):
-    """In-kernel channel (fused v5 prologue) == decoding the oracle's LLRs (flood and fused),
-    and the oracle decoder agrees, on codewords away from grid boundaries."""
+    """In-kernel channel (the v5 prologue with an APP export, the bit-sliced kernels' byte
+    channel for counters) == decoding the oracle's LLRs (flood and fused), and the oracle
+    decoder agrees."""
     import torch
     from ldpc_error_floor_amd.code import CodeParams
     dec = _decoder(cuda_device, "wman_N0576_R34_z24", 24, 2, 5, T=20)
     sigma = float(CodeParams(dec.graph.proto, 24).sigma(2.0))
-    B, off, seed = 2000, 1 << 20, 4242
-    ref, raw = awgn_llr(B, dec.n_vars, sigma, seed, off, decoding_type=2, q_bit=5)
-    clean = ~near_boundary(raw, 5).any(axis=1)
-    assert clean.mean() > 0.5
+    B, off, seed = 2000, (1 << 20) + 2, 4242
+    ref, _ = awgn_llr(B, dec.n_vars, sigma, seed, off, decoding_type=2, q_bit=5)
     ref_t = torch.from_numpy(ref).to(cuda_device)
     for k in ("fused", "flood"):
-        want = dec.decode(ref_t, app=False, counters=True, flags=True, kernel=k)
-        got = dec.decode_awgn(B, sigma, seed, offset=off, counters=True, flags=True, kernel=k)
-        f_got, f_want = got.flags.cpu().numpy(), want.flags.cpu().numpy()
-        assert np.array_equal(f_got[clean], f_want[clean]), k
+        want = dec.decode(ref_t, app=False, counters=True, flags=True, kernel=k, iter_wrong=True)
+        got = dec.decode_awgn(B, sigma, seed, offset=off, counters=True, flags=True, kernel=k,
+                              iter_wrong=True)
+        for a, b in ((got.flags, want.flags), (got.counters, want.counters),
+                     (got.iter_wrong, want.iter_wrong)):
+            assert np.array_equal(a.cpu().numpy(), b.cpu().numpy()), k
+        if k == "fused":
+            assert dec.last_kernel().startswith("bsl["), dec.last_kernel()
+    # the v5 prologue channel (APP export)
+    got = dec.decode_awgn(64, sigma, seed, offset=off + 5, app=True)
+    want = dec.decode(ref_t[5:69], app=True)
+    assert np.array_equal(got.app.cpu().numpy(), want.app.cpu().numpy())
     W = dec.weights
-    idx = np.flatnonzero(clean)[:64]
+    idx = np.arange(0, B, 31)[:64]
     o = nms_oracle.decode(ref[idx], dec.graph.proto, 24, W.alpha, W.alpha_ucn, W.beta, 20, 2, 5)
     app = dec.decode(ref_t[torch.from_numpy(idx).to(cuda_device)], app=True).app.cpu().numpy()
     assert np.array_equal(app, o["app"])
+
+
+@pytest.mark.parametrize("config", ["C2", "C3", "C4", "C5"])
+@pytest.mark.parametrize("off", [0, 3])
+def test_byte_channel_equals_float_channel(config, off, cuda_device):
+    """ldpc_decode_awgn's byte channel (k_awgn_q8 into the bit-sliced kernels' Q8 build) gives
+    the counters, frame flags and per-iteration frame errors of ldpc_channel_awgn's float LLRs
+    decoded by the same kernel, on every SURVEY workload (shortened bits through the BIG
+    marker on C4 / C5), ragged batch, aligned and unaligned offsets; LDPC_AWGN_Q8=0 is the
+    float path through ldpc_decode_awgn (read once per process, so compared here through
+    decode(awgn(...)))."""
+    import bench
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    cfg = bench.CONFIGS[config]
+    proto, g, W, cp = bench.load_problem(config=config)
+    dec = NMSDecoder(proto, cfg["z"], W, 2, 5, device=cuda_device)
+    punct, short = cfg.get("punct", (0, 0)), cfg.get("short", (0, 0))
+    B, sigma = 8195, float(cp.sigma(cfg["snr"]))
+    llr = dec.awgn(B, sigma, 17, offset=1000 + off, punct=punct, short=short)
+    want = dec.decode(llr, app=False, counters=True, flags=True, iter_wrong=True)
+    k_float = dec.last_kernel()
+    got = dec.decode_awgn(B, sigma, 17, offset=1000 + off, punct=punct, short=short,
+                          counters=True, flags=True, iter_wrong=True)
+    assert dec.last_kernel() == k_float and k_float.startswith(("bsl[", "bsc[")), k_float
+    for a, b in ((got.flags, want.flags), (got.counters, want.counters),
+                 (got.iter_wrong, want.iter_wrong)):
+        assert np.array_equal(a.cpu().numpy(), b.cpu().numpy())
+    assert int(want.counters[1]) > 0

@@ -196,3 +196,31 @@ def test_fused5_group_dealing_bit_exact(balance, merge, cuda_device, monkeypatch
         assert np.array_equal(app, c["app"]), (name, np.abs(app - c["app"]).max())
         ran += 1
     assert ran >= 5
+
+
+SP_CASES = [n for n in DECODER_CASES if "_sp_" in n]
+
+
+@pytest.mark.parametrize("name", SP_CASES)
+def test_sp_flood_against_oracle(name, cuda_device):
+    """Sum-product flood (and the fused SP kernel's counters) against the oracle's float32
+    restatement, which is within 1.1e-4 of the reference fixture: per-iteration APP statistics
+    (written to $LDPC_SP_STATS when set) and the bar of SP_* above."""
+    import json
+    from oracle import nms_oracle
+    c = load_case(name)
+    dec = _decoder(c, "flood", cuda_device)
+    app = dec.decode(c["llr"], app=True).app.cpu().numpy()
+    W = c["W"]
+    o = nms_oracle.decode(c["llr"], c["g"].proto, c["z"], W.alpha, W.alpha_ucn, W.beta, c["T"], 0,
+                          5)["app"][:, :, :app.shape[2]]
+    d_or, d_ref = np.abs(app - o), np.abs(app - c["app"])
+    stats = {"name": name, "max_vs_oracle": [float(x.max()) for x in d_or],
+             "p99_vs_oracle": [float(np.percentile(x, 99)) for x in d_or],
+             "max_vs_fixture": [float(x.max()) for x in d_ref],
+             "flips_vs_oracle": int(((app >= 0) != (o >= 0)).sum())}
+    if os.environ.get("LDPC_SP_STATS"):
+        with open(os.environ["LDPC_SP_STATS"], "a") as f:
+            f.write(json.dumps(stats) + "\n")
+    for t in range(c["T"]):
+        assert np.percentile(d_or[t], 99) <= SP_P99 and d_or[t].max() <= SP_MAX, (t, d_or[t].max())
