@@ -20,7 +20,8 @@ Prints ONE JSON line (rank 0).  Besides the driver's fields it carries:
                 bound "valu", achieved = SQ_INSTS_VALU per launch (PMC of this build,
                 profiles/traffic_<kernel>.json) / kernel time against one wave64 VALU issue
                 per 2 cycles per SIMD; hbm_frac = measured PMC traffic / time / 8 TB/s and
-                effective_frac = the §8 d figure / 8 TB/s ride along.  traffic = PMC HBM
+                x_two_kernel_roofline = the §8 d figure / 8 TB/s (a speed-up over the
+                two-kernel design at the HBM roofline) ride along.  traffic = PMC HBM
                 bytes per launch (null without a profile of this kernel at this batch).
   cpu_baseline  the dense TF-graph-equivalent numpy restatement of the reference decoder
                 (oracle/nms_dense.py) on the C1 sample (B=120, T=20, 3.5 dB), rank 0, N=1,
@@ -314,8 +315,11 @@ def main():
                     "traffic": traffic,
                     "hbm_frac": (round(traffic / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
                                  if traffic else None),
-                    "effective_frac": round(effective / HBM_PEAK_GBS, 4),
+                    "x_two_kernel_roofline": round(effective / HBM_PEAK_GBS, 2),
                     "valu_insts_per_launch": vi,
+                    "valu_per_pack_edge_iter": (round(vi / ((B + 31) // 32 * g.E * z * T), 3)
+                                                if vi and primary["name"].startswith(("bsl", "bsc"))
+                                                else None),
                     "valu_busy": vb or None,
                     "lds_busy": prof.get("lds_busy") if prof else None,
                     "wait_any_frac": prof.get("wait_any_frac") if prof else None,
@@ -334,9 +338,12 @@ def main():
                             "DESIGN.md 3.3). valu_busy = the busy model of the same PMC run: "
                             "quad-cycles with a VALU issue (SQ_INSTS_VALU - "
                             "SQ_ACTIVE_INST_VALU2) / (1024 SIMDs x GRBM_GUI_ACTIVE/8/4), at the "
-                            "clock of that run. effective_frac = SURVEY 8d two-kernel "
-                            "bytes/codeword x B / time / 8 TB/s (design comparison, not a "
-                            "bandwidth).")
+                            "clock of that run. x_two_kernel_roofline = this kernel's "
+                            "codewords/s over the most a two-kernel HBM-resident decoder could "
+                            "reach (SURVEY 8d bytes/codeword at 8 TB/s): a speed-up factor, not "
+                            "a bandwidth fraction. valu_per_pack_edge_iter = VALU "
+                            "wave-instructions / (32-codeword packs x lifted edges x T), the "
+                            "bit-sliced kernels' instruction cost per edge update.")
     else:
         roofline = {"bound": "hbm", "achieved": round(effective, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(effective / HBM_PEAK_GBS, 4), "traffic": traffic,
