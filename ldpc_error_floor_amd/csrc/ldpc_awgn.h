@@ -39,9 +39,10 @@ struct Philox {
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
         const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-        c[0] = hi1 ^ c[1] ^ k[0];
+        // (three-input xors as one v_bitop3 each)
+        c[0] = __builtin_amdgcn_bitop3_b32(hi1, c[1], k[0], 0x96);
         c[1] = lo1;
-        c[2] = hi0 ^ c[3] ^ k[1];
+        c[2] = __builtin_amdgcn_bitop3_b32(hi0, c[3], k[1], 0x96);
         c[3] = lo0;
     }
     static __device__ __forceinline__ void gen(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
@@ -128,22 +129,30 @@ __device__ __forceinline__ int awgn_level(const AwgnParams& a, P16 bucket, P32 t
     return lv;
 }
 
-// the bucket table of a's thresholds, built by the threads of a workgroup (tid < n) into LDS
+// the bucket table of a's thresholds, built by the threads of a workgroup (tid < n, n a
+// multiple of 64 dividing 1024) into LDS: one pass over the (uniform) thresholds, each lane
+// counting for its 1024 / n buckets
 __device__ __forceinline__ void awgn_bucket_fill(const AwgnParams& a, uint16_t* bucket, uint32_t* thi,
                                                  uint32_t* tlo, int tid, int n) {
-    for (int i = tid; i < a.nb; i += n) {
-        thi[i] = a.thr_hi[i];
-        tlo[i] = a.thr_lo[i];
+    if (tid < a.nb) {
+        thi[tid] = a.thr_hi[tid];
+        tlo[tid] = a.thr_lo[tid];
     }
-    for (int b = tid; b < (1 << AWGN_KB); b += n) {
-        int base = 0, cnt = 0;
-        for (int i = 0; i < a.nb; ++i) {
-            const uint32_t tb = a.thr_hi[i] >> (32 - AWGN_KB);
-            base += tb < (uint32_t)b ? 1 : 0;
-            cnt += tb == (uint32_t)b ? 1 : 0;
+    constexpr int NB = 1 << AWGN_KB;
+    uint32_t base[4] = {0u, 0u, 0u, 0u}, cnt[4] = {0u, 0u, 0u, 0u};
+    const int per = NB / n;                 // 4 at 256 threads
+    for (int i = 0; i < a.nb; ++i) {
+        const uint32_t tb = __builtin_amdgcn_readfirstlane(a.thr_hi[i]) >> (32 - AWGN_KB);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t b = (uint32_t)(tid + k * n);
+            base[k] += tb < b ? 1u : 0u;
+            cnt[k] += tb == b ? 1u : 0u;
         }
-        bucket[b] = (uint16_t)(base | cnt << 8);
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (k < per) bucket[tid + k * n] = (uint16_t)(base[k] | cnt[k] << 8);
 }
 
 // the levels of codewords 4 gq .. 4 gq + 3 at variable v (0-based; punctured / shortened

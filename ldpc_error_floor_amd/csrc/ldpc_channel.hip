@@ -118,15 +118,17 @@ __global__ void __launch_bounds__(256) k_awgn_q8(uint32_t* __restrict__ out, int
             w = (uint32_t)(48 - qmax) * 0x01010101u;
         } else {
             const uint64_t gb = g0 + (uint64_t)(pk * 32 + 4 * i);
-            int la[4], lb[4];
+            int la[4];
             awgn_levels4(a, bucket, thi, tlo, (uint32_t)v, gb >> 2, la);
-            if (sh) awgn_levels4(a, bucket, thi, tlo, (uint32_t)v, (gb >> 2) + 1, lb);
-            w = 0u;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int x = sh + k;
-                const int lv = x < 4 ? la[x & 3] : lb[x & 3];
-                w |= ((uint32_t)lv + boff) << (8 * k);
+            w = ((uint32_t)la[0] + boff) | ((uint32_t)la[1] + boff) << 8 | ((uint32_t)la[2] + boff) << 16 |
+                ((uint32_t)la[3] + boff) << 24;
+            if (sh) {               // (wave-uniform) a batch offset off the quads: rows from two quads
+                int lb[4];
+                awgn_levels4(a, bucket, thi, tlo, (uint32_t)v, (gb >> 2) + 1, lb);
+                const uint32_t wb = ((uint32_t)lb[0] + boff) | ((uint32_t)lb[1] + boff) << 8 |
+                                    ((uint32_t)lb[2] + boff) << 16 | ((uint32_t)lb[3] + boff) << 24;
+                // rows k = 0..3 are words sh + k of the quad pair (la, lb): one byte funnel shift
+                w = __builtin_amdgcn_alignbyte(wb, w, (uint32_t)sh);
             }
         }
         out[id] = w;

@@ -10,12 +10,17 @@ from _helpers import counters_from_app, flags_from_app
 pytestmark = pytest.mark.gpu
 KERNEL_NAMES = ["flood", "fused"]
 MS_ATOL = 1e-3
-# Sum-product (decoding_type 0): tanh/atanh in fp32 differ by ulps between the GPU and numpy,
-# and atanh near the +-(1 - 1e-7) clip amplifies a 1-ulp product difference to ~0.25, which
-# then propagates.  Measured on the SP fixtures: t <= 1 within 1e-6, p99 <= 2e-3 and max
-# <= 0.66 at t = 9, no hard-decision flip.  The bar: t <= 1 within SP_ATOL_EARLY, every
-# iteration p99 <= SP_P99 and max <= SP_MAX, hard decisions exact where |APP_ref| >= SP_HARD.
-SP_ATOL_EARLY, SP_P99, SP_MAX, SP_HARD = 1e-3, 1e-2, 1.0, 0.1
+# Sum-product (decoding_type 0): the GPU restates the oracle's float32 order (tanh / atanh in
+# float64 rounded once, the product over the other edges left to right), so the remaining
+# difference is numpy's float32 tanh against the correctly rounded one (<= 1 ulp), which atanh
+# near the +-(1 - 1e-7) clip amplifies once a message saturates (a 1-ulp product change moves
+# -2 atanh by ~0.2) and the iterations then carry.  Measured on the SP fixtures (T = 10,
+# r4b): t < 6 within 2.4e-4, p99 <= 1.7e-3 at every iteration, max 0.66 at t = 9 (one
+# message of the 5G BG2 case), no hard-decision flip.  The bar: t < SP_T_EARLY within
+# SP_ATOL_EARLY (SURVEY §8 c's 1e-3), every iteration p99 <= SP_P99 and max <= SP_MAX, hard
+# decisions exact where |APP_ref| >= SP_HARD.
+SP_T_EARLY = 6
+SP_ATOL_EARLY, SP_P99, SP_MAX, SP_HARD = 1e-3, 5e-3, 1.0, 0.1
 
 
 def _decoder(c, kernel, device):
@@ -65,7 +70,7 @@ def test_decoder_matches_reference(name, kernel, cuda_device):
         hard_ok = np.ones(c["hard"].shape, bool)
     elif c["dt"] == 0:
         d = np.abs(app - ref)
-        np.testing.assert_allclose(app[:2], ref[:2], rtol=0, atol=SP_ATOL_EARLY)
+        np.testing.assert_allclose(app[:SP_T_EARLY], ref[:SP_T_EARLY], rtol=0, atol=SP_ATOL_EARLY)
         for t in range(c["T"]):
             assert np.percentile(d[t], 99) <= SP_P99 and d[t].max() <= SP_MAX, (t, d[t].max())
         hard_ok = np.ones(c["hard"].shape, bool)
@@ -222,5 +227,7 @@ def test_sp_flood_against_oracle(name, cuda_device):
     if os.environ.get("LDPC_SP_STATS"):
         with open(os.environ["LDPC_SP_STATS"], "a") as f:
             f.write(json.dumps(stats) + "\n")
+    np.testing.assert_allclose(app[:SP_T_EARLY], o[:SP_T_EARLY], rtol=0, atol=SP_ATOL_EARLY)
     for t in range(c["T"]):
         assert np.percentile(d_or[t], 99) <= SP_P99 and d_or[t].max() <= SP_MAX, (t, d_or[t].max())
+    assert stats["flips_vs_oracle"] == 0
