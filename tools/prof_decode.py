@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--config", default="C2", help="a bench.py SURVEY 8d workload (C2..C5)")
     ap.add_argument("--decoding-type", type=int, default=2)
     ap.add_argument("--q-bit", type=int, default=5)
+    ap.add_argument("--e2e", action="store_true",
+                    help="decode_awgn (the channel kernel + the decoder) instead of decode")
     a = ap.parse_args()
     import torch
     import bench
@@ -28,8 +30,12 @@ def main():
     llr = dec.awgn(a.batch, float(cp.sigma(snr)), seed=1076, punct=cfg.get("punct", (0, 0)),
                    short=cfg.get("short", (0, 0)))
     cnt = torch.zeros(4, dtype=torch.int64, device=llr.device)
-    for _ in range(a.reps):
-        dec.decode(llr, T=cfg["T"], app=False, counters=cnt)
+    for i in range(a.reps):
+        if a.e2e:
+            dec.decode_awgn(a.batch, float(cp.sigma(snr)), seed=1077 + i, punct=cfg.get("punct", (0, 0)),
+                            short=cfg.get("short", (0, 0)), T=cfg["T"], counters=cnt)
+        else:
+            dec.decode(llr, T=cfg["T"], app=False, counters=cnt)
     torch.cuda.synchronize()
     print("counters", cnt.tolist(), "kernel", dec.kernel_info()[1])
 
