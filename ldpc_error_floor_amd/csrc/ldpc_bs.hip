@@ -222,6 +222,9 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     if (BS_CH_LDS) {                               // the channel planes, 16 B per (lane, variable)
         p.off_ch = (uint32_t)o;
         o += (size_t)16 * k.VPL * 64 * p.nw;
+    } else if (BS_GBLDS && k.CPL == 1) {           // the check lanes' slot-base words
+        p.off_ch = (uint32_t)o;
+        o += (size_t)4 * 64 * p.nw;
     }
     p.lds = (o + 15) & ~(size_t)15;
     if (p.lds > BS_LDS_MAX) return p;

@@ -100,7 +100,9 @@ struct BsArgs {
     uint32_t* hdx;               // XP builds: [T][packs][n_vars] hard decisions (bit r = codeword
                                  // 32 pack + r), the hard-bit / syndrome export
     uint32_t off_slots, off_pad, off_zero, off_red, off_alut, off_blut, off_hdz, off_btid;   // LDS byte offsets
-    uint32_t off_ch;             // BS_CH_LDS: the channel's magnitude planes, [lane][VPL][4] words
+    uint32_t off_ch;             // per-lane LDS words: BS_CH_LDS the channel's magnitude planes,
+                                 // [lane][VPL][4]; else (BS_GBLDS, one-chunk instances) the check
+                                 // lane's slot base (| alpha-table address << 16), [lane]
                                  // (RED: 16 words, then T words: iteration t's frame-error word)
     int ablate;   // timing diagnostics, builds with -DBS_DIAG only (LDPC_DIAG_ABLATE, wrong
                   // results): 1 no check phase, 2 no beta table, 4 no V->C pass, 8 no frame
@@ -494,6 +496,12 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
 // and iteration) instead of 4 registers held through the whole decode (A/B switch)
 #ifndef BS_CH_LDS
 #define BS_CH_LDS 0
+#endif
+// the one-chunk instances' check-lane slot base (packed with the alpha-table address) kept in
+// one LDS word per lane and read at each check phase, instead of a register held through the T
+// loop (which the 64- and 80-VGPR builds spilled: a scratch reload + vmcnt(0) per iteration)
+#ifndef BS_GBLDS
+#define BS_GBLDS 1
 #endif
 // The channel planes of one variable for the 32 codewords of a pack: sign cs, magnitude planes
 // cm[0..3] of Q(ch) in grid units, shortened-bit flags bg (BIG); returns 1 when a row is off the
@@ -1074,6 +1082,8 @@ k_bs(BsArgs a) {
     }
     const uint32_t cstride = (uint32_t)(a.z * SLOT_B);
     const uint32_t tabu = (uint32_t)(a.arows * LUT_W * 4);        // alpha' tables after the alpha ones
+    constexpr bool GBL = BS_GBLDS && CPL == 1 && !BS_CH_LDS;
+    if constexpr (GBL) lds_put(a.off_ch + 4u * (uint32_t)tid, gbase[0]);
     __syncthreads();
 
     for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
@@ -1124,8 +1134,18 @@ k_bs(BsArgs a) {
             const bool active = (CPL == 1) ? (BS_TIDFREE ? wave * 64 < a.cn_lanes : tid < a.cn_lanes)
                                            : (gchunk[c] >= 0);   // (cn_lanes: 64 k)
             if (!active || ABL(1)) continue;
-            uint32_t cbase = gbase[c];
-            asm volatile("" : "+v"(cbase));
+            uint32_t cbase;
+            if constexpr (GBL) {
+                // (the lane index from an operand the loop cannot hoist: a hoisted address was
+                // itself held through the loop and spilled)
+                uint32_t all = ~0u;
+                asm volatile("" : "+s"(all));
+                const uint32_t ln = __builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
+                cbase = lds_w(a.off_ch + ((uint32_t)wave << 8) + 4u * ln);
+            } else {
+                cbase = gbase[c];
+                asm volatile("" : "+v"(cbase));
+            }
             uint32_t ctab = PKG ? (cbase >> 16) : gtab[c];
             if constexpr (PKG) cbase &= 0xFFFFu;
             const int cdeg = gdeg[c];
