@@ -125,21 +125,25 @@ int ldpc_ctx_last_kernel(const ldpc_ctx* c, char* name, int32_t name_len);
 
 /* On-GPU AWGN channel for the all-zero codeword (create_mix_epoch, Print_Functions.py:29-72):
    writes llr_dev [B][n_vars] f32 = Q(2(sigma*n - 1)/sigma^2) with punctured (1-based bits
-   punct_start..punct_end, 0 = none) -> 0 and shortened -> -clip_llr.  n ~ N(0,1) from a
-   counter-based Philox stream indexed by (seed, offset + b, element): shards generated with
-   their global codeword offset reproduce the single-GPU stream.  fp32 arithmetic with a 53-bit
-   uniform under the logarithm (tails to ~8.6 sigma); see csrc/ldpc_awgn.h. */
+   punct_start..punct_end, 0 = none) -> 0 and shortened -> -clip_llr.  Counter-based Philox
+   streams indexed by (seed, offset + b, element): shards generated with their global codeword
+   offset reproduce the single-GPU stream.  QMS: the quantized level is sampled exactly from
+   its distribution (64-bit CDF thresholds computed in float64, one Philox per 4 codewords of a
+   variable); float modes: Box-Muller with a 53-bit uniform under the logarithm (tails to ~8.6
+   sigma).  See csrc/ldpc_awgn.h. */
 int ldpc_channel_awgn(float* llr_dev, int64_t B, int32_t n_vars, double sigma, uint64_t seed,
                       int64_t offset, int32_t decoding_type, int32_t q_bit, int32_t punct_start,
                       int32_t punct_end, int32_t short_start, int32_t short_end, float clip_llr,
                       void* stream);
 
 /* In-decoder channel for throughput sweeps (SURVEY §8 f rank 1): the LLRs of the B codewords
-   are generated by the same Philox AWGN generator as ldpc_channel_awgn (same seed, global
-   codeword offset, puncture/shorten) and decoded without touching HBM (fused v5 generates them
-   in the kernel prologue; other kernels generate into a context buffer first).  The result is
-   identical to ldpc_channel_awgn followed by ldpc_decode.  Replaces create_mix_epoch +
-   sess.run in the compute_results loop (Print_Functions.py:29-72, :130-165). */
+   come from the same generator as ldpc_channel_awgn (same seed, global codeword offset,
+   puncture/shorten) and never cross HBM as floats: APP exports generate them in the fused v5
+   kernel's prologue; counters-only QMS decodes of the bit-sliced kernels take a byte channel
+   (one byte per LLR, already in the layout their prologue packs into bit planes); flood and the
+   float-mode kernel generate float LLRs into a context buffer first.  The result is identical to
+   ldpc_channel_awgn followed by ldpc_decode.  Replaces create_mix_epoch + sess.run in the
+   compute_results loop (Print_Functions.py:29-72, :130-165). */
 typedef struct ldpc_channel_params {
     double sigma;                 /* noise standard deviation (SNR -> sigma: init_parameter) */
     uint64_t seed;
