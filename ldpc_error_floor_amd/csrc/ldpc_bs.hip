@@ -704,6 +704,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.cu = p.cu > 0.f ? p.cu : -1.f;
     a.qmax = bs_qmax(mode);
     a.ucn = p.ucn ? 1 : 0;
+    a.ucn_iter = g.w_ucn_iter;
     a.beta_id = g.w_beta_id_mask;        // (identity on m <= 15 implies it on m <= qmax)
     a.row_ptr = g.row_ptr;
     a.z = g.z;

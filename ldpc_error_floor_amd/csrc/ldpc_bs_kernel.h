@@ -108,6 +108,8 @@ struct BsArgs {
                   // results): 1 no check phase, 2 no beta table, 4 no V->C pass, 8 no frame
                   // flags, 16 no iterations, 32 no LLR loads.  (Compiled in, the uniform
                   // tests alone cost 4 %.)
+    uint64_t ucn_iter;           // bit t (t < 64): iteration t's alpha' differs from alpha (its
+                                 // check phase needs the syndromes); iterations >= 64: on
 };
 
 // ---- bit-plane arithmetic ---------------------------------------------------------------------
@@ -681,6 +683,11 @@ k_bs(BsArgs a) {
     uint32_t* ALUT = reinterpret_cast<uint32_t*>(smem + a.off_alut);   // [2][AR][LUT_W]
     uint32_t* BLUT = reinterpret_cast<uint32_t*>(smem + a.off_blut);   // [2][bcols][BLUT_W]
     const bool ucn = UCN && a.ucn;
+    // UCN work of iteration t's check phase (the syndromes, the alpha' table) and of the hard
+    // decisions the variable phase writes for it: skipped where alpha'_t = alpha_t
+    auto ucn_on = [&](int t) __attribute__((always_inline)) -> bool {
+        return ucn && (t >= 64 || ((a.ucn_iter >> t) & 1));
+    };
 
     // ---- per-lane variables: slot addresses, variable index, degree bounds of the wave ----------
     uint32_t va[VPL][VNA];
@@ -958,7 +965,7 @@ k_bs(BsArgs a) {
                     for (int i = 0; i < SB - 1; ++i) c = B3(T_MAJ, S[i], i < 4 ? (cmu[i] ^ c_s) : c_s, c);
                     hd = B3(T_XNOR3, S[SB - 1], c_s, c);
                 }
-                if (UCN && !last && ucn && v >= 0) lds_put(hda, hd);   // HD[v] (Main_Functions.py:184-188)
+                if (UCN && !last && v >= 0 && ucn_on(tb)) lds_put(hda, hd);   // HD[v] (Main_Functions.py:184-188)
                 hd &= valid;                                     // APP >= 0 -> hard decision 1
                 if constexpr (XP) {                              // iteration tb - 1's hard decisions
                     if (v >= 0) a.hdx[((size_t)(tb - 1) * (size_t)((a.B + 31) >> 5) + blockIdx.x) * nv + v] = hd;
@@ -983,7 +990,7 @@ k_bs(BsArgs a) {
             const int dwm = dwmin[u];
             if (first) {
                 // UCN at t = 0: the hard decision of x~ = Q(beta_0 ch) (Main_Functions.py:181-182)
-                if (UCN && ucn && v >= 0) lds_put(hda, ~Tv[5]);
+                if (UCN && v >= 0 && ucn_on(0)) lds_put(hda, ~Tv[5]);
                 uint32_t x[7], X[4];
 #pragma unroll
                 for (int i = 0; i < 7; ++i) x[i] = Tv[i < 6 ? i : 5];
@@ -1176,8 +1183,9 @@ k_bs(BsArgs a) {
             // UCN: syndrome of the previous hard decisions over the check (padding edges read a
             // zero word): odd -> the check is unsatisfied, its messages weighted by alpha'
             uint32_t syn = 0u;
+            const bool ucn_t = ucn_on(t);
             if constexpr (UCN) {
-                if (ucn) {
+                if (ucn_t) {
                     // (the packed addresses made opaque per iteration: unpacked per use, not
                     // hoisted out of the T loop as EPL registers that the loop then spilled)
 #pragma unroll
@@ -1249,7 +1257,7 @@ k_bs(BsArgs a) {
                 // whose checks are all satisfied in all 32 codewords (most waves once the
                 // frames have converged) skips its table (the same messages, exactly)
                 bool any_unsat = false;
-                if constexpr (UCN) any_unsat = ucn && (!(BS_USKIP && CPL > 1) || __builtin_amdgcn_ballot_w64(syn != 0u) != 0ull);
+                if constexpr (UCN) any_unsat = ucn_t && (!(BS_USKIP && CPL > 1) || __builtin_amdgcn_ballot_w64(syn != 0u) != 0ull);
                 // tables of the fixed set: every lane evaluates all 4 bits of both minima with
                 // immediate truth tables (no table words, no lane exchange)
                 bool fixed = false;

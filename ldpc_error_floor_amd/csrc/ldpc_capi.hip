@@ -309,6 +309,13 @@ int ldpc_graph_query(const ldpc_graph* g, int32_t* dims) {
 int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* alpha_ucn,
                      const float* beta) {
     if (!g) return LDPC_ERR_ARG;
+    // alpha' equal to alpha bit for bit at every iteration: the unsatisfied-check weighting
+    // (Main_Functions.py:266-304) selects between equal weights, so every kernel decodes it as a
+    // decoder without UCN (no syndrome / hard-decision work; the same outputs exactly).  The
+    // 5G BG2 trained weights of C4 are such a table.
+    if (alpha && alpha_ucn && T > 0 && g->h.E > 0 &&
+        std::memcmp(alpha, alpha_ucn, (size_t)T * g->h.E * sizeof(float)) == 0)
+        alpha_ucn = nullptr;
     host::WeightInfo wi;
     const int sta = host::analyze_weights(g->h, T, alpha, alpha_ucn, beta, wi);
     if (sta != LDPC_OK) return sta;
@@ -353,6 +360,7 @@ int ldpc_weights_set(ldpc_graph* g, int32_t T, const float* alpha, const float* 
     g->dev.w_beta_nonneg = wi.beta_nonneg;
     g->dev.w_beta_one = wi.beta_one;
     g->dev.w_beta_id_mask = wi.beta_id_mask;
+    g->dev.w_ucn_iter = wi.ucn_iter_mask;
     g->dev.w_version++;
     return LDPC_OK;
 }

@@ -134,6 +134,13 @@ int analyze_weights(const GraphTables& g, int32_t T, const float* alpha, const f
         }
         if (id) w.beta_id_mask |= (uint64_t)1 << t;
     }
+    if (alpha_ucn)
+        for (int t = 0; t < T && t < 64; ++t)
+            for (int e = 0; e < g.E; ++e)
+                if (alpha_ucn[(size_t)t * g.E + e] != alpha[(size_t)t * g.E + e]) {
+                    w.ucn_iter_mask |= (uint64_t)1 << t;
+                    break;
+                }
     w.beta_tid.resize((size_t)T * g.N);
     for (size_t x = 0; x < (size_t)T * g.N; ++x) w.beta_tid[x] = beta_table_id(beta[x]);
     for (int t = 0; t < T; ++t) {

@@ -78,6 +78,9 @@ struct WeightInfo {
     // bit t (t < 64): every column's q5/q-5 channel table of iteration t is the identity,
     // min(15, |rint(fl32(m beta))|) == m for m = 0..15 (the bit-sliced kernels skip it)
     uint64_t beta_id_mask = 0;
+    // bit t (t < 64): alpha_ucn[t] differs from alpha[t] for some edge (with equal tables the
+    // unsatisfied-check weighting of that iteration is the identity, Main_Functions.py:266-304)
+    uint64_t ucn_iter_mask = 0;
     std::vector<int32_t> row_merge;
     // [T][N]: index into kBetaTab (ldpc_beta_tabs.h) of column j's q5 / q-5 channel table at
     // iteration t, min(15, |rint(fl32(m beta))|) for m = 0..15; -1 when beta < 0 or the table is

@@ -32,6 +32,8 @@ struct DevGraph {
     int w_alpha_uniform, w_beta_uniform, w_beta_nonneg, w_beta_one;
     int w_alpha_pair_uniform;            // alpha and alpha_ucn: one value per iteration each
     uint64_t w_beta_id_mask;     // iterations whose q5 channel table is the identity
+    uint64_t w_ucn_iter;         // bit t (t < 64): iteration t's alpha' differs from its alpha
+                                 // somewhere (UCN weighting matters); iterations >= 64: assumed
     const int32_t* beta_tid;     // [T][N] kBetaTab index of each column's q5 channel table, -1
     uint64_t w_version;          // incremented by every ldpc_weights_set (table caches)
 };

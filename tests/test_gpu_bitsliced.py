@@ -106,10 +106,15 @@ def test_off_grid_packs_many_blocks_per_fixup_workgroup(cuda_device):
 
 # ---- the large / UCN instances: 802.11n (C3: degree 22, [3,3,3] UCN, T=50) and 5G BG2 (C4:
 # 1,280 variables, [2,2,2] UCN per row and column, puncture and shortening) --------------------
-def _config(device, cfg, T=None):
+def _config(device, cfg, T=None, ucn_scale=None):
+    """A SURVEY workload's decoder; ``ucn_scale``: alpha' = alpha x scale instead of the trained
+    alpha' (C4's trained alpha' equals its alpha, which every kernel folds into a decoder without
+    UCN: scaling keeps the UCN path of the 5G BG2 instance under test)."""
     import bench
     from ldpc_error_floor_amd.decoder import NMSDecoder
     proto, g, W, cp = bench.load_problem(T=T, config=cfg)
+    if ucn_scale is not None:
+        W.alpha_ucn = (W.alpha * np.float32(ucn_scale)).astype(np.float32)
     dec = NMSDecoder(proto, g.z, W, 2, 5, device=device)
     c = bench.CONFIGS[cfg]
     dec.punct = c.get("punct", (0, 0))
@@ -122,7 +127,7 @@ def _config(device, cfg, T=None):
                                          ("C4", 8, 40000, "4")])
 def test_bitsliced_large_and_ucn(cuda_device, cfg, T, B, lpc, monkeypatch):
     monkeypatch.setenv("LDPC_BS_LPC", lpc)
-    dec, cp, c = _config(cuda_device, cfg, T)
+    dec, cp, c = _config(cuda_device, cfg, T, ucn_scale=0.8 if cfg == "C4" else None)
     name = dec.kernel_info()[1]
     assert name.startswith("bsl") and ",ucn" in name, name
     if cfg == "C3":
@@ -141,8 +146,28 @@ def test_bitsliced_large_and_ucn(cuda_device, cfg, T, B, lpc, monkeypatch):
     assert np.array_equal(r.counters.cpu().numpy(), out["flood"][0])
 
 
+def test_identity_ucn_weights_fold(cuda_device):
+    """C4's trained alpha' equals its alpha at every iteration, so the unsatisfied-check
+    weighting is the identity and ldpc_weights_set folds it away (no ",ucn" kernel): counters and
+    flags still equal flood's, and the APP equals the oracle's decode, which applies the UCN
+    selection of Main_Functions.py:266-304 with the trained alpha'."""
+    from oracle import nms_oracle
+    dec, cp, c = _config(cuda_device, "C4", 20)
+    assert ",ucn" not in dec.kernel_info()[1], dec.kernel_info()
+    llr = dec.awgn(3001, float(cp.sigma(c["snr"] - 0.75)), seed=5, offset=77,
+                   punct=c["punct"], short=c["short"])
+    out = _both(dec, llr)
+    assert np.array_equal(out["fused"][0], out["flood"][0])
+    assert np.array_equal(out["fused"][1], out["flood"][1])
+    W = dec.weights
+    x = llr[:48].cpu().numpy()
+    o = nms_oracle.decode(x, dec.graph.proto, 64, W.alpha, W.alpha_ucn, W.beta, 20, 2, 5)
+    app = dec.decode(llr[:48], app=True).app.cpu().numpy()
+    assert np.array_equal(app, o["app"])
+
+
 def test_bitsliced_ucn_off_grid_fixup(cuda_device, lpc):
-    dec, cp, c = _config(cuda_device, "C4", 10)
+    dec, cp, c = _config(cuda_device, "C4", 10, ucn_scale=0.8)
     assert dec.kernel_info()[1].startswith("bsl"), dec.kernel_info()
     llr = dec.awgn(2000, float(cp.sigma(1.5)), seed=9)
     llr[40, 3] += 0.1            # pack 1 off the grid
