@@ -57,11 +57,13 @@ constexpr BsInst kBsInst[] = {
     {16, 8, 4, 1, 1, false, false, true, 8},
     {15, 6, 2, 1, 1, false, false, true, 8},     // LDPC_BS_LPC=2 A/B
     {24, 4, 4, 1, 1, true, true, true, 6},       // 802.11n (C3): degree 22, UCN
+    {10, 8, 2, 2, 2, false, true, false, 4},     // 5G BG2 without UCN weighting (C4's trained
+                                                 // alpha' = alpha folds to it)
     {10, 8, 2, 2, 2, true, true, false, 4},      // 5G BG2 (C4): 1,280 variables, 640 checks;
                                                  // 18.2 ms vs 21.2 for LPC 4 (CPL 3), same box
     {10, 8, 4, 2, 3, true, true, false, 4},      // LDPC_BS_LPC=4 A/B
     // 5G BG2 with 10 waves (20 variable and 20 check chunks, no idle place) at up to 168 VGPRs
-    // (no spills, 2-3 waves per SIMD): LDPC_BS_INST=6 A/B
+    // (no spills, 2-3 waves per SIMD): LDPC_BS_INST=7 A/B
     {10, 8, 2, 2, 2, true, true, false, 3, 10},
 };
 constexpr int kBsNInst = sizeof(kBsInst) / sizeof(kBsInst[0]);
