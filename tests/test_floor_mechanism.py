@@ -49,7 +49,7 @@ def test_c4_flare_is_degree1_saturation():
         sweep = json.load(f)
     for r in sweep["scan"]:
         s = r["sigma"]
-        p_bit = 1.0 - ndtr(7.25 * s / 2 + 1 / s)
+        p_bit = ndtr(-(7.25 * s / 2 + 1 / s))
         pred = 1.0 - (1.0 - p_bit) ** n_bits
         if r["snr_db"] >= 3.0:
             assert abs(pred / r["fer_last"] - 1) < 0.011, (r["snr_db"], pred, r["fer_last"])
@@ -62,3 +62,37 @@ def test_c4_flare_is_degree1_saturation():
     assert all(x > np.sqrt(2 / 7.25) for x in sig)
     fers = [r["fer_last"] for r in sweep["scan"] if r["snr_db"] >= 2.5]
     assert fers == sorted(fers)
+
+
+def test_c5_floor_is_degree1_saturation_over_ten_decades():
+    """The same mechanism with C5's flat weights (5G BG1 n2112, alpha = 0.75, beta = 1, q5,
+    T = 50): BG1's 432 degree-1 bits (columns 26-31) get at most Q(0.75 x 7.5) = 5.5 from their
+    check, so a channel LLR that rounds to >= 5.5 (raw >= 5.25) leaves APP >= 0, a frame error.
+    FER = 1 - (1 - Q(5.25 sigma / 2 + 1 / sigma))^432 predicts every committed C5 sweep point
+    (profiles/r2/sweep_c5*, 4.2e6 to 1.07e10 codewords per point, 3 to 15 dB, FER 0.22 down to
+    1.9e-9) within Poisson noise."""
+    import sys
+    from scipy.special import ndtr
+    sys.path.insert(0, ROOT)
+    import bench
+    proto, g, W, cp = bench.load_problem(config="C5")
+    P = np.asarray(proto)
+    cols = np.flatnonzero((P >= 0).sum(axis=0) == 1)
+    assert cols.tolist() == list(range(26, 32))
+    assert np.all(W.alpha == np.float32(0.75)) and np.all(W.beta == np.float32(1.0))
+    assert _q5(np.float32(0.75) * np.float32(7.5)) == 5.5
+    n_bits = len(cols) * 72
+    pts = []
+    for f in ("sweep_c5/sweep_c5.json", "sweep_c5_deep/sweep_c5_14.5dB.json",
+              "sweep_c5_deep/sweep_c5_15dB.json"):
+        with open(os.path.join(ROOT, "profiles", "r2", f)) as fh:
+            d = json.load(fh)
+        pts += d["scan"] + d["deep"]
+    assert len(pts) >= 15
+    for r in pts:
+        s, n = r["sigma"], r["codewords"]
+        p_bit = ndtr(-(5.25 * s / 2 + 1 / s))
+        exp = n * (1.0 - (1.0 - p_bit) ** n_bits)
+        obs = r["frame_err_last"]
+        # Poisson noise, plus 0.5 % for the frames the mechanism does not cover at low SNR
+        assert abs(obs - exp) <= 4.0 * np.sqrt(exp) + 0.005 * exp + 3, (r["snr_db"], obs, exp)
