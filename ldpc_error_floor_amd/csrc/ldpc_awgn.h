@@ -105,26 +105,35 @@ __device__ __forceinline__ void awgn_pair(const AwgnParams& a, int64_t b, int pr
 }
 
 // ---- QMS level sampler -------------------------------------------------------------------------
-// Level of each of the four codewords 4 gq + j (global quad gq) at variable v (0-based), from the
-// high words hw (Philox(v, gq, 'LDQ4')).  bucket / thi / tlo: the bucket table (awgn_bucket_fill)
-// and thresholds, in LDS or global memory.  A bucket holds base | count << 8: U's top AWGN_KB
-// bits fix every threshold but the `count` ones starting at `base`, compared one by one.
+// Level of a codeword from the high word u of its uniform.  bucket / thi: the bucket table
+// (awgn_bucket_fill) and thresholds, in LDS or global memory.  A bucket holds base | count << 8:
+// U's top AWGN_KB bits fix every threshold but the `count` ones starting at `base`, compared one
+// by one.  A tie of the high words (u == thi[lv], P ~ nb 2^-32) stops the scan with `tie` set:
+// the low word decides (awgn_tie_scan), drawn only then -- kept out of this loop so that the
+// compiler cannot hoist the second Philox in front of it.
 constexpr int AWGN_KB = 10;                 // bucket bits (1024 buckets, 2 KB of LDS)
 template <typename P16, typename P32>
-__device__ __forceinline__ int awgn_level(const AwgnParams& a, P16 bucket, P32 thi, P32 tlo,
-                                          uint32_t u, uint32_t v, uint64_t gq, int j) {
+__device__ __forceinline__ int awgn_level_hi(P16 bucket, P32 thi, uint32_t u, bool& tie) {
     const uint32_t e = bucket[u >> (32 - AWGN_KB)];
     int lv = (int)(e & 0xFFu);
     const int cnt = (int)(e >> 8);
     for (int i = 0; i < cnt; ++i) {
         const uint32_t th = thi[lv];
-        if (u < th) break;                       // thresholds ascend: the rest are above U too
-        if (u == th) {                           // the high words tie: compare the low words
-            uint32_t c[4] = {v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_R};
-            Philox::gen(c, a.k0, a.k1);
-            if (c[j] < tlo[lv]) break;
+        if (u <= th) {                           // thresholds ascend: the rest are above U too
+            tie = u == th;
+            break;
         }
         ++lv;
+    }
+    return lv;
+}
+
+// the scan from a tie at level lv on: full 64-bit comparisons (hi word u, low word lo)
+template <typename P32>
+__device__ __forceinline__ int awgn_tie_scan(int nb, P32 thi, P32 tlo, uint32_t u, uint32_t lo, int lv) {
+    for (; lv < nb; ++lv) {
+        const uint32_t th = thi[lv];
+        if (u < th || (u == th && lo < tlo[lv])) break;
     }
     return lv;
 }
@@ -162,8 +171,16 @@ __device__ __forceinline__ void awgn_levels4(const AwgnParams& a, P16 bucket, P3
                                              uint32_t v, uint64_t gq, int (&lv)[4]) {
     uint32_t c[4] = {v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_Q};
     Philox::gen(c, a.k0, a.k1);
+    bool tie[4] = {false, false, false, false};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) lv[j] = awgn_level(a, bucket, thi, tlo, c[j], v, gq, j);
+    for (int j = 0; j < 4; ++j) lv[j] = awgn_level_hi(bucket, thi, c[j], tie[j]);
+    if (tie[0] | tie[1] | tie[2] | tie[3]) {
+        uint32_t r[4] = {v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_R};
+        Philox::gen(r, a.k0, a.k1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (tie[j]) lv[j] = awgn_tie_scan(a.nb, thi, tlo, c[j], r[j], lv[j]);
+    }
 }
 
 // what a QMS element at 1-based bit `bit` is: 0 random, 1 punctured (LLR 0), 2 shortened (-clip)
@@ -186,14 +203,11 @@ __device__ __forceinline__ float awgn_qms_elem(const AwgnParams& a, uint64_t gb,
     Philox::gen(c, a.k0, a.k1);
     const uint32_t u = c[j];
     int lv = 0;
-    for (int i = 0; i < a.nb; ++i) {
-        if (u < a.thr_hi[i]) break;
-        if (u == a.thr_hi[i]) {
-            uint32_t r[4] = {(uint32_t)v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_R};
-            Philox::gen(r, a.k0, a.k1);
-            if (r[j] < a.thr_lo[i]) break;
-        }
-        ++lv;
+    while (lv < a.nb && u > a.thr_hi[lv]) ++lv;
+    if (lv < a.nb && u == a.thr_hi[lv]) {        // a tie of the high words: draw the low word
+        uint32_t r[4] = {(uint32_t)v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_R};
+        Philox::gen(r, a.k0, a.k1);
+        lv = awgn_tie_scan(a.nb, a.thr_hi, a.thr_lo, u, r[j], lv);
     }
     return a.val[lv];
 }

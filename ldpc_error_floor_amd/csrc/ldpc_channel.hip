@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(256) k_awgn_qf(float* __restrict__ out, int64_
 // wman codeword instead of 2,304.  One thread per (pack, variable, codeword quad), the quad
 // index fastest: a wave stores 8 variables x 32 bytes, contiguous.  Rows past B are generated
 // too (the decoder masks them).
+template <bool WIDE>
 __global__ void __launch_bounds__(256) k_awgn_q8(uint32_t* __restrict__ out, int64_t npk, int n_vars,
                                                  AwgnParams a, int qmax) {
     __shared__ uint16_t bucket[1 << AWGN_KB];
@@ -107,9 +108,18 @@ __global__ void __launch_bounds__(256) k_awgn_q8(uint32_t* __restrict__ out, int
     for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
          id += (int64_t)gridDim.x * blockDim.x) {
         const int i = (int)(id & 7);
-        const int64_t pv = id >> 3;
-        const int64_t pk = pv / n_vars;
-        const int v = (int)(pv - pk * n_vars);
+        int64_t pk;
+        int v;
+        if (WIDE) {
+            const int64_t pv = id >> 3;
+            pk = pv / n_vars;
+            v = (int)(pv - pk * n_vars);
+        } else {                         // (a 32-bit division when the grid has < 2^32 words)
+            const uint32_t pv = (uint32_t)id >> 3;
+            const uint32_t q = pv / (uint32_t)n_vars;
+            pk = q;
+            v = (int)(pv - q * (uint32_t)n_vars);
+        }
         const int fx = awgn_fixed(a, v + 1);
         uint32_t w;
         if (fx == 1) {
@@ -200,7 +210,10 @@ int channel_q8(uint32_t* q8, int64_t B, int n_vars, const AwgnParams& a, int qma
     const int64_t npk = (B + 31) / 32;
     const int64_t total = npk * n_vars * 8;
     const unsigned grid = (unsigned)std::min<int64_t>(8192, (total + 255) / 256);
-    hipLaunchKernelGGL(k_awgn_q8, dim3(grid), dim3(256), 0, s, q8, npk, n_vars, a, qmax);
+    if (total + (int64_t)grid * 256 >= ((int64_t)1 << 32))
+        hipLaunchKernelGGL(k_awgn_q8<true>, dim3(grid), dim3(256), 0, s, q8, npk, n_vars, a, qmax);
+    else
+        hipLaunchKernelGGL(k_awgn_q8<false>, dim3(grid), dim3(256), 0, s, q8, npk, n_vars, a, qmax);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 

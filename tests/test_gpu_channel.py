@@ -119,3 +119,26 @@ def test_byte_channel_equals_float_channel(config, off, cuda_device):
                  (got.iter_wrong, want.iter_wrong)):
         assert np.array_equal(a.cpu().numpy(), b.cpu().numpy())
     assert int(want.counters[1]) > 0
+
+
+@pytest.mark.parametrize("off", [4096, 4097])
+def test_qms_high_word_tie_bit_exact(cuda_device, off):
+    """A uniform whose high word ties the lowest threshold (sigmas from
+    test_philox_oracle.tie_sigmas): the device's low-word draw orders it like the oracle's
+    64-bit comparison, in ldpc_channel_awgn's level sampler and in the v5 prologue's channel
+    (aligned batches: awgn_levels4, as k_awgn_q8; unaligned: awgn_qms_elem)."""
+    import torch
+    from test_philox_oracle import tie_sigmas
+    dec = _decoder(cuda_device, "wman_N0576_R34_z24", 24, 2, 5, T=2)
+    seed = 7
+    b, v, s0, s1 = tie_sigmas(dec.n_vars, seed, off & ~3, bmin=off & 3)
+    b -= off & 3                              # the element's row in a batch starting at off
+    for s, lv in ((s0, 0), (s1, 1)):
+        B = 64
+        got = dec.awgn(B, s, seed, offset=off).cpu().numpy()
+        ref, _ = awgn_llr(B, dec.n_vars, s, seed, off, decoding_type=2, q_bit=5)
+        assert ref[b, v] == (-7.5 if lv == 0 else -7.0)
+        assert np.array_equal(got, ref)
+        app = dec.decode_awgn(B, s, seed, offset=off, app=True).app.cpu().numpy()
+        want = dec.decode(torch.from_numpy(ref).to(cuda_device), app=True).app.cpu().numpy()
+        assert np.array_equal(app, want)

@@ -116,3 +116,48 @@ def test_qms_stream_sharding_and_layout():
     rows = q8.transpose(0, 2, 1).reshape(96, 130).astype(np.int64)
     assert np.array_equal(rows[:, 3:119] - 16, grid[:, 3:119])
     assert np.all(rows[:, :3] == 16) and np.all(rows[:, 119:] == 48 - 15)
+
+
+def tie_sigmas(n_vars, seed, offset, q_bit=5, D=1 << 20, bmin=0):
+    """Two channel sigmas at which the lowest QMS threshold T_0 shares its high word with the
+    uniform U of one element (codeword b >= bmin of offset .. offset + 3, variable v): T_0 = U + ~D
+    (level 0) and T_0 = U - ~D (level 1), so that the level rides on the low words.  T_0 falls
+    as sigma rises (its boundary is negative), so both come from bisection on sigma; D keeps
+    them clear of a last-ulp difference between the host's and the oracle's erfc.
+    Returns (b, v, sigma_level0, sigma_level1)."""
+    from oracle.philox_oracle import _qms_uniforms, qms_levels
+    T0 = lambda s: int(qms_levels(s, q_bit)[0][0])           # noqa: E731
+    U = _qms_uniforms(4, n_vars, seed, offset)
+    lo_s, hi_s = 0.6, 1.2
+    b, v = next((b, v) for b in range(bmin, 4) for v in range(n_vars)
+                if T0(hi_s) + 2 * D < int(U[b, v]) < T0(lo_s) - 2 * D
+                and 2 * D < (int(U[b, v]) & 0xFFFFFFFF) < (1 << 32) - 2 * D)
+    u = int(U[b, v])
+
+    def sigma_at(target):
+        a, c = lo_s, hi_s                                     # T0(a) > target >= T0(c)
+        for _ in range(80):
+            m = 0.5 * (a + c)
+            if T0(m) > target:
+                a = m
+            else:
+                c = m
+        return a, c
+
+    s0 = sigma_at(u + D)[0]            # T_0 just above U + D: U < T_0, level 0
+    s1 = sigma_at(u - D)[1]            # T_0 at most U - D: U >= T_0, level >= 1
+    return b, v, s0, s1
+
+
+def test_qms_high_word_ties_resolve_on_the_low_word():
+    """The sampler's 64-bit comparison: at both tie sigmas T_0 and U share the high word (the
+    device's first pass stops there and draws the 'LDQR' word), and the level is 0 or 1 as the
+    low words order them (the GPU side: tests/test_gpu_channel.py)."""
+    from oracle.philox_oracle import _qms_uniforms, qms_levels
+    seed, off = 7, 4096
+    b, v, s0, s1 = tie_sigmas(576, seed, off)
+    u = int(_qms_uniforms(4, 576, seed, off)[b, v])
+    for s, lv in ((s0, 0), (s1, 1)):
+        t0 = int(qms_levels(s, 5)[0][0])
+        assert t0 >> 32 == u >> 32 and t0 != u
+        assert awgn_qms_levels(4, 576, s, seed, off)[b, v] == lv
