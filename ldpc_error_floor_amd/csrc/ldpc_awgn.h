@@ -138,30 +138,33 @@ __device__ __forceinline__ int awgn_tie_scan(int nb, P32 thi, P32 tlo, uint32_t 
     return lv;
 }
 
-// the bucket table of a's thresholds, built by the threads of a workgroup (tid < n, n a
-// multiple of 64 dividing 1024) into LDS: one pass over the (uniform) thresholds, each lane
-// counting for its 1024 / n buckets
+// the bucket table of a's thresholds, built by the threads of a workgroup (tid < n) into LDS:
+// each pass over the (uniform) thresholds counts for four buckets per lane, b = tid + k n
+// (one pass from 256 threads on)
 __device__ __forceinline__ void awgn_bucket_fill(const AwgnParams& a, uint16_t* bucket, uint32_t* thi,
                                                  uint32_t* tlo, int tid, int n) {
-    if (tid < a.nb) {
-        thi[tid] = a.thr_hi[tid];
-        tlo[tid] = a.thr_lo[tid];
+    for (int i = tid; i < a.nb; i += n) {
+        thi[i] = a.thr_hi[i];
+        tlo[i] = a.thr_lo[i];
     }
     constexpr int NB = 1 << AWGN_KB;
-    uint32_t base[4] = {0u, 0u, 0u, 0u}, cnt[4] = {0u, 0u, 0u, 0u};
-    const int per = NB / n;                 // 4 at 256 threads
-    for (int i = 0; i < a.nb; ++i) {
-        const uint32_t tb = __builtin_amdgcn_readfirstlane(a.thr_hi[i]) >> (32 - AWGN_KB);
+    for (int b0 = tid; b0 < NB; b0 += 4 * n) {
+        uint32_t base[4] = {0u, 0u, 0u, 0u}, cnt[4] = {0u, 0u, 0u, 0u};
+        for (int i = 0; i < a.nb; ++i) {
+            // (readfirstlane returns an int: shifted as unsigned, or the thresholds above 2^31
+            // would sign-extend out of every bucket)
+            const uint32_t tb = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.thr_hi[i]) >> (32 - AWGN_KB);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t b = (uint32_t)(tid + k * n);
-            base[k] += tb < b ? 1u : 0u;
-            cnt[k] += tb == b ? 1u : 0u;
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t b = (uint32_t)(b0 + k * n);
+                base[k] += tb < b ? 1u : 0u;
+                cnt[k] += tb == b ? 1u : 0u;
+            }
         }
-    }
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (k < per) bucket[tid + k * n] = (uint16_t)(base[k] | cnt[k] << 8);
+        for (int k = 0; k < 4; ++k)
+            if (b0 + k * n < NB) bucket[b0 + k * n] = (uint16_t)(base[k] | cnt[k] << 8);
+    }
 }
 
 // the levels of codewords 4 gq .. 4 gq + 3 at variable v (0-based; punctured / shortened

@@ -642,6 +642,13 @@ __device__ __forceinline__ void pack_channel_q8(const uint32_t* __restrict__ q8,
 #ifndef BS_USKIP
 #define BS_USKIP 1
 #endif
+// the variable phase's channel-table ids (a.btid, one global load per variable place and
+// iteration, whose result the table jump waits for) loaded before the check phase instead of
+// at their use: 1 for the multi-chunk instances (one workgroup per CU, so nothing else hides a
+// wave's L2 round trip after the barrier), 2 for every instance, 0 off (A/B switch)
+#ifndef BS_BKPF
+#define BS_BKPF 1
+#endif
 
 // Register budget: the small instances run at 64 VGPRs (WPE 8: three 9-wave workgroups per CU).
 // At a 72-register budget only two were resident (the waves of a workgroup are not spread evenly
@@ -843,6 +850,10 @@ k_bs(BsArgs a) {
     //   else:  S = sum of the C->V, APP_t = Q(ch) + S (hard decision, counters); unless last,
     //          Tv = clamp(Q(beta_{t+1} ch) + S) and V->C_e = clamp(Tv - C->V_e, +-15) per edge
     //   UCN:   the hard decision (APP_t >= 0; first: lw_0 >= 0) to HD[v] for the next check phase
+    constexpr bool BKPF = !XP && BS_BFIX && !BS_BTID_LDS && (BS_BKPF == 2 || (BS_BKPF == 1 && VPL > 1));
+    int bkp[VPL];                        // (BKPF) the ids of iteration tb's tables, loaded early
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) bkp[u] = -1;
     auto vn_phase = [&](const bool first, const bool last, const uint32_t bslice, const int tb)
                         __attribute__((always_inline)) {
         uint32_t wr = 0u, apos = 0u, nb = 0u;
@@ -876,7 +887,8 @@ k_bs(BsArgs a) {
             if constexpr (!XP && BS_BFIX) {
                 if (!first && !last && a.btid) {
                     const int col = (a.bcols == 1) ? 0 : pcol[u];
-                    if (col >= 0)
+                    if (BKPF) bk = __builtin_amdgcn_readfirstlane(bkp[u]);
+                    else if (col >= 0)
                         bk = __builtin_amdgcn_readfirstlane(BS_BTID_LDS ? (int)lds_w(a.off_btid + 4u * (uint32_t)col)
                                                                         : a.btid[(size_t)tb * a.btid_n + col]);
                 }
@@ -1135,6 +1147,15 @@ k_bs(BsArgs a) {
                 if (!XP && BS_BFIX && BS_BTID_LDS && a.btid)
                     for (int w = tl; w < (a.bcols == 1 ? 1 : a.btid_n); w += NT)
                         lds_put(a.off_btid + 4u * (uint32_t)w, (uint32_t)a.btid[(size_t)(t + 1) * a.btid_n + w]);
+            }
+        }
+        if constexpr (BKPF) {                // this iteration's variable phase: ids of row t + 1
+            if (t + 2 < a.T && a.btid) {
+#pragma unroll
+                for (int u = 0; u < VPL; ++u) {
+                    const int col = (a.bcols == 1) ? 0 : pcol[u];
+                    bkp[u] = col >= 0 ? a.btid[(size_t)(t + 1) * a.btid_n + col] : -1;
+                }
             }
         }
         // ======== check nodes ===================================================================
