@@ -1098,7 +1098,9 @@ k_bs(BsArgs a) {
         }
         if constexpr (UCN) {
 #pragma unroll
-            for (int p = 0; p < HDW; ++p) ghd[c][p] = (ucn && gchunk[c] >= 0) ? a.cn_hd[(size_t)ql * HDW + p] : 0u;
+            // (the table holds the cn_lanes check lanes: a one-chunk instance's waves past them
+            // read nothing -- their reads ran off the end of the allocation)
+            for (int p = 0; p < HDW; ++p) ghd[c][p] = (ucn && gchunk[c] >= 0 && ql < a.cn_lanes) ? a.cn_hd[(size_t)ql * HDW + p] : 0u;
         }
     }
     const uint32_t cstride = (uint32_t)(a.z * SLOT_B);
@@ -1150,7 +1152,7 @@ k_bs(BsArgs a) {
             }
         }
         if constexpr (BKPF) {                // this iteration's variable phase: ids of row t + 1
-            if (t + 2 < a.T && a.btid) {
+            if (t + 1 < a.T && a.btid) {     // (the last variable phase takes no table)
 #pragma unroll
                 for (int u = 0; u < VPL; ++u) {
                     const int col = (a.bcols == 1) ? 0 : pcol[u];

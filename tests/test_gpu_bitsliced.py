@@ -127,7 +127,9 @@ def _config(device, cfg, T=None, ucn_scale=None):
                                          ("C4", 8, 40000, "4")])
 def test_bitsliced_large_and_ucn(cuda_device, cfg, T, B, lpc, monkeypatch):
     monkeypatch.setenv("LDPC_BS_LPC", lpc)
-    dec, cp, c = _config(cuda_device, cfg, T, ucn_scale=0.8 if cfg == "C4" else None)
+    # (C4's trained alpha' equals its alpha and C3's does for t < 20: both fold to decoders
+    # without UCN unless alpha' is scaled)
+    dec, cp, c = _config(cuda_device, cfg, T, ucn_scale=0.8 if (cfg == "C4" or T <= 20) else None)
     name = dec.kernel_info()[1]
     assert name.startswith("bsl") and ",ucn" in name, name
     if cfg == "C3":
@@ -179,7 +181,8 @@ def test_bitsliced_ucn_off_grid_fixup(cuda_device, lpc):
 
 # ---- the compressed bit-sliced kernel (csrc/ldpc_bsc.hip): 5G BG1 (C5: flat [3,0,3], T=50,
 # puncture 1-144, shortening 1537-1584), whose per-edge slots do not fit the LDS --------------
-@pytest.mark.parametrize("T,B,snr", [(50, 3001, 2.0), (12, 40000, 1.75), (50, 33, 2.5)])
+# (T = 12 at 3 dB: about 40 % of the frames fail in the oracle; at 1.75 dB every one does)
+@pytest.mark.parametrize("T,B,snr", [(50, 3001, 2.0), (12, 40000, 3.0), (50, 33, 2.5)])
 def test_bitsliced_compressed_bg1(cuda_device, T, B, snr, monkeypatch):
     dec, cp, c = _config(cuda_device, "C5", T)
     name = dec.kernel_info()[1]
@@ -330,7 +333,8 @@ def test_bitsliced_q4_q3_large_graphs(cuda_device, cfg, q, monkeypatch):
     dec = NMSDecoder(proto, c["z"], W, 2, q, device=cuda_device)
     dec.punct, dec.short = c.get("punct", (0, 0)), c.get("short", (0, 0))
     assert dec.kernel_info()[1].startswith(("bsl[", "bsc[")), dec.kernel_info()
-    llr = dec.awgn(2500, float(cp.sigma(c["snr"] - 0.5)), seed=13)
+    # (BG1 at T = 12: 0.5 dB above its 3 dB point, where q = 3 still fails ~85 % of the frames)
+    llr = dec.awgn(2500, float(cp.sigma(c["snr"] + (0.5 if cfg == "C5" else -0.5))), seed=13)
     out = _both(dec, llr)
     assert np.array_equal(out["fused"][0], out["flood"][0]), (cfg, q, out["fused"][0], out["flood"][0])
     assert np.array_equal(out["fused"][1], out["flood"][1])
