@@ -186,6 +186,85 @@ __device__ __forceinline__ void awgn_levels4(const AwgnParams& a, P16 bucket, P3
     }
 }
 
+// ---- the channel kernels' form: each bucket carries its first threshold -----------------------
+// (ldpc_channel.hip: 8 KB of LDS per workgroup).  A bucket entry is {base | count << 8, the high
+// word of threshold `base` (0 if count = 0)}: one ds_read_b64 decides U's level whenever its
+// bucket holds at most one threshold (all but the few buckets where the CDF climbs by more than
+// one level within 2^-10: the far tails); the others scan on from there.  Same levels as
+// awgn_levels4.
+__device__ __forceinline__ void awgn_bucket_fill2(const AwgnParams& a, uint2* bucket, uint32_t* thi,
+                                                  uint32_t* tlo, int tid, int n) {
+    for (int i = tid; i < a.nb; i += n) {
+        thi[i] = a.thr_hi[i];
+        tlo[i] = a.thr_lo[i];
+    }
+    constexpr int NB = 1 << AWGN_KB;
+    for (int b0 = tid; b0 < NB; b0 += 4 * n) {
+        uint32_t base[4] = {0u, 0u, 0u, 0u}, cnt[4] = {0u, 0u, 0u, 0u}, first[4] = {0u, 0u, 0u, 0u};
+        for (int i = 0; i < a.nb; ++i) {
+            const uint32_t th = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.thr_hi[i]);
+            const uint32_t tb = th >> (32 - AWGN_KB);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t b = (uint32_t)(b0 + k * n);
+                base[k] += tb < b ? 1u : 0u;
+                if (tb == b) {
+                    if (cnt[k] == 0u) first[k] = th;
+                    ++cnt[k];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (b0 + k * n < NB) bucket[b0 + k * n] = make_uint2(base[k] | cnt[k] << 8, first[k]);
+    }
+}
+
+// the levels of codewords 4 gq .. 4 gq + 3 at variable v from the inline-threshold table: the
+// four bucket reads issued together, the level from the entry alone (U against the bucket's
+// first threshold), and only then the rare scans: buckets holding more thresholds, high-word ties
+template <typename P32>
+__device__ __forceinline__ void awgn_levels4b(const AwgnParams& a, const uint2* bucket, P32 thi, P32 tlo,
+                                              uint32_t v, uint64_t gq, int (&lv)[4]) {
+    uint32_t c[4] = {v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_Q};
+    Philox::gen(c, a.k0, a.k1);
+    uint2 e[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[j] = bucket[c[j] >> (32 - AWGN_KB)];
+    uint32_t ties = 0u, more = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t cnt = e[j].x >> 8;
+        const bool in = cnt != 0u;
+        const bool gt = in && c[j] > e[j].y;
+        lv[j] = (int)(e[j].x & 0xFFu) + (gt ? 1 : 0);
+        ties |= (in && c[j] == e[j].y) ? 1u << j : 0u;
+        more |= (cnt > 1u && gt) ? 1u << j : 0u;
+    }
+    if (more) {                         // (rare) more thresholds inside U's bucket
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (!((more >> j) & 1u)) continue;
+            const uint32_t cnt = e[j].x >> 8;
+            for (uint32_t i = 1; i < cnt; ++i) {
+                const uint32_t th = thi[lv[j]];
+                if (c[j] <= th) {
+                    if (c[j] == th) ties |= 1u << j;
+                    break;
+                }
+                ++lv[j];
+            }
+        }
+    }
+    if (ties) {
+        uint32_t r[4] = {v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_R};
+        Philox::gen(r, a.k0, a.k1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if ((ties >> j) & 1u) lv[j] = awgn_tie_scan(a.nb, thi, tlo, c[j], r[j], lv[j]);
+    }
+}
+
 // what a QMS element at 1-based bit `bit` is: 0 random, 1 punctured (LLR 0), 2 shortened (-clip)
 __device__ __forceinline__ int awgn_fixed(const AwgnParams& a, int bit) {
     if (a.ss > 0 && bit >= a.ss && bit <= a.se) return 2;

@@ -43,39 +43,34 @@ __global__ void __launch_bounds__(256) k_awgn(float* __restrict__ out, int64_t B
 
 // QMS: Box-Muller's replacement.  One thread per (global codeword quad, variable); variable
 // fastest, so each of the four row stores is coalesced across the wave.  The bucket table and
-// thresholds are built in LDS by each workgroup (awgn_bucket_fill, ~2 KB).
-template <bool WIDE>
+// thresholds are built in LDS by each workgroup (awgn_bucket_fill2, 8 KB).  A thread's (quad,
+// variable) advances by the grid stride without a division per item: the stride's quotient and
+// remainder by n_vars are fixed.
 __global__ void __launch_bounds__(256) k_awgn_qf(float* __restrict__ out, int64_t B, int n_vars,
                                                  AwgnParams a) {
-    __shared__ uint16_t bucket[1 << AWGN_KB];
+    __shared__ uint2 bucket[1 << AWGN_KB];
     __shared__ uint32_t thi[AWGN_NB_MAX], tlo[AWGN_NB_MAX];
     __shared__ float val[AWGN_NB_MAX + 1];
-    awgn_bucket_fill(a, bucket, thi, tlo, threadIdx.x, blockDim.x);
+    awgn_bucket_fill2(a, bucket, thi, tlo, threadIdx.x, blockDim.x);
     if (threadIdx.x <= (unsigned)a.nb) val[threadIdx.x] = a.val[threadIdx.x];
     __syncthreads();
     const uint64_t g0 = (uint64_t)a.offset;
     const uint64_t q0 = g0 >> 2;
     const int64_t nq = (int64_t)(((g0 + (uint64_t)B - 1) >> 2) - q0 + 1);
-    const int64_t total = nq * n_vars;
-    for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
-         id += (int64_t)gridDim.x * blockDim.x) {
-        int64_t m;
-        int v;
-        if (WIDE) {
-            m = id / n_vars;
-            v = (int)(id - m * n_vars);
-        } else {
-            const uint32_t q = (uint32_t)id / (uint32_t)n_vars;
-            m = q;
-            v = (int)((uint32_t)id - q * (uint32_t)n_vars);
-        }
+    const int64_t id0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t S = (int64_t)gridDim.x * blockDim.x;
+    int64_t m = id0 / n_vars;
+    int v = (int)(id0 - m * n_vars);
+    const int64_t dm = S / n_vars;
+    const int dv = (int)(S - dm * n_vars);
+    for (; m < nq; m += dm) {
         const uint64_t gq = q0 + (uint64_t)m;
         const int64_t bq = (int64_t)(gq * 4 - g0);          // batch index of the quad's word 0
         const int fx = awgn_fixed(a, v + 1);
         float l[4];
         if (fx == 0) {
             int lv[4];
-            awgn_levels4(a, bucket, thi, tlo, (uint32_t)v, gq, lv);
+            awgn_levels4b(a, bucket, thi, tlo, (uint32_t)v, gq, lv);
 #pragma unroll
             for (int j = 0; j < 4; ++j) l[j] = val[lv[j]];
         } else {
@@ -85,41 +80,38 @@ __global__ void __launch_bounds__(256) k_awgn_qf(float* __restrict__ out, int64_
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             if (bq + j >= 0 && bq + j < B) out[(bq + j) * n_vars + v] = l[j];
+        v += dv;
+        if (v >= n_vars) {
+            v -= n_vars;
+            ++m;
+        }
     }
 }
 
 // QMS bytes for the bit-sliced decoders (ldpc_decode_awgn): [packs][n_vars][32] u8, byte r of
 // (pack, v) = grid value + 16 of codeword 32 pack + r (+ 32 on a shortened bit: the BIG
 // instances' marker, pack_channel) — the bytes pack_channel builds from float LLRs, 576 B per
-// wman codeword instead of 2,304.  One thread per (pack, variable, codeword quad), the quad
+// wman codeword instead of 2,304.  One thread per 4-byte word (4 codewords of one variable), word
 // index fastest: a wave stores 8 variables x 32 bytes, contiguous.  Rows past B are generated
-// too (the decoder masks them).
-template <bool WIDE>
+// too (the decoder masks them).  The grid stride is a multiple of 8 words: a thread keeps its
+// word index and steps (pack, variable) by the stride's fixed quotient and remainder.
 __global__ void __launch_bounds__(256) k_awgn_q8(uint32_t* __restrict__ out, int64_t npk, int n_vars,
                                                  AwgnParams a, int qmax) {
-    __shared__ uint16_t bucket[1 << AWGN_KB];
+    __shared__ uint2 bucket[1 << AWGN_KB];
     __shared__ uint32_t thi[AWGN_NB_MAX], tlo[AWGN_NB_MAX];
-    awgn_bucket_fill(a, bucket, thi, tlo, threadIdx.x, blockDim.x);
+    awgn_bucket_fill2(a, bucket, thi, tlo, threadIdx.x, blockDim.x);
     __syncthreads();
     const uint64_t g0 = (uint64_t)a.offset;
     const int sh = (int)(g0 & 3);                            // the batch's first quad offset
-    const int64_t total = npk * n_vars * 8;
     const uint32_t boff = (uint32_t)(16 + a.kmin);           // byte of level 0
-    for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
-         id += (int64_t)gridDim.x * blockDim.x) {
-        const int i = (int)(id & 7);
-        int64_t pk;
-        int v;
-        if (WIDE) {
-            const int64_t pv = id >> 3;
-            pk = pv / n_vars;
-            v = (int)(pv - pk * n_vars);
-        } else {                         // (a 32-bit division when the grid has < 2^32 words)
-            const uint32_t pv = (uint32_t)id >> 3;
-            const uint32_t q = pv / (uint32_t)n_vars;
-            pk = q;
-            v = (int)(pv - q * (uint32_t)n_vars);
-        }
+    const int64_t id0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int i = (int)(id0 & 7);
+    const int64_t pv0 = id0 >> 3, dpv = ((int64_t)gridDim.x * blockDim.x) >> 3;
+    int64_t pk = pv0 / n_vars;
+    int v = (int)(pv0 - pk * n_vars);
+    const int64_t dpk = dpv / n_vars;
+    const int dv = (int)(dpv - dpk * n_vars);
+    for (; pk < npk; pk += dpk) {
         const int fx = awgn_fixed(a, v + 1);
         uint32_t w;
         if (fx == 1) {
@@ -129,19 +121,24 @@ __global__ void __launch_bounds__(256) k_awgn_q8(uint32_t* __restrict__ out, int
         } else {
             const uint64_t gb = g0 + (uint64_t)(pk * 32 + 4 * i);
             int la[4];
-            awgn_levels4(a, bucket, thi, tlo, (uint32_t)v, gb >> 2, la);
+            awgn_levels4b(a, bucket, thi, tlo, (uint32_t)v, gb >> 2, la);
             w = ((uint32_t)la[0] + boff) | ((uint32_t)la[1] + boff) << 8 | ((uint32_t)la[2] + boff) << 16 |
                 ((uint32_t)la[3] + boff) << 24;
             if (sh) {               // (wave-uniform) a batch offset off the quads: rows from two quads
                 int lb[4];
-                awgn_levels4(a, bucket, thi, tlo, (uint32_t)v, (gb >> 2) + 1, lb);
+                awgn_levels4b(a, bucket, thi, tlo, (uint32_t)v, (gb >> 2) + 1, lb);
                 const uint32_t wb = ((uint32_t)lb[0] + boff) | ((uint32_t)lb[1] + boff) << 8 |
                                     ((uint32_t)lb[2] + boff) << 16 | ((uint32_t)lb[3] + boff) << 24;
                 // rows k = 0..3 are words sh + k of the quad pair (la, lb): one byte funnel shift
                 w = __builtin_amdgcn_alignbyte(wb, w, (uint32_t)sh);
             }
         }
-        out[id] = w;
+        out[(pk * n_vars + v) * 8 + i] = w;
+        v += dv;
+        if (v >= n_vars) {
+            v -= n_vars;
+            ++pk;
+        }
     }
 }
 
@@ -185,10 +182,7 @@ extern "C" int ldpc_channel_awgn(float* llr_dev, int64_t B, int32_t n_vars, doub
         const int64_t nq = (int64_t)((((uint64_t)offset + (uint64_t)B - 1) >> 2) - ((uint64_t)offset >> 2) + 1);
         const int64_t total = nq * n_vars;
         const unsigned grid = (unsigned)std::min<int64_t>(8192, (total + 255) / 256);
-        if (total + (int64_t)grid * 256 >= ((int64_t)1 << 32))
-            hipLaunchKernelGGL((ldpc::k_awgn_qf<true>), dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a);
-        else
-            hipLaunchKernelGGL((ldpc::k_awgn_qf<false>), dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a);
+        hipLaunchKernelGGL(ldpc::k_awgn_qf, dim3(grid), dim3(256), 0, s, llr_dev, B, (int)n_vars, a);
         return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
     }
     // float modes: Box-Muller per element pair
@@ -210,10 +204,7 @@ int channel_q8(uint32_t* q8, int64_t B, int n_vars, const AwgnParams& a, int qma
     const int64_t npk = (B + 31) / 32;
     const int64_t total = npk * n_vars * 8;
     const unsigned grid = (unsigned)std::min<int64_t>(8192, (total + 255) / 256);
-    if (total + (int64_t)grid * 256 >= ((int64_t)1 << 32))
-        hipLaunchKernelGGL(k_awgn_q8<true>, dim3(grid), dim3(256), 0, s, q8, npk, n_vars, a, qmax);
-    else
-        hipLaunchKernelGGL(k_awgn_q8<false>, dim3(grid), dim3(256), 0, s, q8, npk, n_vars, a, qmax);
+    hipLaunchKernelGGL(k_awgn_q8, dim3(grid), dim3(256), 0, s, q8, npk, n_vars, a, qmax);
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 
