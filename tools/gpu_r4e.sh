@@ -10,4 +10,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-f
 cat $O/bench_C2.json
 timeout -k 10 300 python3 bench.py --kernel flood --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_flood.json 2> $O/bench_flood.err || exit 1
 cat $O/bench_flood.json
-bash tools/gpu_session.sh r4e ab:C4:ab_libs/llrall.so,default:3 || exit 1
+bash tools/gpu_session.sh r4e ab:C4:ab_libs/llrall.so,ab_libs/afix.so,default,env=LDPC_BS_STAGGER=50,env=LDPC_BS_STAGGER=200:2 ab:C2:ab_libs/afix.so,default:2 || exit 1
