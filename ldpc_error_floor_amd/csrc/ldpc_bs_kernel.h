@@ -611,6 +611,10 @@ __device__ __forceinline__ void pack_channel_q8(const uint32_t* __restrict__ q8,
 #ifndef BS_REREAD
 #define BS_REREAD 0
 #endif
+// (the multi-chunk instances, one workgroup per CU with registers to spare: BS_KEEP_MC)
+#ifndef BS_KEEP_MC
+#define BS_KEEP_MC BS_KEEP
+#endif
 #ifndef BS_KEEP
 #define BS_KEEP 4
 #endif
@@ -937,7 +941,8 @@ k_bs(BsArgs a) {
             // again (BS_KEEP: 4 measured best within the 64-register budget)
             // (at most DV - 1: 802.11n, DV = 4, keeps three and reads its fourth edge again,
             // 14.48 -> 14.41 ms same box (r3zh); wman and 5G BG2 keep BS_KEEP = 4 of 6 / 8)
-            constexpr int KEEP = BS_KEEP < DV ? BS_KEEP : DV - 1;
+            constexpr int KEEP0 = (VPL > 1 || CPL > 1) ? BS_KEEP_MC : BS_KEEP;
+            constexpr int KEEP = KEEP0 < DV ? KEEP0 : DV - 1;
             uint32_t mn[KEEP > 0 ? KEEP : 1], mb[KEEP > 0 ? KEEP : 1][4];
             uint32_t S[SB];
 #pragma unroll
