@@ -611,9 +611,15 @@ __device__ __forceinline__ void pack_channel_q8(const uint32_t* __restrict__ q8,
 #ifndef BS_REREAD
 #define BS_REREAD 0
 #endif
-// (the multi-chunk instances, one workgroup per CU with registers to spare: BS_KEEP_MC)
+// (the multi-chunk instances, one workgroup per CU with registers to spare: BS_KEEP_MC; 5G BG2
+// keeps 7 of its 8: C4 11.85-11.88 -> 11.60-11.65 ms, 6: 11.76-11.79, same box, r4f)
+// the multi-chunk instances' real-edge-position word, read per iteration through an opaque copy
+// (A/B switch; see rpk in k_bs)
+#ifndef BS_RPW
+#define BS_RPW 1
+#endif
 #ifndef BS_KEEP_MC
-#define BS_KEEP_MC BS_KEEP
+#define BS_KEEP_MC 7
 #endif
 #ifndef BS_KEEP
 #define BS_KEEP 4
@@ -941,7 +947,7 @@ k_bs(BsArgs a) {
             // again (BS_KEEP: 4 measured best within the 64-register budget)
             // (at most DV - 1: 802.11n, DV = 4, keeps three and reads its fourth edge again,
             // 14.48 -> 14.41 ms same box (r3zh); wman and 5G BG2 keep BS_KEEP = 4 of 6 / 8)
-            constexpr int KEEP0 = (VPL > 1 || CPL > 1) ? BS_KEEP_MC : BS_KEEP;
+            constexpr int KEEP0 = ((VPL > 1 || CPL > 1) && !UCN) ? BS_KEEP_MC : BS_KEEP;
             constexpr int KEEP = KEEP0 < DV ? KEEP0 : DV - 1;
             uint32_t mn[KEEP > 0 ? KEEP : 1], mb[KEEP > 0 ? KEEP : 1][4];
             uint32_t S[SB];
@@ -1108,6 +1114,20 @@ k_bs(BsArgs a) {
             for (int p = 0; p < HDW; ++p) ghd[c][p] = (ucn && gchunk[c] >= 0 && ql < a.cn_lanes) ? a.cn_hd[(size_t)ql * HDW + p] : 0u;
         }
     }
+    // the lane's real edge positions, one word for all its chunks (bit RB c + m: position m of
+    // chunk c holds an edge of the lane's check), read through an opaque copy per iteration so
+    // [LPC m + j < degree] is not hoisted out of the T loop as CPL x EPL 64-bit lane masks whose
+    // SGPR pairs the loop spilled (bsc: 166 v_readlane reloads in the loop body before).  The
+    // multi-chunk instances only: the one-chunk builds spill VGPRs with it (C2 3 -> 9, C3 7 -> 10)
+    constexpr bool RPW = BS_RPW && CPL > 1;
+    constexpr int RB = EPL;
+    static_assert(CPL * RB <= 32, "real-position word");
+    uint32_t rpk = 0u;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+#pragma unroll
+        for (int m = 0; m < EPL; ++m)
+            if (RPW && (LPC * m + LPC - 1 < cn_dmin || LPC * m + cj < gdeg[c])) rpk |= 1u << (RB * c + m);
     const uint32_t cstride = (uint32_t)(a.z * SLOT_B);
     const uint32_t tabu = (uint32_t)(a.arows * LUT_W * 4);        // alpha' tables after the alpha ones
     constexpr bool GBL = BS_GBLDS && CPL == 1 && !BS_CH_LDS;
@@ -1127,7 +1147,7 @@ k_bs(BsArgs a) {
         const int nx = (t + 1) & 1;
 #pragma unroll
         for (int u = 0; u < VPL; ++u) asm volatile("" : "+s"(dw[u]), "+s"(dwmin[u]));   // compared per use, not hoisted as masks
-        asm volatile("" : "+s"(cn_dmin));
+        if (!RPW) asm volatile("" : "+s"(cn_dmin));
         // next iteration's tables (their slots were last read two phases ago)
         if (t + 1 < a.T) {
             // (the lane index made opaque per iteration: the copy addresses are recomputed here
@@ -1185,12 +1205,15 @@ k_bs(BsArgs a) {
             }
             uint32_t ctab = PKG ? (cbase >> 16) : gtab[c];
             if constexpr (PKG) cbase &= 0xFFFFu;
-            const int cdeg = gdeg[c];
             int gmc = gm[c];
             asm volatile("" : "+s"(gmc));
-            // slot m of the lane: always a real edge while LPC m + LPC - 1 < cn_dmin
+            uint32_t rp = rpk;
+            if (RPW) asm volatile("" : "+v"(rp));
+            const int cdeg = gdeg[c];
+            // slot m of the lane: a real edge (always while LPC m + LPC - 1 < cn_dmin)
             auto real = [&](int m) __attribute__((always_inline)) -> bool {
-                return LPC * m + LPC - 1 < cn_dmin || LPC * m + cj < cdeg;
+                if constexpr (RPW) return ((rp >> (RB * c + m)) & 1u) != 0u;
+                else return LPC * m + LPC - 1 < cn_dmin || LPC * m + cj < cdeg;
             };
             auto caddr = [&](int m) __attribute__((always_inline)) -> uint32_t {
                 return real(m) ? cbase + m * cstride : a.off_pad;

@@ -368,7 +368,26 @@ k_bsc(BscArgs a) {
         for (int p = 0; p < CVW; ++p) gvar[c][p] = gchunk[c] >= 0 ? a.cn_var[(size_t)ql * CVW + p] : 0u;
     }
     const uint32_t sstride = (uint32_t)(4 * a.z);
-    int cn_dmin = a.cn_dmin;
+    // the lane's real edge positions, one word for all its chunks: bit RB c + m = position m of
+    // chunk c holds an edge of the lane's check, bit RB c + EPL = the lane holds a check.  Read
+    // through an opaque copy per iteration, so [L m + j < degree] is not hoisted out of the T
+    // loop as CPL x EPL x 2 64-bit lane masks, whose SGPR pairs the loop spilled and reloaded by
+    // v_readlane (C5: 166 reloads in the loop body)
+    constexpr int RB = EPL + 1;                  // bits per chunk
+    static_assert(CPL * RB <= 32, "real-position word");
+    uint32_t rpk = 0u;
+    {
+        const int cn_dmin = a.cn_dmin;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int L = (!MIX || gl4[c]) ? LPC : LPC / 2;
+            const int cjl = lane & (L - 1);
+#pragma unroll
+            for (int m = 0; m < EPL; ++m)
+                if (L * m + L - 1 < cn_dmin || L * m + cjl < gdeg[c]) rpk |= 1u << (RB * c + m);
+            if (gdeg[c] > 0) rpk |= 1u << (RB * c + EPL);
+        }
+    }
     __syncthreads();
 
     for (int t = 0; t < a.T; ++t) {
@@ -381,7 +400,8 @@ k_bsc(BscArgs a) {
         const int nx = (t + 1) & 1;
 #pragma unroll
         for (int u = 0; u < VPL; ++u) asm volatile("" : "+s"(dw[u]));
-        asm volatile("" : "+s"(cn_dmin));
+        uint32_t rp = rpk;
+        asm volatile("" : "+v"(rp));
         if (t + 1 < a.T) {
             // (the lane index made opaque per iteration: the copy addresses are recomputed here
             // rather than hoisted out of the T loop into registers the loop body spills)
@@ -406,14 +426,14 @@ k_bsc(BscArgs a) {
             constexpr int L = decltype(LC)::value;
             constexpr int OBL = 4 / L;
             const int cjl = lane & (L - 1);
-            const int cdeg = gdeg[c];
             int gmc = gm[c];
             asm volatile("" : "+s"(gmc));
             uint32_t sbase = gslot[c];
             asm volatile("" : "+v"(sbase));
             auto real = [&](int m) __attribute__((always_inline)) -> bool {
-                return L * m + L - 1 < cn_dmin || L * m + cjl < cdeg;
+                return ((rp >> (RB * c + m)) & 1u) != 0u;
             };
+            const bool has_check = ((rp >> (RB * c + EPL)) & 1u) != 0u;
             // V->C = clamp(Tv - C->V_old, +-15) of the lane's edges (padding: negative, 15)
             v4u q1o = {0u, 0u, 0u, 0u}, q2o = {0u, 0u, 0u, 0u};
             if (t > 0) {
@@ -450,7 +470,7 @@ k_bsc(BscArgs a) {
                 }
                 abs_sat(Xs[m], x);
                 ns[m] = x[6];
-                if (!(L * m + L - 1 < cn_dmin) && !real(m)) {
+                if (!real(m)) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) Xs[m][i] = ~0u;
                     ns[m] = ~0u;
@@ -499,7 +519,7 @@ k_bsc(BscArgs a) {
                     fixed = true;
                     uint32_t p1[4], p2[4];
                     table_asm2(p1, p2, m1, m2, k);
-                    if (cdeg > 0 && cjl == 0) {
+                    if (has_check && cjl == 0) {
                         lds_qput(grec[c], p1);
                         lds_qput(grec[c] + REC_Q2, p2);
                     }
@@ -520,7 +540,7 @@ k_bsc(BscArgs a) {
             // the record: lane j writes planes OBL j .. of q1 and q2 (the whole group has read the
             // old record above: same wave, LDS operations in program order); idle lanes past
             // the last check (degree 0) share its clamped record address and must not write
-            if (!fixed && cdeg > 0) {
+            if (!fixed && has_check) {
 #pragma unroll
                 for (int b = 0; b < OBL; ++b) {
                     lds_put(grec[c] + 4u * (uint32_t)(OBL * cjl + b), qb[b][0]);
