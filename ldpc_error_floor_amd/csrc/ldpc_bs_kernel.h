@@ -618,6 +618,9 @@ __device__ __forceinline__ void pack_channel_q8(const uint32_t* __restrict__ q8,
 #ifndef BS_RPW
 #define BS_RPW 1
 #endif
+#ifndef BS_VVO
+#define BS_VVO 1
+#endif
 #ifndef BS_KEEP_MC
 #define BS_KEEP_MC 7
 #endif
@@ -1148,6 +1151,13 @@ k_bs(BsArgs a) {
 #pragma unroll
         for (int u = 0; u < VPL; ++u) asm volatile("" : "+s"(dw[u]), "+s"(dwmin[u]));   // compared per use, not hoisted as masks
         if (!RPW) asm volatile("" : "+s"(cn_dmin));
+        // (the lane's variable made opaque per iteration on the multi-chunk instances: [v >= 0]
+        // and [v < target bits] are compared per use, not held through the loop as spilled
+        // 64-bit lane masks)
+        if (BS_VVO == 2 || (BS_VVO && RPW)) {
+#pragma unroll
+            for (int u = 0; u < VPL; ++u) asm volatile("" : "+v"(vv[u]));
+        }
         // next iteration's tables (their slots were last read two phases ago)
         if (t + 1 < a.T) {
             // (the lane index made opaque per iteration: the copy addresses are recomputed here
