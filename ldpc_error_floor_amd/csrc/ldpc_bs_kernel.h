@@ -65,6 +65,10 @@ constexpr BsInst kBsInst[] = {
     // 5G BG2 with 10 waves (20 variable and 20 check chunks, no idle place) at up to 168 VGPRs
     // (no spills, 2-3 waves per SIMD): LDPC_BS_INST=7 A/B
     {10, 8, 2, 2, 2, true, true, false, 3, 10},
+    // 802.11n as a multi-chunk instance: two variables and two check chunks per lane on 8 waves,
+    // two workgroups per CU at up to 128 VGPRs (the 80-VGPR one-chunk build spills 7): A/B only
+    // (LDPC_BS_INST=8)
+    {24, 4, 4, 2, 2, true, true, false, 4, 8},
 };
 constexpr int kBsNInst = sizeof(kBsInst) / sizeof(kBsInst[0]);
 

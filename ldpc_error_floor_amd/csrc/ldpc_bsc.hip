@@ -400,6 +400,12 @@ k_bsc(BscArgs a) {
         const int nx = (t + 1) & 1;
 #pragma unroll
         for (int u = 0; u < VPL; ++u) asm volatile("" : "+s"(dw[u]));
+        // (the lane's variables opaque per iteration: [v >= 0], [v < target bits] compared per
+        // use, not held through the loop as spilled lane masks; BS_VVO as bsl)
+        if (BS_VVO) {
+#pragma unroll
+            for (int u = 0; u < VPL; ++u) asm volatile("" : "+v"(vv[u]));
+        }
         uint32_t rp = rpk;
         asm volatile("" : "+v"(rp));
         if (t + 1 < a.T) {
