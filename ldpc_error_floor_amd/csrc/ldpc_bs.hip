@@ -86,7 +86,7 @@ struct BsPlan {
     bool ok = false;
     int inst = -1, nw = 0, cn_lanes = 0, arows = 1, bcols = 1;
     uint32_t off_slots = 0, off_pad = 0, off_zero = 0, off_red = 0, off_alut = 0, off_blut = 0, off_hdz = 0,
-             off_btid = 0, off_ch = 0;
+             off_btid = 0, off_ch = 0, off_hdl = 0;
     int cn_dmin = 0;
     bool ucn = false;
     bool colalign = false;         // variable lanes: each column on a half-wave of its own
@@ -225,6 +225,11 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     } else if (BS_GBLDS && k.CPL == 1) {           // the check lanes' slot-base words
         p.off_ch = (uint32_t)o;
         o += (size_t)4 * 64 * p.nw;
+    }
+    if (BS_HDLDS && k.UCN && k.CPL == 1) {         // the check lanes' hard-decision addresses
+        const int EPL = (k.D + k.LPC - 1) / k.LPC, HDW = (EPL + 1) / 2;
+        p.off_hdl = (uint32_t)o;
+        o += (size_t)4 * HDW * 64 * p.nw;
     }
     p.lds = (o + 15) & ~(size_t)15;
     if (p.lds > BS_LDS_MAX) return p;
@@ -736,6 +741,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.off_blut = p.off_blut;
     a.off_hdz = p.off_hdz;
     a.off_btid = p.off_btid;
+    a.off_hdl = p.off_hdl;
     a.off_ch = p.off_ch;
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // -DBS_DIAG builds
     const int nblocks = (int)((b.B + PACK - 1) / PACK);

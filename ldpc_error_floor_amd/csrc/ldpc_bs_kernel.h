@@ -116,6 +116,9 @@ struct BsArgs {
                   // tests alone cost 4 %.)
     uint64_t ucn_iter;           // bit t (t < 64): iteration t's alpha' differs from alpha (its
                                  // check phase needs the syndromes); iterations >= 64: on
+    uint32_t off_hdl;            // BS_HDLDS (one-chunk UCN instances): the check lanes' packed
+                                 // hard-decision addresses, [HDW][lane] words
+    uint32_t pad_;
 };
 
 // ---- bit-plane arithmetic ---------------------------------------------------------------------
@@ -624,6 +627,11 @@ __device__ __forceinline__ void pack_channel_q8(const uint32_t* __restrict__ q8,
 #endif
 #ifndef BS_VVO
 #define BS_VVO 1
+#endif
+// the one-chunk UCN instances' packed hard-decision addresses (HDW words per check lane) in LDS,
+// read at each check phase, instead of registers the 80-VGPR build spilled (A/B switch)
+#ifndef BS_HDLDS
+#define BS_HDLDS 1
 #endif
 #ifndef BS_KEEP_MC
 #define BS_KEEP_MC 7
@@ -1139,6 +1147,11 @@ k_bs(BsArgs a) {
     const uint32_t tabu = (uint32_t)(a.arows * LUT_W * 4);        // alpha' tables after the alpha ones
     constexpr bool GBL = BS_GBLDS && CPL == 1 && !BS_CH_LDS;
     if constexpr (GBL) lds_put(a.off_ch + 4u * (uint32_t)tid, gbase[0]);
+    constexpr bool HDL = BS_HDLDS && UCN && CPL == 1;
+    if constexpr (HDL) {
+#pragma unroll
+        for (int p = 0; p < HDW; ++p) lds_put(a.off_hdl + 4u * (uint32_t)(p * NT + tid), ghd[0][p]);
+    }
     __syncthreads();
 
     for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
@@ -1254,13 +1267,27 @@ k_bs(BsArgs a) {
             if constexpr (UCN) {
                 if (ucn_t) {
                     // (the packed addresses made opaque per iteration: unpacked per use, not
-                    // hoisted out of the T loop as EPL registers that the loop then spilled)
+                    // hoisted out of the T loop as EPL registers that the loop then spilled;
+                    // HDL: read from LDS, through a lane index the loop cannot hoist)
+                    uint32_t hwv[HDW];
+                    if constexpr (HDL) {
+                        uint32_t all = ~0u;
+                        asm volatile("" : "+s"(all));
+                        const uint32_t ln = __builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
 #pragma unroll
-                    for (int p = 0; p < HDW; ++p) asm volatile("" : "+v"(ghd[c][p]));
+                        for (int p = 0; p < HDW; ++p)
+                            hwv[p] = lds_w(a.off_hdl + 4u * (uint32_t)(p * NT) + ((uint32_t)wave << 8) + 4u * ln);
+                    } else {
+#pragma unroll
+                        for (int p = 0; p < HDW; ++p) {
+                            asm volatile("" : "+v"(ghd[c][p]));
+                            hwv[p] = ghd[c][p];
+                        }
+                    }
 #pragma unroll
                     for (int m = 0; m < EPL; ++m) {
                         if (SKIPM && m >= gmc) continue;
-                        const uint32_t hw = ghd[c][m >> 1];
+                        const uint32_t hw = hwv[m >> 1];
                         syn ^= lds_w((m & 1) ? (hw >> 16) : (hw & 0xFFFFu));
                     }
                     syn ^= qperm<QP_X1>(syn);

@@ -337,7 +337,7 @@ k_bsc(BscArgs a) {
     // check groups (as bsl): lane LPC c + j of a chunk takes edges k = LPC m + j of check c
     // (MIX: each chunk's lanes per check from its lane map; lane 0 of a chunk always holds a check)
     int gchunk[CPL], gdeg[CPL], gm[CPL], gl4[CPL];
-    uint32_t gslot[CPL], grec[CPL], gvar[CPL][CVW];
+    uint32_t gslot[CPL], grec[CPL], gtab[CPL], gvar[CPL][CVW];
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
         gchunk[c] = __builtin_amdgcn_readfirstlane(a.cn_chunk[wave * CPL + c]);
@@ -363,6 +363,7 @@ k_bsc(BscArgs a) {
         (void)nwv;
         gslot[c] = (uint32_t)(4 * (a.row_lay[2 * ci] + cjc * a.row_lay[2 * ci + 1] + (cc - ci * a.z)));
         grec[c] = a.off_rec + rec_off((uint32_t)min(cc, a.n_checks - 1));
+        gtab[c] = a.off_alut + (uint32_t)((a.arows > 1 ? ci : 0) * LUT_W * 4) + (uint32_t)(cjc * (4 / Lc) * 64);
 #pragma unroll
         for (int p = 0; p < CVW; ++p) gvar[c][p] = gchunk[c] >= 0 ? a.cn_var[(size_t)ql * CVW + p] : 0u;
     }
@@ -533,16 +534,7 @@ k_bsc(BscArgs a) {
             uint32_t qb[OBL][2];
             if (!fixed) {
                 const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
-                // the lane's table bits (and its row's table when alpha is per row: the row from
-                // the record address, whose check index it encodes), recomputed per use rather
-                // than held per chunk through the loop (a spilled register before)
-                uint32_t tabb = a.off_alut + (uint32_t)(cjl * OBL * 64);
-                if (a.arows > 1) {
-                    const uint32_t ro = grec[c] - a.off_rec;
-                    const int cr = (int)(((ro >> 9) << 4) | ((ro >> 4) & 15u));
-                    tabb += (uint32_t)(min(cr / a.z, a.n_checks / a.z - 1) * LUT_W * 4);
-                }
-                const uint32_t tab = tabb + (uint32_t)((t & 1) * AL * 4);
+                const uint32_t tab = gtab[c] + (uint32_t)((t & 1) * AL * 4);
 #pragma unroll
                 for (int b = 0; b < OBL; ++b) {
                     uint32_t o[2];
