@@ -630,6 +630,11 @@ __device__ __forceinline__ void pack_channel_q8(const uint32_t* __restrict__ q8,
 #endif
 // the one-chunk UCN instances' packed hard-decision addresses (HDW words per check lane) in LDS,
 // read at each check phase, instead of registers the 80-VGPR build spilled (A/B switch)
+// the one-chunk instances' channel-table ids by scalar loads (s_load from the constant address
+// space: an SGPR result, no vector-memory round trip and vmcnt wait per variable phase) (A/B)
+#ifndef BS_BTID_S
+#define BS_BTID_S 1
+#endif
 #ifndef BS_HDLDS
 #define BS_HDLDS 1
 #endif
@@ -913,9 +918,11 @@ k_bs(BsArgs a) {
                 if (!first && !last && a.btid) {
                     const int col = (a.bcols == 1) ? 0 : pcol[u];
                     if (BKPF) bk = __builtin_amdgcn_readfirstlane(bkp[u]);
-                    else if (col >= 0)
-                        bk = __builtin_amdgcn_readfirstlane(BS_BTID_LDS ? (int)lds_w(a.off_btid + 4u * (uint32_t)col)
-                                                                        : a.btid[(size_t)tb * a.btid_n + col]);
+                    else if (col >= 0)   // (BS_BTID_S: a scalar load, through the constant address space)
+                        bk = __builtin_amdgcn_readfirstlane(
+                            BS_BTID_LDS ? (int)lds_w(a.off_btid + 4u * (uint32_t)col)
+                            : BS_BTID_S ? (int)((const ConstW*)a.btid)[(size_t)tb * a.btid_n + col]
+                                        : a.btid[(size_t)tb * a.btid_n + col]);
                 }
             }
             if (!last) {
