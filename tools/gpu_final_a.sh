@@ -5,7 +5,8 @@ set -o pipefail
 export TMPDIR=/tmp
 TAG=${TAG:-r4f}
 OUT=gpurun_out/ev_$TAG; mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest tests -m gpu -v -rs --timeout 150 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -3 $OUT/pytest_gpu.log; grep -E "FAILED|^ERROR" $OUT/pytest_gpu.log | head -20
+rc=0
+[ -n "$SKIP_TESTS" ] || { timeout -k 10 900 python -u -m pytest tests -m gpu -v -rs --timeout 150 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -3 $OUT/pytest_gpu.log; grep -E "FAILED|^ERROR" $OUT/pytest_gpu.log | head -20; }
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
 cat $OUT/smoke.log
