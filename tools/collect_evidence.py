@@ -25,10 +25,16 @@ def main():
     ks = os.path.join(src, "bench_trace", "bench_kernel_stats.csv")
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(dst, "bench_c2_rocprof_kernel_stats.csv"))
+    sys.path.insert(0, ROOT)
+    from ldpc_error_floor_amd.build import source_fingerprint
+    fp = source_fingerprint()
     for tj in glob.glob(os.path.join(src, "traffic_fused5_*.json")) + \
             glob.glob(os.path.join(src, "traffic_bsl_*.json")) + \
+            glob.glob(os.path.join(src, "traffic_bsc_*.json")) + \
             glob.glob(os.path.join(src, "traffic_flood*.json")):
         d = json.load(open(tj))
+        if d.get("src_fingerprint") != fp:       # another build's profile that rode along
+            continue
         old = d.get("source", "")
         cfg = os.path.basename(old.rstrip("/"))
         d["source"] = os.path.relpath(os.path.join(dst, cfg), ROOT)
