@@ -110,6 +110,20 @@ static void validation_cases() {
     CHECK(host::analyze_weights(g, 3, a.data(), nullptr, b.data(), wi) == LDPC_OK);
     CHECK(wi.beta_one == 0 && wi.beta_id_mask == 1u);
     std::fill(b.begin(), b.end(), 1.0f);
+    // UCN iterations: bit t set when alpha'_t differs from alpha_t at some edge (the kernels
+    // skip the unsatisfied-check work of the others); no alpha' -> no bit
+    CHECK(host::analyze_weights(g, 3, a.data(), nullptr, b.data(), wi) == LDPC_OK && wi.ucn_iter_mask == 0u);
+    {
+        std::vector<float> u(a);
+        u[(size_t)1 * g.E + (g.E - 1)] = 0.5f;               // iteration 1, last edge
+        CHECK(host::analyze_weights(g, 3, a.data(), u.data(), b.data(), wi) == LDPC_OK);
+        CHECK(wi.ucn_iter_mask == 2u);
+        u[0] = 0.25f;                                         // iteration 0, first edge
+        CHECK(host::analyze_weights(g, 3, a.data(), u.data(), b.data(), wi) == LDPC_OK);
+        CHECK(wi.ucn_iter_mask == 3u);
+        CHECK(host::analyze_weights(g, 3, a.data(), a.data(), b.data(), wi) == LDPC_OK);
+        CHECK(wi.ucn_iter_mask == 0u);
+    }
 
     // decode parameters
     ldpc_decode_params p{};
@@ -281,8 +295,25 @@ static void vorder_cases(int rounds) {
     CHECK(c.first == 4 + 2 && c.second == 2 + 2);   // (the empty second half-wave: 1 per round)
 }
 
+// the QMS level sampler's thresholds and level values (host::awgn_qms_levels) as JSON, for
+// tests/test_host_sanitized.py to compare with oracle/philox_oracle.qms_levels
+static int qms(double sigma, int q_bit) {
+    int nb = 0, kmin = 0;
+    uint32_t hi[64], lo[64];
+    float val[65];
+    host::awgn_qms_levels(sigma, q_bit, &nb, &kmin, hi, lo, val);
+    std::printf("{\"nb\": %d, \"kmin\": %d, \"thr\": [", nb, kmin);
+    for (int j = 0; j < nb; ++j)
+        std::printf("%s%llu", j ? ", " : "", (unsigned long long)(((uint64_t)hi[j] << 32) | lo[j]));
+    std::printf("], \"val\": [");
+    for (int j = 0; j <= nb; ++j) std::printf("%s%.9g", j ? ", " : "", (double)val[j]);
+    std::printf("]}\n");
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc >= 4 && std::string(argv[1]) == "tables") return tables(argv[2], std::atoi(argv[3]));
+    if (argc >= 4 && std::string(argv[1]) == "qms") return qms(std::atof(argv[2]), std::atoi(argv[3]));
     if (argc >= 2 && std::string(argv[1]) == "selftest") {
         validation_cases();
         fuzz(argc >= 3 ? std::atoi(argv[2]) : 3000);

@@ -70,3 +70,20 @@ def test_tables_equal_python_graph(host_check, path):
     col_ptr = np.concatenate([[0], np.cumsum(g.vn_deg)])
     np.testing.assert_array_equal(t["col_ptr"], col_ptr)
     np.testing.assert_array_equal(np.asarray(t["col_pe"]), np.lexsort((g.pe_row, g.pe_col)))
+
+
+@pytest.mark.parametrize("q", [6, 5, -5, 4, 3])
+@pytest.mark.parametrize("sigma", [0.4, 0.5478, 0.61, 0.7943282, 1.1])
+def test_qms_thresholds_equal_oracle(host_check, q, sigma):
+    """The channel's level-sampler tables (host::awgn_qms_levels: erfc in float64, the 64-bit
+    CDF threshold of each rounding boundary) equal the oracle's restatement bit for bit — what
+    the GPU sampler compares its Philox words against (tests/test_gpu_channel.py checks the
+    levels it draws)."""
+    from oracle.philox_oracle import qms_levels
+    r = _run(host_check, "qms", repr(sigma), str(q))
+    assert r.returncode == 0, r.stderr[-2000:]
+    t = json.loads(r.stdout)
+    T, vals, kmin = qms_levels(sigma, q)
+    assert t["nb"] == len(T) and t["kmin"] == kmin
+    assert [int(x) for x in t["thr"]] == [int(x) for x in T]
+    np.testing.assert_array_equal(np.float32(t["val"]), vals)
