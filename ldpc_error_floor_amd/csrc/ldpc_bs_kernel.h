@@ -638,10 +638,6 @@ __device__ __forceinline__ void pack_channel_q8(const uint32_t* __restrict__ q8,
 #ifndef BS_HDLDS
 #define BS_HDLDS 1
 #endif
-// a variable lane keeps every C->V when KEEP reaches its degree bound (A/B; 0: one re-read)
-#ifndef BS_KEEP_ALL
-#define BS_KEEP_ALL 0
-#endif
 #ifndef BS_KEEP_MC
 #define BS_KEEP_MC 7
 #endif
@@ -974,7 +970,7 @@ k_bs(BsArgs a) {
             // (at most DV - 1: 802.11n, DV = 4, keeps three and reads its fourth edge again,
             // 14.48 -> 14.41 ms same box (r3zh); wman and 5G BG2 keep BS_KEEP = 4 of 6 / 8)
             constexpr int KEEP0 = ((VPL > 1 || CPL > 1) && !UCN) ? BS_KEEP_MC : BS_KEEP;
-            constexpr int KEEP = KEEP0 < DV ? KEEP0 : (BS_KEEP_ALL ? DV : DV - 1);
+            constexpr int KEEP = KEEP0 < DV ? KEEP0 : DV - 1;
             uint32_t mn[KEEP > 0 ? KEEP : 1], mb[KEEP > 0 ? KEEP : 1][4];
             uint32_t S[SB];
 #pragma unroll
