@@ -1,4 +1,4 @@
-# round-end evidence, part A (the committed build): pytest -m gpu, smoke, per-config kernel
+# round-end evidence, part A (the committed build; replaces round_evidence.sh): pytest -m gpu, smoke, per-config kernel
 # trace + PMC passes (tools/evidence.sh -> traffic JSON for bench.py), the default bench line
 # with the CPU baseline and its rocprofv3 kernel-trace summary -> gpurun_out/ev_$TAG
 set -o pipefail
