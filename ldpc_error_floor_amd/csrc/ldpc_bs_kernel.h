@@ -320,16 +320,10 @@ __device__ __forceinline__ void lut_bit(uint32_t (&o)[NI], const uint32_t (&in)[
 // global -> LDS without registers (global_load_lds_dword: lane l of the wave whose first word is
 // w0 writes word w0 + l).  Nothing waits for the loads here: the next __syncthreads (vmcnt(0))
 // retires them, before any wave reads the table.
-template <bool OPQ = false>
 __device__ __forceinline__ void copy_async(uint32_t lds, const uint32_t* src, int n, int wave, int NT) {
-    // (wave-uniform loop; the lane index from mbcnt, so no thread index is kept live for it;
-    // OPQ: of an opaque mask, so [w < n] is not hoisted out of the caller's T loop as a lane
-    // mask that the loop spills — the one-chunk builds: C2 spill-free, 3 -> 0 VGPRs)
-    uint32_t all = ~0u;
-    if (OPQ) asm volatile("" : "+s"(all));
-    const int ln = (int)__builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
+    // (wave-uniform loop; the lane index from mbcnt, so no thread index is kept live for it)
     for (int w0 = wave * 64; w0 < n; w0 += NT) {
-        const int w = w0 + ln;
+        const int w = w0 + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         if (w < n)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + w),
                                              (__attribute__((address_space(3))) void*)(uintptr_t)(lds + 4u * (uint32_t)w0),
@@ -1199,9 +1193,9 @@ k_bs(BsArgs a) {
                     asm volatile("" : "+v"(tl));
                     cw = __builtin_amdgcn_readfirstlane(tl >> 6);
                 }
-                copy_async<CPL == 1>(a.off_alut + 4u * (uint32_t)(nx * AL), a.alut + (size_t)(t + 1) * AL, AL, cw, NT);
+                copy_async(a.off_alut + 4u * (uint32_t)(nx * AL), a.alut + (size_t)(t + 1) * AL, AL, cw, NT);
                 if (a.bcols > 1)
-                    copy_async<CPL == 1>(a.off_blut + 4u * (uint32_t)(nx * BL), a.blut + (size_t)(t + 1) * BL, BL, cw, NT);
+                    copy_async(a.off_blut + 4u * (uint32_t)(nx * BL), a.blut + (size_t)(t + 1) * BL, BL, cw, NT);
                 if (!XP && BS_BFIX && BS_BTID_LDS && a.btid)   // this iteration's variable phase: ids of row t + 1
                     copy_async(a.off_btid, reinterpret_cast<const uint32_t*>(a.btid) + (size_t)(t + 1) * a.btid_n,
                                a.bcols == 1 ? 1 : a.btid_n, cw, NT);
