@@ -425,18 +425,26 @@ __device__ __forceinline__ void alpha_fixed(uint32_t (&p)[4], uint32_t (&q)[4], 
 #ifndef BS_AFIX
 #define BS_AFIX 0
 #endif
+// DPP moves with bound_ctrl (A/B switch; see qperm)
+#ifndef BS_DPP_BC
+#define BS_DPP_BC true
+#endif
 
-// lane permutation inside each group of 4 lanes (DPP quad_perm, a VALU move)
+// lane permutation inside each group of 4 lanes (DPP quad_perm, a VALU move).  bound_ctrl on:
+// every lane of a quad_perm / row mirror has a source lane, so the "old" operand is dead — with
+// it off the compiler materialised the old value 0 in the destination first (one v_mov_b32 0
+// per DPP move: 26 of the ~200 VALU of a C2 check lane), and with it on a DPP move whose
+// consumer is a VOP2 op folds into it (v_xor_b32_dpp)
 template <int CTRL>
 __device__ __forceinline__ uint32_t qperm(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, BS_DPP_BC);
 }
 constexpr int QP_X1 = 0xB1;          // [1, 0, 3, 2]
 constexpr int QP_X2 = 0x4E;          // [2, 3, 0, 1]
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, BS_DPP_BC);
 }
 // OR / sum over the wave (wave-uniform result): butterflies inside each row of 16 lanes by DPP
 // (quad_perm, row_half_mirror, row_mirror), then the four row results by readlane

@@ -87,6 +87,20 @@ __global__ void __launch_bounds__(256) k_mix(uint32_t* out, uint32_t seed, unsig
                 asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[j]) : "v"(b[j]));
             } else if (MIX == 26) {    // v_and_b32 with an inline constant
                 asm volatile("v_and_b32 %0, 0x7fff, %0" : "+v"(a[j]));
+            } else if (MIX == 28) {    // DPP move, quad_perm, bound_ctrl (the lane-group merges)
+                asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 29) {    // VOP2 xor with a DPP quad_perm source (a folded DPP move)
+                asm volatile("v_xor_b32_dpp %0, %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(a[j]) : "v"(b[j]));
+            } else if (MIX == 30) {    // v_mov_b32 of an inline constant (VOP1)
+                asm volatile("v_mov_b32 %0, 0" : "=v"(a[j]));
+            } else if (MIX == 31) {    // 1 DPP move + 3 v_bitop3 (the merge mix)
+                asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(c[j]) : "v"(b[j]));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(b[j]) : "v"(a[j]), "v"(c[j]));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+            } else if (MIX == 32) {    // a v_bitop3 and a dependent VOP2 xor
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
+                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(b[j]) : "v"(a[j]));
             } else if (MIX == 27) {    // ds_read_b128 broadcast (all lanes, same LDS address) + 2 bitop3
                 // (LDS traffic in the VALU loop: the table-leaf alternative)
                 asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x6c" : "+v"(a[j]) : "v"(b[j]), "v"(c[j]));
@@ -133,7 +147,7 @@ int main() {
     printf("%s  CUs %d  clock %.3f GHz (device max; the measured rate uses it)\n", p.name, ncu, clk);
     uint32_t* d;
     hipMalloc(&d, (size_t)ncu * 8 * 256 * 4 * 4);
-    for (int w : {2, 6}) {
+    for (int w : {2, 6, 8}) {
         run<0>("v_add_u32", 1, w, ncu, clk, d);
         run<1>("v_med3_u32", 1, w, ncu, clk, d);
         run<2>("v_sub_u32_sdwa", 1, w, ncu, clk, d);
@@ -161,6 +175,11 @@ int main() {
         run<24>("v_mov_b32 from sgpr", 1, w, ncu, clk, d);
         run<25>("v_xor_b32 vv", 1, w, ncu, clk, d);
         run<26>("v_and_b32 inline const", 1, w, ncu, clk, d);
+        run<28>("v_mov_b32_dpp quad_perm", 1, w, ncu, clk, d);
+        run<29>("v_xor_b32_dpp quad_perm", 1, w, ncu, clk, d);
+        run<30>("v_mov_b32 0", 1, w, ncu, clk, d);
+        run<31>("dpp mov + 3 bitop3", 4, w, ncu, clk, d);
+        run<32>("bitop3 + v_xor (dependent)", 2, w, ncu, clk, d);
     }
     hipFree(d);
     return 0;
