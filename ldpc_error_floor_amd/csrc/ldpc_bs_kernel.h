@@ -506,6 +506,25 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
 #else
 #define ABL(bit) 0
 #endif
+// Phase markers for the ISA attribution (tools/isa_phase_table.py), analysis builds only
+// (-DBS_MARK: an assembler comment ";@ph NAME.K" at each phase start; the product build has none)
+// PH4 / PH8 / PH9 tie the marker to the values the phase starts from ("+v"), so the phase's first
+// instructions cannot be scheduled above it
+#ifdef BS_MARK
+#define PH(name, k) asm volatile(";@ph " name ".%0" ::"i"(k))
+#define PH4(name, k, x) asm volatile(";@ph " name ".%4" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]) : "i"(k))
+#define PH8(name, k, x, y)                                                                        \
+    asm volatile(";@ph " name ".%8" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(y[0]),  \
+                 "+v"(y[1]), "+v"(y[2]), "+v"(y[3]) : "i"(k))
+#define PH9(name, k, x, y, z)                                                                     \
+    asm volatile(";@ph " name ".%9" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(y[0]),  \
+                 "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(z) : "i"(k))
+#else
+#define PH(name, k) ((void)0)
+#define PH4(name, k, x) ((void)0)
+#define PH8(name, k, x, y) ((void)0)
+#define PH9(name, k, x, y, z) ((void)0)
+#endif
 // C->V messages of a variable lane's first BS_KEEP edges kept in registers from the sum pass to
 // the V->C pass (the others are read from their slots again).  Measured per instance, same box,
 // 2 rounds (tools/bs_variant.sh -DBS_KEEP=k): C2 5.79 (0) / 5.70 (1) / 5.58 (2) / 5.56 (3) /
@@ -900,6 +919,7 @@ k_bs(BsArgs a) {
             // a (wave, u) place without a variable chunk (dw = -1, wave-uniform): nothing to do
             // (5G BG2: 20 chunks on 32 places; their beta table and Tv work used to run anyway)
             if (BS_VSKIP && VPL > 1 && dw[u] < 0) continue;
+            PH("vn_setup", (last ? 100 : 0) + u);
 #pragma unroll
             for (int p = 0; p < VNA; ++p) asm volatile("" : "+v"(va[u][p]));   // unpacked per use
             auto vaddr = [&](int f) __attribute__((always_inline)) -> uint32_t {
@@ -933,12 +953,15 @@ k_bs(BsArgs a) {
                                         : a.btid[(size_t)tb * a.btid_n + col]);
                 }
             }
+            PH("vn_beta", (last ? 100 : 0) + u);
             if (!last) {
                 // identity table: |Q(beta ch)| = |ch| (the mask covers iterations 0..63)
                 if (ABL(2) || (tb < 64 && ((a.beta_id >> tb) & 1))) {
+                    PH("vn_beta_id", u);
 #pragma unroll
                     for (int i = 0; i < 4; ++i) lw[0][i] = cmu[i];
                 } else if (bk >= 0 && bk < kNBetaTab) {   // a table of the fixed set
+                    PH("vn_beta_fix", u);
                     beta_asm(lw[0], cmu, bk);
                     if constexpr (BIG) {            // shortened bits: |Q(beta cu)| from the table words
                         if (a.bcols == 1) {
@@ -954,6 +977,7 @@ k_bs(BsArgs a) {
                         }
                     }
                 } else if (a.bcols == 1) {          // one beta per iteration: table in SGPRs
+                    PH("vn_beta_sg", u);
                     const ConstW* tg = (const ConstW*)(a.blut) + (size_t)tb * BLUT_W;
                     lut_s(lw[0], cmu, tg);
                     if constexpr (BIG) {
@@ -961,6 +985,7 @@ k_bs(BsArgs a) {
                         for (int i = 0; i < 4; ++i) lw[0][i] = mux(bg[u], tg[LUT_W + i], lw[0][i]);
                     }
                 } else {
+                    PH("vn_beta_lds", u);
                     const uint32_t btab = bslice + tab_b[u];
                     const uint32_t cmi[1][4] = {{cmu[0], cmu[1], cmu[2], cmu[3]}};
                     lut<1>(lw, cmi, btab);
@@ -988,6 +1013,7 @@ k_bs(BsArgs a) {
 #pragma unroll
                 for (int f = 0; f < DV; ++f) {
                     if (f < dwu) {
+                        PH("vn_sum", (last ? 100 : 0) + f);
                         uint32_t M[4], n, b[4];
                         read_slot(n, M, vaddr(f));
 #pragma unroll
@@ -1001,6 +1027,7 @@ k_bs(BsArgs a) {
                         }
                     }
                 }
+                if constexpr (SB == 8) PH8("vn_app", (last ? 100 : 0) + u, S, (S + 4));
                 // APP_t = Q(ch) + S: the sign (hard decision) from the carry chain alone, the full
                 // sum only in the last iteration (APP > 0 for the loss counter)
                 uint32_t hd, nz = 0u;
@@ -1035,6 +1062,7 @@ k_bs(BsArgs a) {
                 }
             }
             if (last) continue;
+            if constexpr (SB == 8) PH8("vn_tv", (last ? 100 : 0) + u, S, (S + 4));
             // Tv = clamp(Q(beta ch) + S): the table gives |Q(beta ch)|, the channel the sign
             uint32_t lb[4];
 #pragma unroll
@@ -1058,6 +1086,7 @@ k_bs(BsArgs a) {
                 for (int f = 0; f < DV; ++f) {
                     if (f < dwu) {
                         if (ABL(4)) continue;
+                        PH("vn_vc", (last ? 100 : 0) + f);
                         uint32_t x[7], X[4], n, b[4];
                         if (f < KEEP) {
                             n = mn[f < KEEP ? f : 0];
@@ -1077,6 +1106,7 @@ k_bs(BsArgs a) {
             }
         }
         if (!first) {
+            PH("vn_flags", last ? 100 : 0);
             if (!ABL(8)) wr = wave_or(wr);
             if (last) {
                 apos = wave_or(apos);
@@ -1170,6 +1200,7 @@ k_bs(BsArgs a) {
     __syncthreads();
 
     for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
+        PH("top", 0);
         if ((BS_TIDFREE ? wave == 0 : tid == 0) && t > 0) {   // fold iteration t-1's frame flags
             // (every lane of wave 0 writes the same words: a wave-uniform branch, no thread
             // index kept live through the loop; kept in LDS for the iter_wrong export after the
@@ -1233,6 +1264,7 @@ k_bs(BsArgs a) {
             const bool active = (CPL == 1) ? (BS_TIDFREE ? wave * 64 < a.cn_lanes : tid < a.cn_lanes)
                                            : (gchunk[c] >= 0);   // (cn_lanes: 64 k)
             if (!active || ABL(1)) continue;
+            PH("ck_addr", c);
             uint32_t cbase;
             if constexpr (GBL) {
                 // (the lane index from an operand the loop cannot hoist: a hoisted address was
@@ -1265,6 +1297,7 @@ k_bs(BsArgs a) {
             // (the lane's EPL slots are read once, all loads issued before any use, and kept
             // in registers for pass 2)
             uint32_t Xs[EPL][4], ns[EPL];
+            PH("ck_read", c);
 #pragma unroll
             for (int m = 0; m < EPL; ++m) {
                 if (SKIPM && m >= gmc) {             // padding for the whole chunk
@@ -1278,6 +1311,7 @@ k_bs(BsArgs a) {
             // UCN: syndrome of the previous hard decisions over the check (padding edges read a
             // zero word): odd -> the check is unsatisfied, its messages weighted by alpha'
             uint32_t syn = 0u;
+            PH("ck_syn", c);
             const bool ucn_t = ucn_on(t);
             if constexpr (UCN) {
                 if (ucn_t) {
@@ -1309,6 +1343,7 @@ k_bs(BsArgs a) {
                     if (LPC == 4) syn ^= qperm<QP_X2>(syn);
                 }
             }
+            PH4("ck_min", c, Xs[EPL - 1]);
             uint32_t m1[4] = {Xs[0][0], Xs[0][1], Xs[0][2], Xs[0][3]}, m2[4] = {~0u, ~0u, ~0u, ~0u};
             uint32_t par = ns[0];
             if constexpr (!SKIPM && EPL >= 2) {
@@ -1347,6 +1382,7 @@ k_bs(BsArgs a) {
                 par ^= ns[m];
             }
             }
+            PH9("ck_merge", c, m1, m2, par);
             par ^= qperm<QP_X1>(par);
             merge_lanes<QP_X1>(m1, m2);
             if (LPC == 4) {
@@ -1358,6 +1394,7 @@ k_bs(BsArgs a) {
             // LPC EPL slots (an even count, padding included)
             // weighted, quantized minima: each lane evaluates OB output bits, the group shares them
             uint32_t q1[4], q2[4];
+            PH9("ck_tab", c, m1, m2, par);
             {
                 const uint32_t mm[2][4] = {{m1[0], m1[1], m1[2], m1[3]}, {m2[0], m2[1], m2[2], m2[3]}};
                 const uint32_t tab = ctab + (uint32_t)((t & 1) * AL * 4);
@@ -1427,7 +1464,9 @@ k_bs(BsArgs a) {
             // (if it is not the only one, the two minima are equal), the others the minimum
 #pragma unroll
             for (int m = 0; m < EPL; ++m) {
+                if (m == 0) PH8("ck_pass2", 0, q1, q2);
                 if (real(m)) {
+                    if (m > 0) PH("ck_pass2", m);
                     const uint32_t addr = cbase + m * cstride;
                     uint32_t X[4], n;
                     if constexpr (RR) {
