@@ -490,6 +490,91 @@ __device__ __forceinline__ void sort2(uint32_t (&lo)[4], uint32_t (&hi)[4], cons
         hi[i] = mux(l, A[i], B[i]);
     }
 }
+// AND over the LPC lanes of a check's group (the DPP folds into v_and_b32_dpp)
+template <int LPC>
+__device__ __forceinline__ uint32_t grp_and(uint32_t a) {
+    a &= qperm<QP_X1>(a);
+    if (LPC == 4) a &= qperm<QP_X2>(a);
+    return a;
+}
+// The check's two minima by a bit-serial search over the whole lane group, most significant
+// plane first: plane i of the minimum is the AND over the edges still tied with it on the planes
+// above (cand), taken across the group by DPP; cand ends as [|V->C| = m1], the edges that get the
+// second minimum in pass 2.  The second minimum is the same search over the other edges, or m1
+// where two or more edges tie at it.  (Against the pair tournament and the two lane-group merges:
+// C2, 4 edges per lane, 98 VALU with 22 DPP per lane against 117 with 18, and pass 2 no longer
+// compares each edge with m1.)  Padding slots (all ones) are magnitude 15: with degree >= 2 they
+// change neither minimum.
+template <int EPL, int LPC>
+__device__ __forceinline__ void min2_bits(uint32_t (&m1)[4], uint32_t (&m2)[4], uint32_t (&cand)[EPL],
+                                          const uint32_t (&X)[EPL][4]) {
+    constexpr unsigned T_ANDORN = (TA & (TB | ~TC)) & 0xFF;      // a & (b | ~c)
+    constexpr unsigned T_ANDOR = (TA & (TB | TC)) & 0xFF;        // a & (b | c)
+    constexpr unsigned T_ANDEQ = (TA & ~(TB ^ TC)) & 0xFF;       // a & (b == c)
+    constexpr unsigned T_NANDEQ = (~TA & ~(TB ^ TC)) & 0xFF;     // ~a & (b == c)
+    constexpr unsigned T_ORAND = (TA | (TB & TC)) & 0xFF;        // a | (b & c)
+    // m1, most significant plane first
+    uint32_t a = X[0][3];
+#pragma unroll
+    for (int m = 1; m < EPL; ++m) a &= X[m][3];
+    a = grp_and<LPC>(a);
+    m1[3] = a;
+#pragma unroll
+    for (int m = 0; m < EPL; ++m) cand[m] = ~(X[m][3] ^ a);
+#pragma unroll
+    for (int i = 2; i >= 0; --i) {
+        a = X[0][i] | ~cand[0];
+#pragma unroll
+        for (int m = 1; m < EPL; ++m) a = B3(T_ANDORN, a, X[m][i], cand[m]);
+        a = grp_and<LPC>(a);
+        m1[i] = a;
+#pragma unroll
+        for (int m = 0; m < EPL; ++m) cand[m] = B3(T_ANDEQ, cand[m], X[m][i], a);
+    }
+    // two or more edges of the group at the minimum
+    uint32_t one = cand[0], two = 0u;
+#pragma unroll
+    for (int m = 1; m < EPL; ++m) {
+        two = B3(T_ORAND, two, one, cand[m]);
+        one |= cand[m];
+    }
+    {
+        const uint32_t op = qperm<QP_X1>(one);
+        two = qperm<QP_X1>(two) | B3(T_ORAND, two, one, op);
+        one |= op;
+    }
+    if (LPC == 4) {
+        const uint32_t op = qperm<QP_X2>(one);
+        two = qperm<QP_X2>(two) | B3(T_ORAND, two, one, op);
+    }
+    // the minimum of the other edges (c2: not at m1, tied with the search so far)
+    uint32_t c2[EPL];
+    a = X[0][3] | cand[0];
+#pragma unroll
+    for (int m = 1; m < EPL; ++m) a = B3(T_ANDOR, a, X[m][3], cand[m]);
+    a = grp_and<LPC>(a);
+    m2[3] = a;
+#pragma unroll
+    for (int m = 0; m < EPL; ++m) c2[m] = B3(T_NANDEQ, cand[m], X[m][3], a);
+#pragma unroll
+    for (int i = 2; i >= 0; --i) {
+        a = X[0][i] | ~c2[0];
+#pragma unroll
+        for (int m = 1; m < EPL; ++m) a = B3(T_ANDORN, a, X[m][i], c2[m]);
+        a = grp_and<LPC>(a);
+        m2[i] = a;
+        if (i > 0) {
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) c2[m] = B3(T_ANDEQ, c2[m], X[m][i], a);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m2[i] = mux(two, m1[i], m2[i]);
+}
+#ifndef BS_BSMIN
+#define BS_BSMIN 1      // the bit-serial two minima (A/B switch; the one-chunk bsl instances)
+#endif
+
 template <int CTRL>
 __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]) {
     uint32_t b1[4], b2[4];
@@ -1346,7 +1431,14 @@ k_bs(BsArgs a) {
             PH4("ck_min", c, Xs[EPL - 1]);
             uint32_t m1[4] = {Xs[0][0], Xs[0][1], Xs[0][2], Xs[0][3]}, m2[4] = {~0u, ~0u, ~0u, ~0u};
             uint32_t par = ns[0];
-            if constexpr (!SKIPM && EPL >= 2) {
+            // (BSM: the bit-serial search; cand[m] = [|V->C| of slot m = m1] for pass 2)
+            constexpr bool BSM = BS_BSMIN && !SKIPM && !RR;
+            uint32_t cand[BSM ? EPL : 1];
+            if constexpr (BSM) {
+#pragma unroll
+                for (int m = 1; m < EPL; ++m) par ^= ns[m];
+                min2_bits<EPL, LPC>(m1, m2, cand, Xs);
+            } else if constexpr (!SKIPM && EPL >= 2) {
                 // tournament: sort pairs (12 ops), merge sorted pairs (24) — 48 ops for four
                 // edges against 56 for the running two-minima update (only the two values matter)
                 sort2(m1, m2, Xs[0], Xs[1]);
@@ -1384,10 +1476,10 @@ k_bs(BsArgs a) {
             }
             PH9("ck_merge", c, m1, m2, par);
             par ^= qperm<QP_X1>(par);
-            merge_lanes<QP_X1>(m1, m2);
+            if (!BSM) merge_lanes<QP_X1>(m1, m2);
             if (LPC == 4) {
                 par ^= qperm<QP_X2>(par);
-                merge_lanes<QP_X2>(m1, m2);
+                if (!BSM) merge_lanes<QP_X2>(m1, m2);
             }
             // message k is negative iff an even number of the OTHER edges have V->C >= 0
             // (Main_Functions.py:251-254): par ^ n_k, par the parity of [V->C >= 0] over the
@@ -1468,6 +1560,12 @@ k_bs(BsArgs a) {
                 if (real(m)) {
                     if (m > 0) PH("ck_pass2", m);
                     const uint32_t addr = cbase + m * cstride;
+                    uint32_t Mg[4];
+                    if constexpr (BSM) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) Mg[i] = mux(cand[m], q2[i], q1[i]);
+                        write_slot(addr, par ^ ns[m], Mg);
+                    } else {
                     uint32_t X[4], n;
                     if constexpr (RR) {
                         read_slot(n, X, addr);       // (the slot still holds this edge's V->C)
@@ -1476,13 +1574,13 @@ k_bs(BsArgs a) {
 #pragma unroll
                         for (int i = 0; i < 4; ++i) X[i] = Xs[m][i];
                     }
-                    uint32_t Mg[4];
                     uint32_t ne = X[0] ^ m1[0];
 #pragma unroll
                     for (int i = 1; i < 4; ++i) ne = B3(T_ORXOR, ne, X[i], m1[i]);
 #pragma unroll
                     for (int i = 0; i < 4; ++i) Mg[i] = mux(ne, q1[i], q2[i]);
                     write_slot(addr, par ^ n, Mg);
+                    }
                 }
             }
         }
