@@ -223,8 +223,9 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
         p.off_ch = (uint32_t)o;
         o += (size_t)16 * k.VPL * 64 * p.nw;
     } else if (BS_GBLDS && k.CPL == 1) {           // the check lanes' slot-base words
-        p.off_ch = (uint32_t)o;
-        o += (size_t)4 * 64 * p.nw;
+        p.off_ch = (uint32_t)o;                    // (BS_ALDS: + their slot addresses, 2 per word)
+        const int EPL = (k.D + k.LPC - 1) / k.LPC;
+        o += (size_t)4 * (BS_ALDS && k.PK ? ((1 + (EPL + 1) / 2) | 1) : 1) * 64 * p.nw;
     }
     if (BS_HDLDS && k.UCN && k.CPL == 1) {         // the check lanes' hard-decision addresses
         const int EPL = (k.D + k.LPC - 1) / k.LPC, HDW = (EPL + 1) / 2;

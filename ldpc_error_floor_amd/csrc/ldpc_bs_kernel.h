@@ -490,11 +490,17 @@ __device__ __forceinline__ void sort2(uint32_t (&lo)[4], uint32_t (&hi)[4], cons
         hi[i] = mux(l, A[i], B[i]);
     }
 }
-// AND over the LPC lanes of a check's group (the DPP folds into v_and_b32_dpp)
+// AND over the LPC lanes of a check's group: one v_and_b32_dpp per step.  (Each step's result
+// goes through an empty asm, so the two ANDs are not reassociated into one v_bitop3 AND3 — which
+// left both DPP moves unfolded: 2 DPP moves + 2 VALU per step pair instead of 2 DPP ANDs.)
 template <int LPC>
 __device__ __forceinline__ uint32_t grp_and(uint32_t a) {
     a &= qperm<QP_X1>(a);
-    if (LPC == 4) a &= qperm<QP_X2>(a);
+    asm("" : "+v"(a));
+    if (LPC == 4) {
+        a &= qperm<QP_X2>(a);
+        asm("" : "+v"(a));
+    }
     return a;
 }
 // The check's two minima by a bit-serial search over the whole lane group, most significant
@@ -625,6 +631,15 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
 // loop (which the 64- and 80-VGPR builds spilled: a scratch reload + vmcnt(0) per iteration)
 #ifndef BS_GBLDS
 #define BS_GBLDS 1
+#endif
+// with it, the check lane's EPL slot addresses themselves (16 bits each, the PAD slot in place of
+// a padding edge), two per LDS word after the slot-base word: the check phase reads them instead
+// of computing base + m stride and selecting PAD by lane masks (VALU with SGPR operands, ~4
+// cycles each) (A/B switch, off: 0.05 fewer VALU per pack-edge-iteration on C2, but the words
+// push C2's LDS over a third of the CU (two workgroups per CU: 4.81 against 4.69 ms) and C3's
+// over a half (20.2 against 13.5 ms), r5c)
+#ifndef BS_ALDS
+#define BS_ALDS 0
 #endif
 // The channel planes of one variable for the 32 codewords of a pack: sign cs, magnitude planes
 // cm[0..3] of Q(ch) in grid units, shortened-bit flags bg (BIG); returns 1 when a row is off the
@@ -1276,7 +1291,26 @@ k_bs(BsArgs a) {
     const uint32_t cstride = (uint32_t)(a.z * SLOT_B);
     const uint32_t tabu = (uint32_t)(a.arows * LUT_W * 4);        // alpha' tables after the alpha ones
     constexpr bool GBL = BS_GBLDS && CPL == 1 && !BS_CH_LDS;
-    if constexpr (GBL) lds_put(a.off_ch + 4u * (uint32_t)tid, gbase[0]);
+    constexpr bool ALDS = GBL && PK && BS_ALDS;
+    constexpr int HWA = (EPL + 1) / 2;                            // (ALDS) address words per check lane
+    // words per lane (ALDS: [lane][GW], an odd count, so a 32-lane group's reads of one word hit
+    // 32 distinct banks; all of a lane's words read with immediate offsets from one address)
+    constexpr int GW = ALDS ? ((1 + HWA) | 1) : 1;
+    if constexpr (GBL) lds_put(a.off_ch + 4u * (uint32_t)(tid * GW), gbase[0]);
+    if constexpr (ALDS) {
+        const uint32_t b = gbase[0] & 0xFFFFu;
+#pragma unroll
+        for (int p = 0; p < HWA; ++p) {
+            uint32_t w = 0u;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int m = 2 * p + h;
+                const bool re = m < EPL && (LPC * m + LPC - 1 < cn_dmin || LPC * m + cj < gdeg[0]);
+                w |= (re ? b + (uint32_t)m * (uint32_t)(a.z * SLOT_B) : a.off_pad) << (16 * h);
+            }
+            lds_put(a.off_ch + 4u * (uint32_t)(tid * GW + 1 + p), w);
+        }
+    }
     constexpr bool HDL = BS_HDLDS && UCN && CPL == 1;
     if constexpr (HDL) {
 #pragma unroll
@@ -1351,13 +1385,19 @@ k_bs(BsArgs a) {
             if (!active || ABL(1)) continue;
             PH("ck_addr", c);
             uint32_t cbase;
+            uint32_t aw[ALDS ? HWA : 1];
             if constexpr (GBL) {
                 // (the lane index from an operand the loop cannot hoist: a hoisted address was
                 // itself held through the loop and spilled)
                 uint32_t all = ~0u;
                 asm volatile("" : "+s"(all));
                 const uint32_t ln = __builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
-                cbase = lds_w(a.off_ch + ((uint32_t)wave << 8) + 4u * ln);
+                const uint32_t la = a.off_ch + ((uint32_t)wave << 8) * GW + 4u * GW * ln;
+                cbase = lds_w(la);
+                if constexpr (ALDS) {
+#pragma unroll
+                    for (int p = 0; p < HWA; ++p) aw[p] = lds_w(la + 4u * (uint32_t)(1 + p));
+                }
             } else {
                 cbase = gbase[c];
                 asm volatile("" : "+v"(cbase));
@@ -1375,7 +1415,14 @@ k_bs(BsArgs a) {
                 else return LPC * m + LPC - 1 < cn_dmin || LPC * m + cj < cdeg;
             };
             auto caddr = [&](int m) __attribute__((always_inline)) -> uint32_t {
-                return real(m) ? cbase + m * cstride : a.off_pad;
+                if constexpr (ALDS) return (m & 1) ? (aw[m >> 1] >> 16) : (aw[m >> 1] & 0xFFFFu);
+                else return real(m) ? cbase + m * cstride : a.off_pad;
+            };
+            // (ALDS) pass 2's test: real for the whole wave while LPC m + LPC - 1 < cn_dmin, else
+            // the lane's address is not the PAD slot's
+            auto real2 = [&](int m) __attribute__((always_inline)) -> bool {
+                if constexpr (ALDS) return LPC * m + LPC - 1 < cn_dmin || caddr(m) != a.off_pad;
+                else return real(m);
             };
             // pass 1: two minima of |V->C| and the parity of [V->C >= 0] over the lane's edges
             // (padding edges: negative, magnitude 15), then merged across the lane group
@@ -1557,9 +1604,9 @@ k_bs(BsArgs a) {
 #pragma unroll
             for (int m = 0; m < EPL; ++m) {
                 if (m == 0) PH8("ck_pass2", 0, q1, q2);
-                if (real(m)) {
+                if (real2(m)) {
                     if (m > 0) PH("ck_pass2", m);
-                    const uint32_t addr = cbase + m * cstride;
+                    const uint32_t addr = ALDS ? caddr(m) : cbase + m * cstride;
                     uint32_t Mg[4];
                     if constexpr (BSM) {
 #pragma unroll
