@@ -43,14 +43,16 @@ for step in "$@"; do
         python -c "import json;d=json.load(open('$OUT/bench_$c.json'));print('$c', d['value'], d['ms_per_step'], d['config']['kernel'], 'e2e', d['e2e_with_rng']['codewords_per_s'])"
       done ;;
     ab)
-      # variants: default | path/to/lib.so | env=NAME=VALUE (the default build with NAME set)
+      # variants: default | path/to/lib.so | env=NAME=VALUE (the default build with NAME set) |
+      # default@NAME=VALUE | path/to/lib.so@NAME=VALUE
       for r in $(seq 1 ${a3:-2}); do
         for v in ${a2//,/ }; do
           envset=""
+          if [ "${v#*@}" != "$v" ]; then envset=${v#*@}; v=${v%%@*}; fi   # LIB@NAME=VALUE
           if [ "$v" = default ]; then restore
           elif [ "${v#env=}" != "$v" ]; then restore; envset=${v#env=}
           else cp $v $L || exit 1; fi
-          echo -n "$a1 $v: "
+          echo -n "$a1 $v${envset:+@$envset}: "
           if [ -n "$envset" ]; then ( export "$envset"; bench_ms $a1 ) || { restore; exit 1; }
           else bench_ms $a1 || { restore; exit 1; }; fi
         done
