@@ -511,9 +511,12 @@ __device__ __forceinline__ uint32_t grp_and(uint32_t a) {
 // C2, 4 edges per lane, 98 VALU with 22 DPP per lane against 117 with 18, and pass 2 no longer
 // compares each edge with m1.)  Padding slots (all ones) are magnitude 15: with degree >= 2 they
 // change neither minimum.
-template <int EPL, int LPC>
+// (the first K of the EPL slots: the multi-chunk instances skip the positions that are padding
+// for the whole chunk, K = gm by a switch)
+template <int K, int LPC, int EPL>
 __device__ __forceinline__ void min2_bits(uint32_t (&m1)[4], uint32_t (&m2)[4], uint32_t (&cand)[EPL],
                                           const uint32_t (&X)[EPL][4]) {
+    static_assert(K >= 1 && K <= EPL, "active slots");
     constexpr unsigned T_ANDORN = (TA & (TB | ~TC)) & 0xFF;      // a & (b | ~c)
     constexpr unsigned T_ANDOR = (TA & (TB | TC)) & 0xFF;        // a & (b | c)
     constexpr unsigned T_ANDEQ = (TA & ~(TB ^ TC)) & 0xFF;       // a & (b == c)
@@ -522,25 +525,25 @@ __device__ __forceinline__ void min2_bits(uint32_t (&m1)[4], uint32_t (&m2)[4], 
     // m1, most significant plane first
     uint32_t a = X[0][3];
 #pragma unroll
-    for (int m = 1; m < EPL; ++m) a &= X[m][3];
+    for (int m = 1; m < K; ++m) a &= X[m][3];
     a = grp_and<LPC>(a);
     m1[3] = a;
 #pragma unroll
-    for (int m = 0; m < EPL; ++m) cand[m] = ~(X[m][3] ^ a);
+    for (int m = 0; m < K; ++m) cand[m] = ~(X[m][3] ^ a);
 #pragma unroll
     for (int i = 2; i >= 0; --i) {
         a = X[0][i] | ~cand[0];
 #pragma unroll
-        for (int m = 1; m < EPL; ++m) a = B3(T_ANDORN, a, X[m][i], cand[m]);
+        for (int m = 1; m < K; ++m) a = B3(T_ANDORN, a, X[m][i], cand[m]);
         a = grp_and<LPC>(a);
         m1[i] = a;
 #pragma unroll
-        for (int m = 0; m < EPL; ++m) cand[m] = B3(T_ANDEQ, cand[m], X[m][i], a);
+        for (int m = 0; m < K; ++m) cand[m] = B3(T_ANDEQ, cand[m], X[m][i], a);
     }
     // two or more edges of the group at the minimum
     uint32_t one = cand[0], two = 0u;
 #pragma unroll
-    for (int m = 1; m < EPL; ++m) {
+    for (int m = 1; m < K; ++m) {
         two = B3(T_ORAND, two, one, cand[m]);
         one |= cand[m];
     }
@@ -554,31 +557,34 @@ __device__ __forceinline__ void min2_bits(uint32_t (&m1)[4], uint32_t (&m2)[4], 
         two = qperm<QP_X2>(two) | B3(T_ORAND, two, one, op);
     }
     // the minimum of the other edges (c2: not at m1, tied with the search so far)
-    uint32_t c2[EPL];
+    uint32_t c2[K];
     a = X[0][3] | cand[0];
 #pragma unroll
-    for (int m = 1; m < EPL; ++m) a = B3(T_ANDOR, a, X[m][3], cand[m]);
+    for (int m = 1; m < K; ++m) a = B3(T_ANDOR, a, X[m][3], cand[m]);
     a = grp_and<LPC>(a);
     m2[3] = a;
 #pragma unroll
-    for (int m = 0; m < EPL; ++m) c2[m] = B3(T_NANDEQ, cand[m], X[m][3], a);
+    for (int m = 0; m < K; ++m) c2[m] = B3(T_NANDEQ, cand[m], X[m][3], a);
 #pragma unroll
     for (int i = 2; i >= 0; --i) {
         a = X[0][i] | ~c2[0];
 #pragma unroll
-        for (int m = 1; m < EPL; ++m) a = B3(T_ANDORN, a, X[m][i], c2[m]);
+        for (int m = 1; m < K; ++m) a = B3(T_ANDORN, a, X[m][i], c2[m]);
         a = grp_and<LPC>(a);
         m2[i] = a;
         if (i > 0) {
 #pragma unroll
-            for (int m = 0; m < EPL; ++m) c2[m] = B3(T_ANDEQ, c2[m], X[m][i], a);
+            for (int m = 0; m < K; ++m) c2[m] = B3(T_ANDEQ, c2[m], X[m][i], a);
         }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) m2[i] = mux(two, m1[i], m2[i]);
 }
 #ifndef BS_BSMIN
-#define BS_BSMIN 1      // the bit-serial two minima (A/B switch; the one-chunk bsl instances)
+#define BS_BSMIN 1      // the bit-serial two minima (A/B switch)
+#endif
+#ifndef BS_BSMIN_MC
+#define BS_BSMIN_MC 1   // ... on the multi-chunk instances too (A/B switch)
 #endif
 
 template <int CTRL>
@@ -1282,6 +1288,7 @@ k_bs(BsArgs a) {
     constexpr bool RPW = BS_RPW && CPL > 1;
     constexpr int RB = EPL;
     static_assert(CPL * RB <= 32, "real-position word");
+    static_assert(!SKIPM || EPL <= 8, "BS_MIN2_CASE covers 1..8");
     uint32_t rpk = 0u;
 #pragma unroll
     for (int c = 0; c < CPL; ++c)
@@ -1479,12 +1486,25 @@ k_bs(BsArgs a) {
             uint32_t m1[4] = {Xs[0][0], Xs[0][1], Xs[0][2], Xs[0][3]}, m2[4] = {~0u, ~0u, ~0u, ~0u};
             uint32_t par = ns[0];
             // (BSM: the bit-serial search; cand[m] = [|V->C| of slot m = m1] for pass 2)
-            constexpr bool BSM = BS_BSMIN && !SKIPM && !RR;
+            constexpr bool BSM = BS_BSMIN && !RR && (!SKIPM || BS_BSMIN_MC);
             uint32_t cand[BSM ? EPL : 1];
             if constexpr (BSM) {
 #pragma unroll
-                for (int m = 1; m < EPL; ++m) par ^= ns[m];
-                min2_bits<EPL, LPC>(m1, m2, cand, Xs);
+                for (int m = 1; m < EPL; ++m) par ^= ns[m];     // (padding positions: ~0, an even count)
+                if constexpr (SKIPM) {
+                    switch (gmc) {                   // wave-uniform: the chunk's real positions
+#define BS_MIN2_CASE(k)                                                                            \
+    case k:                                                                                        \
+        if constexpr (k <= EPL) min2_bits<k, LPC>(m1, m2, cand, Xs);                               \
+        break;
+                        BS_MIN2_CASE(1) BS_MIN2_CASE(2) BS_MIN2_CASE(3) BS_MIN2_CASE(4) BS_MIN2_CASE(5)
+                        BS_MIN2_CASE(6) BS_MIN2_CASE(7) BS_MIN2_CASE(8)
+#undef BS_MIN2_CASE
+                        default: break;
+                    }
+                } else {
+                    min2_bits<EPL, LPC>(m1, m2, cand, Xs);
+                }
             } else if constexpr (!SKIPM && EPL >= 2) {
                 // tournament: sort pairs (12 ops), merge sorted pairs (24) — 48 ops for four
                 // edges against 56 for the running two-minima update (only the two values matter)

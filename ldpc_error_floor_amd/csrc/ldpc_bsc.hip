@@ -91,6 +91,11 @@ __device__ __forceinline__ void lds_qput(uint32_t addr, const uint32_t (&x)[4]) 
 #ifndef BSC_AFIX
 #define BSC_AFIX 0
 #endif
+// the bit-serial two minima of bsl (min2_bits) in place of the tournament and lane-group merges
+// (A/B switch)
+#ifndef BSC_BSMIN
+#define BSC_BSMIN 1
+#endif
 
 // Check records in blocks of 16: the q1 words of records 16 b .. 16 b + 15 (256 B), then their q2
 // words (256 B), so q2 is q1 + 256 (an instruction offset) and a ds_read_b128 group of 16 lanes
@@ -486,8 +491,26 @@ k_bsc(BscArgs a) {
             // bound hold the all-ones padding, so a pair that straddles it sorts correctly and its
             // padding sign word, XORed by all L lanes of the group, leaves the parity unchanged
             uint32_t m1[4], m2[4];
-            sort2(m1, m2, Xs[0], Xs[1]);
+            uint32_t cand[BSC_BSMIN ? EPL : 1];
             uint32_t par = ns[0] ^ ns[1];
+            if constexpr (BSC_BSMIN) {
+                // the bit-serial search of bsl (min2_bits), over the chunk's real positions
+#pragma unroll
+                for (int m = 2; m < EPL; ++m) par ^= ns[m];
+                switch (gmc) {
+#define BSC_MIN2_CASE(k)                                                                           \
+    case k:                                                                                        \
+        if constexpr (k <= EPL) min2_bits<k, L>(m1, m2, cand, Xs);                                 \
+        break;
+                    BSC_MIN2_CASE(1) BSC_MIN2_CASE(2) BSC_MIN2_CASE(3) BSC_MIN2_CASE(4) BSC_MIN2_CASE(5)
+                    BSC_MIN2_CASE(6) BSC_MIN2_CASE(7) BSC_MIN2_CASE(8) BSC_MIN2_CASE(9) BSC_MIN2_CASE(10)
+#undef BSC_MIN2_CASE
+                    default: break;
+                }
+                par ^= qperm<QP_X1>(par);
+                if (L == 4) par ^= qperm<QP_X2>(par);
+            } else {
+            sort2(m1, m2, Xs[0], Xs[1]);
 #pragma unroll
             for (int m = 2; m + 1 < EPL; m += 2) {
                 if (m >= gmc) continue;
@@ -513,6 +536,7 @@ k_bsc(BscArgs a) {
             if (L == 4) {
                 par ^= qperm<QP_X2>(par);
                 merge_lanes<QP_X2>(m1, m2);
+            }
             }
             // weighted, quantized minima (Main_Functions.py:266-316).  One table of the fixed set
             // for the whole iteration (uniform alpha: C5): all 4 bits of both by immediate truth
@@ -558,12 +582,18 @@ k_bsc(BscArgs a) {
             for (int m = 0; m < EPL; ++m) {
                 if (real(m)) {
                     const uint32_t sa = sbase + m * sstride;
+                    uint32_t eq;
+                    if constexpr (BSC_BSMIN) {
+                        eq = cand[m];
+                    } else {
                     const uint32_t(&X)[4] = Xs[m];
                     uint32_t ne = X[0] ^ m1[0];
 #pragma unroll
                     for (int i = 1; i < 4; ++i) ne = B3(T_ORXOR, ne, X[i], m1[i]);
+                    eq = ~ne;
+                    }
                     lds_put(sa, par ^ ns[m]);
-                    lds_put(sa + a.off_a, ~ne);
+                    lds_put(sa + a.off_a, eq);
                 }
             }
                     };
