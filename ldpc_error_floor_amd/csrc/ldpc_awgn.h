@@ -1,7 +1,7 @@
 // ldpc_awgn.h — the on-GPU AWGN LLR generator shared by ldpc_channel_awgn (ldpc_channel.hip),
-// ldpc_decode_awgn's byte channel for the bit-sliced kernels and the fused v5 decoder's
-// in-prologue channel (ldpc_fused5.hip), so that generating inside the decoder is bit-identical
-// to generating into HBM and decoding.
+// the bit-sliced kernels' in-prologue channel (ldpc_bs_kernel.h gen_bytes) and the fused v5
+// decoder's (ldpc_fused5.hip), so that generating inside the decoder is bit-identical to
+// generating into HBM and decoding.
 //
 // Channel model of create_mix_epoch (Print_Functions.py:29-72) for the all-zero word:
 //   y = sigma * n - 1 (BPSK 0 -> -1),  LLR = 2 y / sigma^2 (log p1/p0);  QMS: Cal_MSA_Q
@@ -77,9 +77,12 @@ struct AwgnParams {
 // host: parameters from the C-ABI arguments, with the QMS level thresholds (ldpc_channel.hip)
 AwgnParams make_awgn(double sigma, uint64_t seed, int64_t offset, int decoding_type, int q_bit,
                      int ps, int pe, int ss, int se, float clip);
-// ldpc_decode_awgn's byte channel for the bit-sliced kernels: q8 = [ceil(B/32)][n_vars][8] words
-// (k_awgn_q8; qmax: the grid's largest magnitude, for the shortened-bit byte)
-int channel_q8(uint32_t* q8, int64_t B, int n_vars, const AwgnParams& a, int qmax, hipStream_t s);
+// the QMS level sampler's lookup tables in one block, built on the host (the same entries as
+// awgn_bucket_fill2): words [0, 2 NB) the bucket entries {base | count << 8, first threshold},
+// then thr_hi[AWGN_NB_MAX], thr_lo[AWGN_NB_MAX] -- the bit-sliced kernels' in-prologue channel
+// copies it into LDS
+constexpr int AWGN_TAB_W = 2 * (1 << 10) + 2 * 32;
+void awgn_gen_table(const AwgnParams& a, uint32_t* out /*[AWGN_TAB_W]*/);
 
 // float modes (SP, MS): LLRs of elements 2*pr and 2*pr+1 of codeword `b` (batch-relative)
 // into l[0], l[1] by Box-Muller (QMS uses the level sampler below)
@@ -112,6 +115,7 @@ __device__ __forceinline__ void awgn_pair(const AwgnParams& a, int64_t b, int pr
 // the low word decides (awgn_tie_scan), drawn only then -- kept out of this loop so that the
 // compiler cannot hoist the second Philox in front of it.
 constexpr int AWGN_KB = 10;                 // bucket bits (1024 buckets, 2 KB of LDS)
+static_assert(AWGN_TAB_W == 2 * (1 << AWGN_KB) + 2 * AWGN_NB_MAX, "awgn_gen_table layout");
 template <typename P16, typename P32>
 __device__ __forceinline__ int awgn_level_hi(P16 bucket, P32 thi, uint32_t u, bool& tie) {
     const uint32_t e = bucket[u >> (32 - AWGN_KB)];
@@ -223,14 +227,19 @@ __device__ __forceinline__ void awgn_bucket_fill2(const AwgnParams& a, uint2* bu
 // the levels of codewords 4 gq .. 4 gq + 3 at variable v from the inline-threshold table: the
 // four bucket reads issued together, the level from the entry alone (U against the bucket's
 // first threshold), and only then the rare scans: buckets holding more thresholds, high-word ties
-template <typename P32>
-__device__ __forceinline__ void awgn_levels4b(const AwgnParams& a, const uint2* bucket, P32 thi, P32 tlo,
+// (A: anything with the key k0, k1 and the boundary count nb: AwgnParams, or the bit-sliced
+// kernels' in-prologue generator; PB / P32: the tables in LDS or global memory)
+template <typename A, typename PB, typename P32>
+__device__ __forceinline__ void awgn_levels4b(const A& a, PB bucket, P32 thi, P32 tlo,
                                               uint32_t v, uint64_t gq, int (&lv)[4]) {
     uint32_t c[4] = {v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_Q};
     Philox::gen(c, a.k0, a.k1);
     uint2 e[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) e[j] = bucket[c[j] >> (32 - AWGN_KB)];
+    for (int j = 0; j < 4; ++j) {
+        const auto ej = bucket[c[j] >> (32 - AWGN_KB)];
+        e[j] = make_uint2(ej.x, ej.y);
+    }
     uint32_t ties = 0u, more = 0u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

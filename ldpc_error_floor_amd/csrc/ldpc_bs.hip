@@ -674,7 +674,8 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
 bool bs_q8_ok(const DevGraph& g, int mode, bool ucn, float clip, int T, bool has_short) {
     const BsPlan p = bs_plan(g, mode, ucn, false, clip, T);
     if (!p.ok) return bsc_q8_ok(g, mode, ucn, clip, T, has_short);
-    return !has_short || p.cu > 0.f;
+    // (the in-prologue channel's tables borrow the slot region)
+    return (!has_short || p.cu > 0.f) && (size_t)(p.off_pad - p.off_slots) >= sizeof(uint32_t) * AWGN_TAB_W;
 }
 
 int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
@@ -698,7 +699,21 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     const int VNW = (k.PK ? (DV + 1) / 2 : DV) + 1;
     const uint32_t* gt = reinterpret_cast<const uint32_t*>(ws.bs_graph);
     BsArgs a{};
-    a.llr = b.q8 ? reinterpret_cast<const float*>(b.q8) : llr;
+    a.llr = llr;
+    if (b.q8) {                          // the in-prologue channel (ldpc_decode_awgn)
+        const AwgnParams& g8 = *reinterpret_cast<const AwgnParams*>(b.gen8);
+        a.gen.tab = b.q8;
+        a.gen.k0 = g8.k0;
+        a.gen.k1 = g8.k1;
+        a.gen.offset = g8.offset;
+        a.gen.nb = g8.nb;
+        a.gen.kmin = g8.kmin;
+        a.gen.ps = g8.ps;
+        a.gen.pe = g8.pe;
+        a.gen.ss = g8.ss;
+        a.gen.se = g8.se;
+        a.gen.lds = p.off_slots;
+    }
     a.B = b.B;
     a.n_vars = g.n_vars;
     a.n_checks = g.n_checks;

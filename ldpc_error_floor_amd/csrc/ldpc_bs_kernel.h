@@ -72,9 +72,22 @@ constexpr BsInst kBsInst[] = {
 };
 constexpr int kBsNInst = sizeof(kBsInst) / sizeof(kBsInst[0]);
 
+// The QMS channel generated in the kernel's prologue (Q8 builds; ldpc_decode_awgn, SURVEY 8 f
+// rank 1): the byte each LLR would have in k_awgn_q8's byte channel, from the same Philox stream
+// and level sampler (ldpc_awgn.h), so the decode is bit-identical to ldpc_channel_awgn +
+// ldpc_decode.  The sampler's tables (awgn_gen_table, 8.25 KB) are copied into LDS at `lds`, a
+// region the kernel writes only after the prologue.
+struct BsGen {
+    const uint32_t* tab;         // [AWGN_TAB_W] (awgn_gen_table)
+    uint32_t k0, k1;             // Philox key (the seed)
+    int64_t offset;              // global index of the batch's first codeword
+    int nb, kmin;                // level count - 1, grid index of level 0
+    int ps, pe, ss, se;          // 1-based puncture / shorten ranges (0: none)
+    uint32_t lds;                // LDS byte address of the tables
+};
+
 struct BsArgs {
-    const float* llr;            // (Q8 builds: the channel as bytes [packs][n_vars][8] words,
-                                 // pack_channel_q8; the field keeps the kernarg layout of the others)
+    const float* llr;            // (Q8 builds: unused, the channel is generated: gen)
     int64_t B;
     int n_vars, n_checks, T, target_bits, cn_lanes, cn_dmin;
     float inv;
@@ -119,6 +132,7 @@ struct BsArgs {
     uint32_t off_hdl;            // BS_HDLDS (one-chunk UCN instances): the check lanes' packed
                                  // hard-decision addresses, [HDW][lane] words
     uint32_t pad_;
+    BsGen gen;                   // Q8 builds: the in-prologue channel
 };
 
 // ---- bit-plane arithmetic ---------------------------------------------------------------------
@@ -716,15 +730,51 @@ __device__ __forceinline__ int pack_channel(const float (&xv)[PACK], float inv, 
     pack_bytes<BIG>(D, valid, cs, cm, bg);
     return off;
 }
-// the channel already as those bytes (ldpc_decode_awgn's byte channel, k_awgn_q8): q8 =
-// [packs][n_vars][8] words; always on the grid
-template <bool BIG>
-__device__ __forceinline__ void pack_channel_q8(const uint32_t* __restrict__ q8, int64_t pk, int nv, int v,
-                                                uint32_t valid, uint32_t& cs, uint32_t (&cm)[4], uint32_t& bg) {
-    const uint4* src = reinterpret_cast<const uint4*>(q8 + ((size_t)pk * nv + v) * 8);
-    const uint4 x0 = src[0], x1 = src[1];
-    const uint32_t D[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-    pack_bytes<BIG>(D, valid, cs, cm, bg);
+// The bytes of variable v for the 32 codewords of pack pk, generated (Q8 builds): byte r of
+// D[r / 4] = level + 16 + kmin of codeword offset + 32 pk + r (a shortened bit: 48 - qmax, a
+// punctured one: 16), exactly k_awgn_q8's words.  Four codewords per Philox call; a batch offset
+// off the quads takes two quads per word and a byte funnel shift (wave-uniform).
+typedef unsigned int v2u_g __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const v2u_g LdsU2;
+__device__ __forceinline__ void gen_bytes(const BsGen& g, int64_t pk, int v, int qmax, uint32_t (&D)[8]) {
+    const int bit = v + 1;
+    if (g.ss > 0 && bit >= g.ss && bit <= g.se) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) D[i] = (uint32_t)(48 - qmax) * 0x01010101u;
+        return;
+    }
+    if (g.ps > 0 && bit >= g.ps && bit <= g.pe) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) D[i] = 0x10101010u;
+        return;
+    }
+    LdsU2* bucket = reinterpret_cast<LdsU2*>((uintptr_t)g.lds);
+    const LdsW* thi = reinterpret_cast<const LdsW*>((uintptr_t)(g.lds + 8u * (1u << AWGN_KB)));
+    const LdsW* tlo = thi + AWGN_NB_MAX;
+    const uint64_t g0 = (uint64_t)g.offset + (uint64_t)pk * 32u;
+    const int sh = (int)(g.offset & 3);
+    const uint32_t boff = (uint32_t)(16 + g.kmin);
+    auto word = [&](const int (&l)[4]) __attribute__((always_inline)) -> uint32_t {
+        return ((uint32_t)l[0] + boff) | ((uint32_t)l[1] + boff) << 8 | ((uint32_t)l[2] + boff) << 16 |
+               ((uint32_t)l[3] + boff) << 24;
+    };
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t gq = (g0 + 4u * (uint32_t)i) >> 2;
+        int la[4];
+        awgn_levels4b(g, bucket, thi, tlo, (uint32_t)v, gq, la);
+        uint32_t w = word(la);
+        if (sh) {
+            int lb[4];
+            awgn_levels4b(g, bucket, thi, tlo, (uint32_t)v, gq + 1, lb);
+            w = __builtin_amdgcn_alignbyte(word(lb), w, (uint32_t)sh);
+        }
+        D[i] = w;
+    }
+}
+// the generator's tables into LDS (every thread of the workgroup; the caller's barrier follows)
+__device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
+    for (int w = tid; w < AWGN_TAB_W; w += NT) lds_put(g.lds + 4u * (uint32_t)w, g.tab[w]);
 }
 #ifndef BS_PACKT
 #define BS_PACKT 1      // pack_channel (A/B switch; 0: per-row bit insertion)
@@ -820,8 +870,8 @@ __device__ __forceinline__ void pack_channel_q8(const uint32_t* __restrict__ q8,
 // synd_bits outputs); the counters-only build is the one the bench and the sweeps run.
 // LB: the workgroup size bound (64 NW for the multi-chunk instances: the register budget is
 // 512 / (waves per SIMD), which a 1024-lane bound would fix at 128)
-// Q8: the channel as bytes (in a.llr: ldpc_decode_awgn's byte channel) instead of float LLRs; a
-// build of its own (a run-time branch moved the register allocation of the whole kernel: C3's
+// Q8: the channel generated in the prologue (a.gen: ldpc_decode_awgn) instead of read as float
+// LLRs; a build of its own (a run-time branch moved the register allocation of the whole kernel: C3's
 // spills 5 -> 9 VGPRs)
 template <int D, int DV, int LPC, int VPL, int CPL, bool UCN, bool BIG, bool PK, int WPE, bool XP, int LB, bool Q8>
 __global__ void __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE)))
@@ -895,6 +945,7 @@ k_bs(BsArgs a) {
         for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(8);
     }
     if (tid == 0) RED[7] = 0u;
+    if constexpr (Q8) gen_tables(a.gen, tid, NT);
     __syncthreads();
     uint32_t cs[VPL], cm[VPL][4], bg[VPL];
     int off = 0;
@@ -922,8 +973,8 @@ k_bs(BsArgs a) {
     // one round trip without holding every variable's 32 values at once
     float xv[VPL][PACK];
     if constexpr (Q8) {
-        // byte channel (ldpc_decode_awgn): two 16-byte loads per variable, no conversion, never
-        // off the grid
+        // generated channel (ldpc_decode_awgn): the grid bytes of the lane's variables from the
+        // Philox stream, packed into planes as pack_channel's; never off the grid
 #pragma unroll
         for (int u = 0; u < VPL; ++u) {
             cs[u] = 0u;
@@ -931,9 +982,11 @@ k_bs(BsArgs a) {
 #pragma unroll
             for (int p = 0; p < 4; ++p) cm[u][p] = 0u;
             const int v = var_of(u);
-            if (v >= 0 && !ABL(32))
-                pack_channel_q8<BIG>(reinterpret_cast<const uint32_t*>(a.llr), blockIdx.x, nv, v, valid, cs[u],
-                                     cm[u], bg[u]);
+            if (v >= 0 && !ABL(32)) {
+                uint32_t Dq[8];
+                gen_bytes(a.gen, blockIdx.x, v, a.qmax, Dq);
+                pack_bytes<BIG>(Dq, valid, cs[u], cm[u], bg[u]);
+            }
         }
     } else {
     if (var_of(0) >= 0 && !ABL(32)) {
@@ -1701,7 +1754,7 @@ int launch_bs_x(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s)
 }
 template <int I>
 int launch_bs(const BsArgs& a, int nblocks, int nw, size_t lds, hipStream_t s, bool q8) {
-    // (the byte channel comes from ldpc_decode_awgn, which exports no hard bits)
+    // (the generated channel comes from ldpc_decode_awgn, which exports no hard bits)
     if (a.hdx) return q8 ? LDPC_ERR_UNSUPPORTED : launch_bs_x<I, true, false>(a, nblocks, nw, lds, s);
     return q8 ? launch_bs_x<I, false, true>(a, nblocks, nw, lds, s) : launch_bs_x<I, false, false>(a, nblocks, nw, lds, s);
 }

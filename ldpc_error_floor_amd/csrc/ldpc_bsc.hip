@@ -46,7 +46,7 @@ constexpr BscInst kBscInst[] = {
 };
 
 struct BscArgs {
-    const float* llr;            // (Q8 builds: the byte channel, as bsl's)
+    const float* llr;            // (Q8 builds: unused, the channel is generated, as bsl's)
     int64_t B;
     int n_vars, n_checks, T, target_bits, cn_dmin, z;
     float inv, cu;
@@ -73,6 +73,7 @@ struct BscArgs {
     uint32_t* hdx;               // XP builds: [T][packs][n_vars] hard decisions (as bsl's)
     uint32_t off_a, off_rec, off_tv, off_red, off_alut, off_blut;   // SGN at LDS byte 0
                                  // (RED: 16 words, then T words: iteration t's frame-error word)
+    BsGen gen;                   // Q8 builds: the in-prologue channel (bsl's; tables at SGN)
 };
 
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
@@ -167,6 +168,7 @@ k_bsc(BscArgs a) {
         for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(8);
     }
     if (tid == 0) RED[7] = 0u;
+    if constexpr (Q8) gen_tables(a.gen, tid, NT);
     __syncthreads();
     uint32_t cs[VPL], cm[VPL][4], bg[VPL];
     int off = 0;
@@ -177,9 +179,10 @@ k_bsc(BscArgs a) {
 #pragma unroll
         for (int p = 0; p < 4; ++p) cm[u][p] = 0u;
         const int v = vv[u] < 0 ? -1 : (vv[u] & 0xFFFF);
-        if (Q8 && v >= 0) {                        // byte channel (ldpc_decode_awgn), a build of its own
-            pack_channel_q8<true>(reinterpret_cast<const uint32_t*>(a.llr), blockIdx.x, nv, v, valid, cs[u],
-                                  cm[u], bg[u]);
+        if (Q8 && v >= 0) {                        // generated channel (ldpc_decode_awgn), a build of its own
+            uint32_t Dq[8];
+            gen_bytes(a.gen, blockIdx.x, v, a.qmax, Dq);
+            pack_bytes<true>(Dq, valid, cs[u], cm[u], bg[u]);
         } else if (v >= 0) {
             // (buffer loads: a wave-uniform descriptor over the pack's rows, the lane's 4 v in
             // voffset, the row's 4 r nv in soffset: no 64-bit VGPR address per load, as bsl)
@@ -914,7 +917,7 @@ static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStre
     static const bool b1_on = [] { const char* e = getenv("LDPC_BSC_B1"); return !(e && atoi(e) == 0); }();
     const bool b1 = b1_on && a.beta_id && a.bcols == 1;
     if constexpr (XP) {
-        // (the byte channel comes from ldpc_decode_awgn, which exports no hard bits)
+        // (the generated channel comes from ldpc_decode_awgn, which exports no hard bits)
         if (q8) return LDPC_ERR_UNSUPPORTED;
     } else {
         if (q8) return b1 ? bsc_launch1<I, false, true, true>(a, nblocks, nw, lds, s)
@@ -930,7 +933,8 @@ using namespace bs;
 
 bool bsc_q8_ok(const DevGraph& g, int mode, bool ucn, float clip, int T, bool has_short) {
     const BscPlan p = bsc_plan(g, mode, ucn, false, clip, T);
-    return p.ok && (!has_short || p.cu > 0.f);
+    // (the in-prologue channel's tables borrow the SGN region at LDS byte 0)
+    return p.ok && (!has_short || p.cu > 0.f) && (size_t)p.off_a >= sizeof(uint32_t) * AWGN_TAB_W;
 }
 
 bool bsc_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T) {
@@ -963,7 +967,22 @@ int bsc_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float
     const int VNW = k.DVH + 1;
     BscArgs a{};
     const bool q8 = b.q8 != nullptr;
-    a.llr = q8 ? reinterpret_cast<const float*>(b.q8) : llr;
+    a.llr = llr;
+    if (b.q8) {                          // the in-prologue channel (ldpc_decode_awgn)
+        const AwgnParams& g8 = *reinterpret_cast<const AwgnParams*>(b.gen8);
+        a.gen.tab = b.q8;
+        a.gen.k0 = g8.k0;
+        a.gen.k1 = g8.k1;
+        a.gen.offset = g8.offset;
+        a.gen.nb = g8.nb;
+        a.gen.kmin = g8.kmin;
+        a.gen.ps = g8.ps;
+        a.gen.pe = g8.pe;
+        a.gen.ss = g8.ss;
+        a.gen.se = g8.se;
+        a.gen.lds = 0u;
+    }
+
     a.B = b.B;
     a.n_vars = g.n_vars;
     a.n_checks = g.n_checks;

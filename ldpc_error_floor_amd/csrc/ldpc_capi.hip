@@ -45,9 +45,11 @@ struct ldpc_ctx {
     // LLR buffer for ldpc_decode_awgn when the kernel cannot generate in its prologue
     float* llr_scratch = nullptr;
     int64_t llr_scratch_n = 0;
-    // byte channel for the bit-sliced kernels ([packs][n_vars][32] u8, k_awgn_q8)
-    uint32_t* q8_scratch = nullptr;
-    int64_t q8_scratch_n = 0;
+    // the bit-sliced kernels' in-prologue channel: the level sampler's tables (awgn_gen_table),
+    // on the device and the host copy last uploaded
+    uint32_t* gen_tab = nullptr;
+    uint32_t gen_host[AWGN_TAB_W] = {};
+    bool gen_valid = false;
     char last_kernel[64] = {0};   // ldpc_ctx_last_kernel
 };
 
@@ -389,14 +391,14 @@ int ldpc_ctx_destroy(ldpc_ctx* c) {
     dev_free(c->wrong); dev_free(c->anypos); dev_free(c->biterr);
     fused_free(c->fused);
     if (c->llr_scratch) (void)hipFree(c->llr_scratch);
-    if (c->q8_scratch) (void)hipFree(c->q8_scratch);
+    if (c->gen_tab) (void)hipFree(c->gen_tab);
     delete c;
     return LDPC_OK;
 }
 
 static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
                        const ldpc_decode_outputs* o, void* stream, const AwgnParams* gen,
-                       const uint32_t* q8 = nullptr);
+                       const uint32_t* q8 = nullptr, const AwgnParams* gen8 = nullptr);
 
 // LDPC_KERNEL_AUTO takes the fused kernel when it serves the request, except for sum-product:
 // its check update is bound by the tanh / atanh / divide VALU work, which flood's four codewords
@@ -420,33 +422,36 @@ int ldpc_decode_awgn(ldpc_ctx* c, int64_t B, const ldpc_decode_params* p,
     int st = decode_impl(c, nullptr, B, p, o, stream, &a);
     if (st != LDPC_ERR_UNSUPPORTED) return st;
     ldpc_graph* g = c->g;
-    // counters-only QMS decodes the bit-sliced kernels serve: the byte channel (k_awgn_q8, one
-    // byte per LLR in the layout the kernels' prologue packs into planes) instead of float LLRs
+    // counters-only QMS decodes the bit-sliced kernels serve: the channel generated in their
+    // prologue (SURVEY 8 f rank 1) -- the LLRs never touch HBM (oracle/philox_oracle.awgn_q8); the
+    // sampler's tables (8.25 KB) are uploaded when the channel parameters change
     const int mode = mode_of(p->decoding_type, p->q_bit);
     static const bool q8_on = [] { const char* e = getenv("LDPC_AWGN_Q8"); return !(e && atoi(e) == 0); }();
     if (q8_on && p->decoding_type == LDPC_DEC_QMS && (!o || !o->app_all) && p->kernel != LDPC_KERNEL_FLOOD &&
         fused_q8_ok(g->dev, mode, p->T, p->clip_llr, g->d_alpha_ucn != nullptr, g->per_edge_w != 0,
                     ch->short_start > 0)) {
-        const int64_t nb = (B + 31) / 32 * 32 * (int64_t)g->h.N * g->h.z;       // bytes
-        if (c->q8_scratch_n < nb) {
-            DeviceGuard dg(g->device);
-            if (c->q8_scratch) (void)hipFree(c->q8_scratch);
-            c->q8_scratch = nullptr;
-            c->q8_scratch_n = 0;
-            if (hipMalloc(reinterpret_cast<void**>(&c->q8_scratch), (size_t)nb) != hipSuccess) {
+        DeviceGuard dg(g->device);
+        if (!c->gen_tab) {
+            if (hipMalloc(reinterpret_cast<void**>(&c->gen_tab), sizeof(c->gen_host)) != hipSuccess) {
                 (void)hipGetLastError();
                 return LDPC_ERR_OOM;
             }
-            c->q8_scratch_n = nb;
+            c->gen_valid = false;
         }
-        {
-            DeviceGuard dg(g->device);
-            st = channel_q8(c->q8_scratch, B, g->h.N * g->h.z, a,
-                            mode == MODE_Q4 ? 7 : mode == MODE_Q3 ? 3 : 15,
-                            reinterpret_cast<hipStream_t>(stream));
+        uint32_t tab[AWGN_TAB_W];
+        awgn_gen_table(a, tab);
+        if (!c->gen_valid || std::memcmp(tab, c->gen_host, sizeof(tab)) != 0) {
+            std::memcpy(c->gen_host, tab, sizeof(tab));
+            // (stream-ordered behind any decode still reading the previous tables; the wait
+            // keeps the host copy stable until the transfer has read it)
+            c->gen_valid = false;
+            if (hipMemcpyAsync(c->gen_tab, c->gen_host, sizeof(tab), hipMemcpyHostToDevice,
+                               reinterpret_cast<hipStream_t>(stream)) != hipSuccess ||
+                hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+                return LDPC_ERR_HIP;
+            c->gen_valid = true;
         }
-        if (st != LDPC_OK) return st;
-        st = decode_impl(c, nullptr, B, p, o, stream, nullptr, c->q8_scratch);
+        st = decode_impl(c, nullptr, B, p, o, stream, nullptr, c->gen_tab, &a);
         if (st != LDPC_ERR_UNSUPPORTED) return st;
     }
     // this kernel reads its LLRs: generate them into the context's buffer, then decode
@@ -514,7 +519,7 @@ int ldpc_kernel_info(const ldpc_ctx* c, const ldpc_decode_params* p, int64_t* by
 
 static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_params* p,
                        const ldpc_decode_outputs* o, void* stream, const AwgnParams* gen,
-                       const uint32_t* q8) {
+                       const uint32_t* q8, const AwgnParams* gen8) {
     if (!c || !p || (!llr_dev && !gen && !q8)) return LDPC_ERR_ARG;
     ldpc_graph* g = c->g;
     if (!g->d_alpha || !g->d_beta) return LDPC_ERR_STATE;
@@ -573,6 +578,7 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     b.awgn = gen;
     b.iter_wrong = out.iter_wrong;
     b.q8 = q8;
+    b.gen8 = gen8;
     if (out.iter_wrong &&
         hipMemsetAsync(out.iter_wrong, 0, (size_t)p->T * ((B + 31) / 32) * sizeof(uint32_t), s) != hipSuccess)
         return LDPC_ERR_HIP;

@@ -88,57 +88,24 @@ __global__ void __launch_bounds__(256) k_awgn_qf(float* __restrict__ out, int64_
     }
 }
 
-// QMS bytes for the bit-sliced decoders (ldpc_decode_awgn): [packs][n_vars][32] u8, byte r of
-// (pack, v) = grid value + 16 of codeword 32 pack + r (+ 32 on a shortened bit: the BIG
-// instances' marker, pack_channel) — the bytes pack_channel builds from float LLRs, 576 B per
-// wman codeword instead of 2,304.  One thread per 4-byte word (4 codewords of one variable), word
-// index fastest: a wave stores 8 variables x 32 bytes, contiguous.  Rows past B are generated
-// too (the decoder masks them).  The grid stride is a multiple of 8 words: a thread keeps its
-// word index and steps (pack, variable) by the stride's fixed quotient and remainder.
-__global__ void __launch_bounds__(256) k_awgn_q8(uint32_t* __restrict__ out, int64_t npk, int n_vars,
-                                                 AwgnParams a, int qmax) {
-    __shared__ uint2 bucket[1 << AWGN_KB];
-    __shared__ uint32_t thi[AWGN_NB_MAX], tlo[AWGN_NB_MAX];
-    awgn_bucket_fill2(a, bucket, thi, tlo, threadIdx.x, blockDim.x);
-    __syncthreads();
-    const uint64_t g0 = (uint64_t)a.offset;
-    const int sh = (int)(g0 & 3);                            // the batch's first quad offset
-    const uint32_t boff = (uint32_t)(16 + a.kmin);           // byte of level 0
-    const int64_t id0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int i = (int)(id0 & 7);
-    const int64_t pv0 = id0 >> 3, dpv = ((int64_t)gridDim.x * blockDim.x) >> 3;
-    int64_t pk = pv0 / n_vars;
-    int v = (int)(pv0 - pk * n_vars);
-    const int64_t dpk = dpv / n_vars;
-    const int dv = (int)(dpv - dpk * n_vars);
-    for (; pk < npk; pk += dpk) {
-        const int fx = awgn_fixed(a, v + 1);
-        uint32_t w;
-        if (fx == 1) {
-            w = 0x10101010u;
-        } else if (fx == 2) {
-            w = (uint32_t)(48 - qmax) * 0x01010101u;
-        } else {
-            const uint64_t gb = g0 + (uint64_t)(pk * 32 + 4 * i);
-            int la[4];
-            awgn_levels4b(a, bucket, thi, tlo, (uint32_t)v, gb >> 2, la);
-            w = ((uint32_t)la[0] + boff) | ((uint32_t)la[1] + boff) << 8 | ((uint32_t)la[2] + boff) << 16 |
-                ((uint32_t)la[3] + boff) << 24;
-            if (sh) {               // (wave-uniform) a batch offset off the quads: rows from two quads
-                int lb[4];
-                awgn_levels4b(a, bucket, thi, tlo, (uint32_t)v, (gb >> 2) + 1, lb);
-                const uint32_t wb = ((uint32_t)lb[0] + boff) | ((uint32_t)lb[1] + boff) << 8 |
-                                    ((uint32_t)lb[2] + boff) << 16 | ((uint32_t)lb[3] + boff) << 24;
-                // rows k = 0..3 are words sh + k of the quad pair (la, lb): one byte funnel shift
-                w = __builtin_amdgcn_alignbyte(wb, w, (uint32_t)sh);
+void awgn_gen_table(const AwgnParams& a, uint32_t* out) {
+    constexpr int NB = 1 << AWGN_KB;
+    for (int b = 0; b < NB; ++b) {
+        uint32_t base = 0u, cnt = 0u, first = 0u;
+        for (int i = 0; i < a.nb; ++i) {
+            const uint32_t tb = a.thr_hi[i] >> (32 - AWGN_KB);
+            if (tb < (uint32_t)b) ++base;
+            if (tb == (uint32_t)b) {
+                if (cnt == 0u) first = a.thr_hi[i];
+                ++cnt;
             }
         }
-        out[(pk * n_vars + v) * 8 + i] = w;
-        v += dv;
-        if (v >= n_vars) {
-            v -= n_vars;
-            ++pk;
-        }
+        out[2 * b] = base | cnt << 8;
+        out[2 * b + 1] = first;
+    }
+    for (int i = 0; i < AWGN_NB_MAX; ++i) {
+        out[2 * NB + i] = i < a.nb ? a.thr_hi[i] : 0u;
+        out[2 * NB + AWGN_NB_MAX + i] = i < a.nb ? a.thr_lo[i] : 0u;
     }
 }
 
@@ -196,16 +163,3 @@ extern "C" int ldpc_channel_awgn(float* llr_dev, int64_t B, int32_t n_vars, doub
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 
-namespace ldpc {
-
-// ldpc_decode_awgn's byte channel: q8 [ceil(B/32)][n_vars][8] words (k_awgn_q8)
-int channel_q8(uint32_t* q8, int64_t B, int n_vars, const AwgnParams& a, int qmax, hipStream_t s) {
-    if (a.decoding_type != LDPC_DEC_QMS || a.nb <= 0) return LDPC_ERR_ARG;
-    const int64_t npk = (B + 31) / 32;
-    const int64_t total = npk * n_vars * 8;
-    const unsigned grid = (unsigned)std::min<int64_t>(8192, (total + 255) / 256);
-    hipLaunchKernelGGL(k_awgn_q8, dim3(grid), dim3(256), 0, s, q8, npk, n_vars, a, qmax);
-    return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
-}
-
-}  // namespace ldpc

@@ -59,8 +59,9 @@ const char* bs_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_
 // word (t, pack, v) = codeword 32 pack + r; the export build of the kernel)
 int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float* llr, int mode,
               bool ucn, int64_t* counters, uint8_t* flags, uint32_t* bad, uint32_t* hdx, hipStream_t s);
-// the byte channel (Bufs::q8) serves this counters-only decode: the bit-sliced kernel applies and,
-// with shortened bits in the channel, has the shortened-bit marker (a BIG instance)
+// the in-prologue channel (Bufs::q8 / gen8) serves this counters-only decode: the bit-sliced
+// kernel applies, has room for the sampler's tables in its slot region and, with shortened bits
+// in the channel, has the shortened-bit marker (a BIG instance)
 bool bs_q8_ok(const DevGraph& g, int mode, bool ucn, float clip, int T, bool has_short);
 bool bsc_q8_ok(const DevGraph& g, int mode, bool ucn, float clip, int T, bool has_short);
 // (fused_decode with it: the bit-sliced kernel or LDPC_ERR_UNSUPPORTED)

@@ -87,7 +87,7 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
     // counters / frame flags / bit exports without APP: the bit-sliced kernel when it applies
     // (its export build stores every iteration's hard decisions, bit-sliced, in ws.hdx)
     const bool bs = !b.app_out && !b.awgn && use_bs(g, mode, b.T, ucn, per_edge_w != 0, b.clip);
-    if (b.q8 && !bs) return LDPC_ERR_UNSUPPORTED;          // the byte channel is the bit-sliced kernels'
+    if (b.q8 && !bs) return LDPC_ERR_UNSUPPORTED;          // the in-prologue channel is the bit-sliced kernels'
 
     ws.bits_packed = false;
     if (want_bits) {
@@ -143,7 +143,7 @@ int fused_decode(const DevGraph& g, Bufs& b, FusedWorkspace& ws, const float* ll
         if (st != LDPC_OK) return st;
         ws.last_kernel = fused_kernel_name(g, mode, b.T, b.clip, ucn, per_edge_w != 0);
         ws.bits_packed = want_bits;
-        if (b.q8) return LDPC_OK;      // byte channel: every pack is on the grid, nothing to fix up
+        if (b.q8) return LDPC_OK;      // generated channel: every pack is on the grid, nothing to fix up
         // test hook: LDPC_BS_FIXUP=0 skips the v5 fixup, so a test can tell that a batch was
         // decoded by the bit-sliced kernel alone (flagged packs then contribute nothing).  Read
         // per decode (a test sets it after other decodes ran in the same process).

@@ -60,8 +60,9 @@ struct Bufs {
                                // prologue instead of reading them (fused v5 only), or null
     uint32_t* iter_wrong;      // [T][ceil(B/32)] per-iteration frame-error words, or null
                                // (ldpc_decode_outputs::iter_wrong; zeroed before the decode)
-    const uint32_t* q8;        // the channel as bytes [packs][n_vars][8] words (k_awgn_q8) for the
-                               // bit-sliced kernels, instead of float LLRs, or null
+    const uint32_t* q8;        // the bit-sliced kernels' in-prologue channel: its sampler tables
+                               // (awgn_gen_table, device), with gen8, instead of LLRs; or null
+    const void* gen8;          // AwgnParams* of that channel (with q8)
 };
 
 // Sum-product check update pieces (decoding_type 0, Main_Functions.py:238-245) shared by flood

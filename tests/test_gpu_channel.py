@@ -4,7 +4,7 @@ Random123 known-answer vectors and its QMS level probabilities by the channel mo
 (tests/test_philox_oracle.py); this pins the device streams to it: QMS LLRs (the level
 sampler) bit-exact for every q_bit and offset, float LLRs (Box-Muller) within a few ulps,
 puncture / shorten exact, and every in-decoder generation (v5 prologue, the bit-sliced
-kernels' byte channel) equal to decoding the oracle's LLRs."""
+kernels' prologue channel) equal to decoding the oracle's LLRs."""
 import os
 
 import numpy as np
@@ -96,7 +96,7 @@ def test_decode_awgn_equals_decoding_oracle_llrs(cuda_device):
 @pytest.mark.parametrize("config", ["C2", "C3", "C4", "C5"])
 @pytest.mark.parametrize("off", [0, 3])
 def test_byte_channel_equals_float_channel(config, off, cuda_device):
-    """ldpc_decode_awgn's byte channel (k_awgn_q8 into the bit-sliced kernels' Q8 build) gives
+    """ldpc_decode_awgn's channel generated in the bit-sliced kernels' prologue (their Q8 build) gives
     the counters, frame flags and per-iteration frame errors of ldpc_channel_awgn's float LLRs
     decoded by the same kernel, on every SURVEY workload (shortened bits through the BIG
     marker on C4 / C5), ragged batch, aligned and unaligned offsets; LDPC_AWGN_Q8=0 is the
@@ -126,7 +126,8 @@ def test_qms_high_word_tie_bit_exact(cuda_device, off):
     """A uniform whose high word ties the lowest threshold (sigmas from
     test_philox_oracle.tie_sigmas): the device's low-word draw orders it like the oracle's
     64-bit comparison, in ldpc_channel_awgn's level sampler and in the v5 prologue's channel
-    (aligned batches: awgn_levels4, as k_awgn_q8; unaligned: awgn_qms_elem)."""
+    (aligned batches: awgn_levels4; unaligned: awgn_qms_elem) and in the bit-sliced kernels'
+    prologue (awgn_levels4b, one or two quads per word)."""
     import torch
     from test_philox_oracle import tie_sigmas
     dec = _decoder(cuda_device, "wman_N0576_R34_z24", 24, 2, 5, T=2)
@@ -142,3 +143,10 @@ def test_qms_high_word_tie_bit_exact(cuda_device, off):
         app = dec.decode_awgn(B, s, seed, offset=off, app=True).app.cpu().numpy()
         want = dec.decode(torch.from_numpy(ref).to(cuda_device), app=True).app.cpu().numpy()
         assert np.array_equal(app, want)
+        # the bit-sliced kernel's in-prologue channel (counters-only): the same tie resolution
+        got = dec.decode_awgn(B, s, seed, offset=off, counters=True, flags=True, iter_wrong=True)
+        assert dec.last_kernel().startswith("bsl["), dec.last_kernel()
+        exp = dec.decode(torch.from_numpy(ref).to(cuda_device), app=False, counters=True, flags=True,
+                         iter_wrong=True)
+        for x, y in ((got.flags, exp.flags), (got.counters, exp.counters), (got.iter_wrong, exp.iter_wrong)):
+            assert np.array_equal(x.cpu().numpy(), y.cpu().numpy())
