@@ -68,7 +68,11 @@ typedef struct ldpc_decode_params {
                                    ABI-1 struct (five pointers, no iter_wrong; ABI-1 callers zeroed
                                    this word as reserved), sizeof(ldpc_decode_outputs) = this
                                    header's struct; any other value -> LDPC_ERR_ARG.  The library
-                                   never reads past the size the caller declares. */
+                                   never reads past the size the caller declares.  An ABI-2
+                                   binary (iter_wrong set, this word zeroed as reserved[0]) is
+                                   read as ABI 1 and gets no iter_wrong: ABI-2 callers must be
+                                   rebuilt against this header, and a caller relying on
+                                   iter_wrong checks ldpc_abi_version() >= 3 first. */
     int32_t reserved;
 } ldpc_decode_params;
 

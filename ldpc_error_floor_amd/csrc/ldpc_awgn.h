@@ -21,9 +21,11 @@
 //    Philox(v, b / 4, tag 'LDQ4') — one Philox call serves four codewords of one variable, and
 //    punctured / shortened variables draw nothing — and its low word (word b mod 4 of
 //    Philox(v, b / 4, tag 'LDQR')) is drawn only when the high word equals a threshold's (about
-//    once per 2^27 elements).  This is the reference's distribution exactly (to 2^-64 per
-//    level, against fp32 Box-Muller's ulp-level boundary errors and its ~8.6 sigma tail cut),
-//    with no logarithm, square root or sine: about a third of the Box-Muller VALU per element.
+//    once per 2^27 elements).  This is the reference's distribution to the precision of the
+//    thresholds: float64 erfc (about 2^-53 relative per level) rounded down to a multiple of
+//    2^-64; a level whose upper tail is below 2^-64 gets probability 2^-64 (threshold 2^64 - 1)
+//    -- against fp32 Box-Muller's ulp-level boundary errors and its ~8.6 sigma tail cut -- with
+//    no logarithm, square root or sine: about a third of the Box-Muller VALU per element.
 // It is NOT the numpy RandomState stream: host-generated LLRs remain the seed-parity path.
 #pragma once
 #include <hip/hip_runtime.h>

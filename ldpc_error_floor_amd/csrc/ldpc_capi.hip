@@ -427,7 +427,10 @@ int ldpc_decode_awgn(ldpc_ctx* c, int64_t B, const ldpc_decode_params* p,
     // sampler's tables (8.25 KB) are uploaded when the channel parameters change
     const int mode = mode_of(p->decoding_type, p->q_bit);
     static const bool q8_on = [] { const char* e = getenv("LDPC_AWGN_Q8"); return !(e && atoi(e) == 0); }();
-    if (q8_on && p->decoding_type == LDPC_DEC_QMS && (!o || !o->app_all) && p->kernel != LDPC_KERNEL_FLOOD &&
+    // (counters / flags / iter_wrong only: hard-bit and syndrome exports take the export build,
+    // which reads its LLRs)
+    if (q8_on && p->decoding_type == LDPC_DEC_QMS && (!o || (!o->app_all && !o->hard_bits && !o->synd_bits)) &&
+        p->kernel != LDPC_KERNEL_FLOOD &&
         fused_q8_ok(g->dev, mode, p->T, p->clip_llr, g->d_alpha_ucn != nullptr, g->per_edge_w != 0,
                     ch->short_start > 0)) {
         DeviceGuard dg(g->device);

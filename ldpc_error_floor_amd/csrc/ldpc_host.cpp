@@ -261,6 +261,8 @@ void awgn_qms_levels(double sigma, int q_bit, int* nb, int* kmin, uint32_t* thr_
             T = (uint64_t)std::ldexp(0.5 * std::erfc(-nz * 0.7071067811865476), 64);
         } else {
             const uint64_t tail = (uint64_t)std::ldexp(0.5 * std::erfc(nz * 0.7071067811865476), 64);
+            // (a tail below 2^-64 rounds to 0: the threshold 2^64 - 1 gives that level
+            // probability 2^-64 instead of its < 2^-64; oracle/philox_oracle.py does the same)
             T = tail == 0 ? ~(uint64_t)0 : (uint64_t)0 - tail;
         }
         thr_hi[n] = (uint32_t)(T >> 32);

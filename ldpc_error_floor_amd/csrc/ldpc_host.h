@@ -121,7 +121,7 @@ std::pair<int, int> order_variable_edges(std::vector<uint32_t>& A, const std::ve
 // thresholds T_j = P(LLR < x_j) 2^64 of the channel LLR = 2 (sigma n - 1) / sigma^2, n ~ N(0, 1)
 // (create_mix_epoch, :29-72), from erfc in float64: for n_j = (x_j sigma^2 / 2 + 1) / sigma,
 // T_j = floor(ldexp(erfc(-n_j / sqrt 2) / 2, 64)) when n_j < 0, else 2^64 - floor(ldexp(erfc(n_j /
-// sqrt 2) / 2, 64)) (2^64 - 1 when that tail is 0).  Writes nb (at most 32) boundaries, level
+// sqrt 2) / 2, 64)) (2^64 - 1 when that tail is 0; float64 erfc: about 2^-53 relative).  Writes nb (at most 32) boundaries, level
 // values val[0..nb] and kmin = val[0] / grid step (the bit-sliced kernels' byte offset; 0 for
 // q = 6, whose levels are not on one grid).  oracle/philox_oracle.py restates it.
 void awgn_qms_levels(double sigma, int q_bit, int* nb, int* kmin, uint32_t* thr_hi, uint32_t* thr_lo,

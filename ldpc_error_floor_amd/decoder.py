@@ -185,10 +185,12 @@ class NMSDecoder:
         return res
 
     def generates_channel_in_kernel(self, T=None, kernel=None) -> bool:
-        """Whether ``decode_awgn`` generates the LLRs inside the decoding kernel (the fused v5
-        kernel's prologue); otherwise ``ldpc_decode_awgn`` runs the channel kernel into HBM and
-        then the decoder (the bit-sliced kernels, flood, ffl)."""
-        return self.kernel_info(T, kernel)[1].startswith("fused5")
+        """Whether ``decode_awgn`` generates the LLRs inside the decoding kernel (the prologue of
+        the fused v5 kernel, and of the bit-sliced kernels for QMS counters-only decodes);
+        otherwise ``ldpc_decode_awgn`` runs the channel kernel into HBM and then the decoder
+        (flood, ffl)."""
+        name = self.kernel_info(T, kernel)[1]
+        return name.startswith("fused5") or (self.decoding_type == DECODING_QMS and name.startswith(("bsl[", "bsc[")))
 
     def last_kernel(self) -> str:
         """The kernel that served this decoder's last decode (``ldpc_ctx_last_kernel``)."""

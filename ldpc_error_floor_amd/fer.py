@@ -77,6 +77,10 @@ def shard_range(total: int, rank: int, world: int):
 
 CKPT_VERSION = 2        # 2: key holds point_seeds and the decoder fingerprint; rank 0's file
                         # is <path> at every world size
+# The on-GPU channel's stream (csrc/ldpc_awgn.h, oracle/philox_oracle.py), part of a checkpoint's
+# key: a resume across a change of the generator (round 4 replaced QMS Box-Muller by the exact
+# level sampler) would add counters from another codeword stream.  Bump it with the stream.
+CHANNEL_STREAM = "philox4x32-10/qms-level-v1/box-muller-v1"
 
 
 class SweepCheckpoint:
@@ -154,11 +158,17 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
 
     ``uncor_path``: append the frames wrong at every iteration to this file in the
     ``Uncor.txt`` format (``sampling_type == 2``, ``Print_Functions.py:155-156``), collected on
-    the GPU; with several ranks each rank writes ``<uncor_path>.rank<r>``.
+    the GPU; with several ranks each rank writes ``<uncor_path>.rank<r>``.  The file is
+    appended to, as the reference appends (``Print_Functions.py:122``): a fresh start
+    (``resume=False``) keeps whatever the file already holds, including the rows of an attempt
+    that died before its first checkpoint -- delete it first for a clean run.  A resume
+    truncates it back to the length its checkpoint recorded.
 
-    ``checkpoint``: path of this sweep's checkpoint (``<path>.rank<r>`` with several ranks),
-    written every ``checkpoint_every`` batches and after every SNR point; ``resume=True``
-    continues from it (a missing file starts from the beginning).
+    ``checkpoint``: path of this sweep's checkpoint -- rank 0 writes ``<path>``, rank r > 0
+    ``<path>.rank<r>`` -- written every ``checkpoint_every`` batches and after every SNR point;
+    ``resume=True`` continues from it (a missing file starts from the beginning).  Its key
+    holds the channel stream (``CHANNEL_STREAM``), the decoder and the partition, so a resume
+    with anything else is refused.
 
     ``overlap``: when the decoding kernel reads its LLRs from HBM (the bit-sliced kernels: the
     channel is a kernel of its own), generate batch j + 1 on a second stream while batch j
@@ -196,7 +206,7 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
                "n_codewords": int(n_codewords), "batch": int(batch),
                "T": None if T is None else int(T), "punct": list(punct), "short": list(short),
                "rank": rank, "world": world, "uncor": upath is not None,
-               "decoder": decoder_fingerprint(decoder, T)}
+               "decoder": decoder_fingerprint(decoder, T), "channel": CHANNEL_STREAM}
         err = ""
         try:
             st = ck.load() if resume else None

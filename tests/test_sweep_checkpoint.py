@@ -151,6 +151,23 @@ def test_fresh_start_keeps_earlier_rows_and_resume_drops_its_own(tmp_path):
     assert path.read_text() == prior + ref
 
 
+def test_resume_refuses_another_channel_stream(tmp_path, monkeypatch):
+    """A checkpoint written under another on-GPU channel stream (fer.CHANNEL_STREAM: e.g. a
+    round-3 file from the Box-Muller QMS channel) is refused, not resumed: its counters came
+    from other codewords."""
+    from ldpc_error_floor_amd import fer
+    dec = _make_decoder()
+    ck = str(tmp_path / "c.ckpt")
+    monkeypatch.setattr(fer, "CHANNEL_STREAM", "philox4x32-10/qms-box-muller")
+    with pytest.raises(Stop):
+        fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=1076, checkpoint=ck, checkpoint_every=1,
+                  progress=_interrupt_after(2))
+    monkeypatch.undo()
+    assert json.load(open(ck))["key"]["channel"] == "philox4x32-10/qms-box-muller"
+    with pytest.raises(ValueError, match="checkpoint is for"):
+        fer_sweep(dec, SIGMAS, N_CW, BATCH, seed=1076, checkpoint=ck, resume=True)
+
+
 def test_old_checkpoint_version_refused(tmp_path):
     ck = tmp_path / "old.ckpt"
     ck.write_text(json.dumps({"version": 1, "key": {}, "si": 0, "pos": 0, "counters": []}))
