@@ -6,6 +6,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -505,9 +507,14 @@ int bs_make_tables(const Bufs& b, const DevGraph& g, int arows, int ar, int bcol
 }
 }  // namespace bs
 
-// graph tables, built once per context on the host (ws.bs_graph)
-static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& ws, hipStream_t s) {
-    if (ws.bs_graph) return LDPC_OK;
+// graph tables, built on the host (bs_graph_tables uploads them once per context)
+struct BsHostTables {
+    std::vector<uint32_t> vn;      // [VPL][64 nw][VNW]
+    std::vector<int32_t> wdeg;     // [VPL][nw][3]
+    std::vector<int32_t> cchunk;   // [nw][CPL]
+    std::vector<uint32_t> chd;     // UCN: [cn_lanes][HDW]
+};
+static BsHostTables bs_host_tables(const DevGraph& g, const BsPlan& p) {
     const host::GraphTables& h = *g.host;
     const BsInst& k = kBsInst[p.inst];
     const int nv = g.n_vars, z = h.z;
@@ -647,6 +654,20 @@ static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& w
             }
         }
     }
+    BsHostTables t;
+    t.vn.swap(vn);
+    t.wdeg.swap(wdeg);
+    t.cchunk.swap(cchunk);
+    t.chd.swap(chd);
+    return t;
+}
+static int bs_graph_tables(const DevGraph& g, const BsPlan& p, FusedWorkspace& ws, hipStream_t s) {
+    if (ws.bs_graph) return LDPC_OK;
+    BsHostTables t = bs_host_tables(g, p);
+    const std::vector<uint32_t>& vn = t.vn;
+    const std::vector<int32_t>& wdeg = t.wdeg;
+    const std::vector<int32_t>& cchunk = t.cchunk;
+    const std::vector<uint32_t>& chd = t.chd;
     const size_t nwords = vn.size() + wdeg.size() + p.lay.size() + cchunk.size() + chd.size();
     void* d = nullptr;
     if (hipMalloc(&d, nwords * 4) != hipSuccess) { (void)hipGetLastError(); return LDPC_ERR_OOM; }
@@ -766,3 +787,190 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
 }
 
 }  // namespace ldpc
+
+// ---- host-side bounds check of the bit-sliced kernel's reads (test infrastructure) -----------
+// For a plan and its host tables (the launch's own planning code: plan_inst, bs_host_tables),
+// every index k_bs reads is recomputed on the host -- the kernel's predicates restated from
+// ldpc_bs_kernel.h -- and checked against what the context allocates: the global tables
+// (vn_tab, vn_wdeg, row_ptr, row_lay, cn_chunk, cn_hd, the channel-table ids), the LDS regions
+// (slots, PAD / ZERO, HD, RED, the alpha / beta tables, the per-lane words) and the dynamic LDS
+// size.  The r4c fault (a one-chunk UCN instance read cn_hd for the waves past cn_lanes) is the
+// class it guards: LDPC_BOUNDS_PRE_GUARD drops the `ql < cn_lanes` term of that read, as the
+// kernel had it before the fix, so a test can see the check catch it.
+namespace ldpc {
+namespace bs {
+enum { LDPC_BOUNDS_PRE_GUARD = 1 };
+struct BoundsReport {
+    int violations = 0;
+    std::string first;
+    void fail(const char* what, long long idx, long long lim) {
+        if (violations++ == 0) {
+            char buf[160];
+            snprintf(buf, sizeof(buf), "%s: index %lld outside [0, %lld)", what, idx, lim);
+            first = buf;
+        }
+    }
+    void in(const char* what, long long idx, long long lim) {
+        if (idx < 0 || idx >= lim) fail(what, idx, lim);
+    }
+    // an LDS byte range [a, a + n) inside [lo, hi)
+    void lds(const char* what, long long a, long long n, long long lo, long long hi) {
+        if (a < lo || a + n > hi) fail(what, a, hi);
+    }
+};
+
+static int bs_bounds_check(const DevGraph& g, const BsPlan& p, const BsHostTables& t, int T, int flags,
+                           BoundsReport& r) {
+    const BsInst& k = kBsInst[p.inst];
+    const host::GraphTables& h = *g.host;
+    const int LPC = k.LPC, VPL = k.VPL, CPL = k.CPL, DV = k.DV;
+    const int EPL = (k.D + LPC - 1) / LPC, HDW = (EPL + 1) / 2, OB = 4 / LPC;
+    const int VNA = k.PK ? (DV + 1) / 2 : DV, VNW = VNA + 1;
+    const int NT = 64 * p.nw, nwv = p.nw, nv = g.n_vars, z = h.z;
+    const bool UCN = k.UCN, ucn = UCN && p.ucn;
+    const int AR = UCN ? 2 * p.arows : p.arows;
+    const long long AL = (long long)AR * LUT_W, BL = (long long)p.bcols * BLUT_W;
+    const long long lds = (long long)p.lds;
+    const bool SKIPM = CPL > 1;
+    const bool GBL = BS_GBLDS && CPL == 1 && !BS_CH_LDS;
+    const bool HDL = BS_HDLDS && UCN && CPL == 1;
+    // the allocations
+    r.in("lds size", lds, (long long)BS_LDS_MAX + 1);
+    if ((long long)t.vn.size() != (long long)VPL * NT * VNW) r.fail("vn_tab size", (long long)t.vn.size(), (long long)VPL * NT * VNW);
+    r.lds("RED", p.off_red, 4LL * (16 + T), 0, p.off_alut);
+    r.lds("ALUT", p.off_alut, 4 * 2 * AL, 0, p.off_blut);
+    r.lds("BLUT", p.off_blut, 4 * 2 * BL, 0, lds);
+    r.lds("PAD+ZERO", p.off_pad, 2 * SLOT_B, p.off_slots, p.off_red);
+    if (UCN) r.lds("HD", 0, 4LL * (nv + 1), 0, p.off_slots);
+    // ---- variable phase: per (u, lane)
+    for (int u = 0; u < VPL; ++u)
+        for (int w = 0; w < nwv; ++w) {
+            const long long wi = 3LL * (u * nwv + w);
+            r.in("vn_wdeg", wi + 2, (long long)t.wdeg.size());
+            if (wi + 2 >= (long long)t.wdeg.size()) continue;
+            const int dw = t.wdeg[(size_t)wi], pcol = t.wdeg[(size_t)wi + 2];
+            if (pcol >= 0) r.in("btid column", pcol, h.N);
+            for (int l = 0; l < 64; ++l) {
+                const long long ti = ((long long)u * NT + 64LL * w + l) * VNW;
+                r.in("vn_tab", ti + VNA, (long long)t.vn.size());
+                if (ti + VNA >= (long long)t.vn.size()) continue;
+                const uint32_t* q = &t.vn[(size_t)ti];
+                const int vv = (int)q[VNA];
+                const int v = (UCN && vv >= 0) ? (vv & 0xFFFF) : vv;
+                if (v >= nv) r.fail("variable", v, nv);
+                if (vv >= 0 && UCN) r.in("HD index", (long long)((uint32_t)vv >> 16), nv);
+                if (vv >= 0 && p.bcols > 1) r.in("beta table", v / (nv / p.bcols), p.bcols);
+                for (int f = 0; f < DV && f < dw; ++f) {     // the kernel reads f < dw (wave max)
+                    const uint32_t a = k.PK ? ((f & 1) ? (q[f >> 1] >> 16) : (q[f >> 1] & 0xFFFFu)) : q[f];
+                    if (a != p.off_zero) r.lds("variable slot", a, SLOT_B, p.off_slots, p.off_pad);
+                }
+            }
+        }
+    // ---- check phase: per (wave, chunk, lane)
+    for (int w = 0; w < nwv; ++w)
+        for (int c = 0; c < CPL; ++c) {
+            r.in("cn_chunk", (long long)w * CPL + c, (long long)t.cchunk.size());
+            const int gchunk = CPL == 1 ? w : t.cchunk[(size_t)w * CPL + c];
+            const bool active = CPL == 1 ? w * 64 < p.cn_lanes : gchunk >= 0;
+            int gm = EPL;
+            if (SKIPM) {                                   // the chunk's real positions (wave_or)
+                uint32_t any = 0u;
+                for (int l = 0; l < 64; ++l) {
+                    const int ql = std::max(gchunk, 0) * 64 + l, cc = ql / LPC;
+                    const int ci = std::min(cc / z, g.n_checks / z - 1);
+                    const int gdeg = cc < g.n_checks ? h.row_ptr[ci + 1] - h.row_ptr[ci] : 0;
+                    any |= (1u << ((gdeg + LPC - 1) / LPC)) - 1u;
+                }
+                gm = __builtin_popcount(any);
+            }
+            for (int l = 0; l < 64; ++l) {
+                const int ql = std::max(gchunk, 0) * 64 + l, cc = ql / LPC, cj = l % LPC;
+                const int ci = std::min(cc / z, g.n_checks / z - 1);
+                r.in("row_ptr", ci + 1, h.M + 1);
+                r.in("row_lay", 2LL * ci + 1, (long long)p.lay.size());
+                const int gdeg = cc < g.n_checks ? h.row_ptr[ci + 1] - h.row_ptr[ci] : 0;
+                // the lane's tables (read by every lane of a chunk, active or not)
+                if (UCN) {
+                    const bool guard = (flags & LDPC_BOUNDS_PRE_GUARD) ? true : ql < p.cn_lanes;
+                    if (ucn && gchunk >= 0 && guard)
+                        for (int pp = 0; pp < HDW; ++pp) r.in("cn_hd", (long long)ql * HDW + pp, (long long)t.chd.size());
+                }
+                if (GBL) r.lds("per-lane word", p.off_ch + 4LL * (64 * w + l), 4, p.off_ch, lds);
+                if (HDL)
+                    for (int pp = 0; pp < HDW; ++pp) r.lds("HD addresses", p.off_hdl + 4LL * (pp * NT + 64 * w + l), 4, p.off_hdl, lds);
+                if (!active) continue;
+                const long long gbase = p.off_slots +
+                    ((long long)p.lay[2 * ci] + (long long)cj * p.lay[2 * ci + 1] + (cc - ci * z)) * SLOT_B;
+                for (int m = 0; m < EPL; ++m) {
+                    if (SKIPM && m >= gm) continue;
+                    const bool re = LPC * m + LPC - 1 < p.cn_dmin || LPC * m + cj < gdeg;
+                    const long long a = re ? gbase + (long long)m * z * SLOT_B : p.off_pad;
+                    r.lds("check slot", a, SLOT_B, p.off_slots, p.off_red);
+                    if (re && a + SLOT_B > p.off_pad) r.fail("check slot past the slot region", a, p.off_pad);
+                    if (ucn && cc < g.n_checks && ql < p.cn_lanes && (size_t)ql * HDW + (m >> 1) < t.chd.size()) {
+                        const uint32_t hw = t.chd[(size_t)ql * HDW + (m >> 1)];
+                        const uint32_t ha = (m & 1) ? (hw >> 16) : (hw & 0xFFFFu);
+                        r.lds("HD read", ha, 4, 0, (long long)p.off_hdz + 4);
+                    }
+                }
+                // the alpha tables: lane cj evaluates OB bits of the row's table (and alpha')
+                const long long ctab = p.off_alut + (long long)(p.arows > 1 ? ci : 0) * LUT_W * 4 + (long long)cj * OB * 64;
+                const long long last = ctab + 4LL * AL + (UCN ? (long long)p.arows * LUT_W * 4 : 0) + (OB - 1) * 64 + 3 * 16;
+                r.lds("alpha table", ctab, 16, p.off_alut, p.off_alut + 4 * 2 * AL);
+                r.lds("alpha table (odd t, alpha')", last, 16, p.off_alut, p.off_alut + 4 * 2 * AL);
+            }
+        }
+    // channel-table ids: a.btid[(t + 1) btid_n + col], t + 1 < T, col < N (beta_tid is [T_w][N])
+    return r.violations;
+}
+}  // namespace bs
+}  // namespace ldpc
+
+// One plan per (instance, UCN) that fits a proto graph with the given weight properties, each
+// checked by bs_bounds_check.  Returns the number of plans checked (>= 0) and writes the first
+// violation into msg ("" when none); *violations = the total.  Host only: no device is touched.
+extern "C" int ldpc_debug_bs_bounds(const int32_t* proto, int32_t M, int32_t N, int32_t z, int32_t T,
+                                    int32_t mode, int32_t alpha_uniform, int32_t beta_uniform,
+                                    float clip, int32_t flags, int32_t* violations, char* msg,
+                                    int32_t msg_len) {
+    using namespace ldpc;
+    using namespace ldpc::bs;
+    if (!proto || !violations || T <= 0) return LDPC_ERR_ARG;
+    host::GraphTables h;
+    const int st = host::build_graph(proto, M, N, z, h);
+    if (st != LDPC_OK) return st;
+    DevGraph g{};
+    g.M = h.M; g.N = h.N; g.z = h.z; g.E = h.E;
+    g.n_checks = h.M * h.z; g.n_vars = h.N * h.z; g.n_edges = h.E * h.z; g.max_cdeg = h.max_cdeg;
+    g.h_row_ptr = h.row_ptr.data();
+    g.host = &h;
+    g.w_alpha_uniform = alpha_uniform;
+    g.w_alpha_pair_uniform = alpha_uniform;
+    g.w_beta_uniform = beta_uniform;
+    g.w_beta_nonneg = 1;
+    int min_cdeg = 1 << 30;
+    for (int i = 0; i < h.M; ++i) min_cdeg = std::min(min_cdeg, h.row_ptr[i + 1] - h.row_ptr[i]);
+    int checked = 0;
+    *violations = 0;
+    std::string first;
+    for (int i = 0; i < kBsNInst; ++i)
+        for (int u = 0; u < 2; ++u) {
+            const BsPlan p = plan_inst(g, i, u != 0, clip, min_cdeg, mode, T);
+            if (!p.ok) continue;
+            const BsHostTables t = bs_host_tables(g, p);
+            BoundsReport r;
+            bs_bounds_check(g, p, t, T, flags, r);
+            ++checked;
+            if (r.violations && first.empty()) {
+                char buf[64];
+                snprintf(buf, sizeof(buf), "instance %d%s: ", i, u ? " ucn" : "");
+                first = std::string(buf) + r.first;
+            }
+            *violations += r.violations;
+        }
+    if (msg && msg_len > 0) {
+        std::strncpy(msg, first.c_str(), (size_t)msg_len - 1);
+        msg[msg_len - 1] = 0;
+    }
+    return checked;
+}

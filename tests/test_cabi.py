@@ -1,5 +1,6 @@
-"""C-ABI library: loads, exports every symbol include/ldpc_nms.h declares, and validates
-arguments before touching the GPU (CPU only — no compute calls)."""
+"""C-ABI library: loads, exports every symbol include/*.h declares (the decoder ABI
+ldpc_nms.h and the test hooks of ldpc_nms_debug.h), and validates arguments before touching
+the GPU (CPU only — no compute calls)."""
 import ctypes
 import os
 import re
@@ -9,13 +10,18 @@ import pytest
 from conftest import ROOT
 
 HEADER = os.path.join(ROOT, "include", "ldpc_nms.h")
+HEADERS = sorted(os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))
+                 if f.endswith(".h"))
 LIB = os.path.join(ROOT, "ldpc_error_floor_amd", "libldpc_nms.so")
 
 
-def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(ldpc_\w+)\s*\(", src, flags=re.M)))
+def declared_functions(headers=(HEADER,)):
+    out = set()
+    for hdr in headers:
+        src = open(hdr).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        out |= set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(ldpc_\w+)\s*\(", src, flags=re.M))
+    return sorted(out)
 
 
 @pytest.fixture(scope="module")
@@ -33,7 +39,9 @@ def test_header_declares_the_boundary():
 
 
 def test_every_declared_symbol_is_exported(lib):
-    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    fns = declared_functions(HEADERS)
+    assert "ldpc_debug_bs_bounds" in fns and "ldpc_decode" in fns
+    missing = [f for f in fns if not hasattr(lib, f)]
     assert not missing, missing
 
 
