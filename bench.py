@@ -216,6 +216,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        from ldpc_error_floor_amd.launch import fail_hook
+        fail_hook(rank, "bench.py")
 
     def allreduce(t, op):
         """In-place all-reduce of a device tensor (host round trip for gloo)."""

@@ -18,7 +18,7 @@ import subprocess
 import sys
 import time
 
-__all__ = ["free_port", "launch_ranks", "rank_info", "init_rank_group"]
+__all__ = ["free_port", "launch_ranks", "rank_info", "init_rank_group", "fail_hook"]
 
 
 def free_port() -> int:
@@ -58,6 +58,17 @@ def launch_ranks(script: str, argv, n: int, tag: str = None, extra_env=None) -> 
                     q.terminate()
         time.sleep(0.05)
     return status
+
+
+def fail_hook(rank: int, tag: str) -> None:
+    """Test hook: ``LDPC_TEST_FAIL_RANK=r`` makes rank r exit with status 7 once its process
+    group is up (the others then wait in their first collective), so a test can check that one
+    failing rank stops the whole job with a non-zero status (``launch_ranks``)."""
+    fr = os.environ.get("LDPC_TEST_FAIL_RANK")
+    if fr is not None and int(fr) == rank:
+        print(f"{tag}: rank {rank}: LDPC_TEST_FAIL_RANK, exiting with status 7", file=sys.stderr,
+              flush=True)
+        os._exit(7)
 
 
 def rank_info():

@@ -86,3 +86,24 @@ def test_sweep_tool_world2_equals_world1(tmp_path, monkeypatch):
     # and a world-1 sweep's checkpoints are refused by a world-2 job, on both ranks
     got = _run_ranks(2, one)
     assert all(g[1] == -1 and "ValueError" in g[2] for g in got), got
+
+
+def test_sweep_tool_world8_equals_world1(tmp_path, monkeypatch):
+    """The world size configs[3] / configs[4] name (8 ranks, gloo on CPU): every SNR point's
+    codewords split over eight ranks give the counters of one process, and each rank keeps its
+    own checkpoint."""
+    import sweep_c5
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("LDPC_SWEEP_BACKEND", "gloo")
+    one = str(tmp_path / "w1")
+    assert sweep_c5.main(ARGS + ["--out", one], make_decoder=make_oracle_decoder) == 0
+    _, c1 = _counters(one)
+    eight = str(tmp_path / "w8")
+    got = _run_ranks(8, eight)
+    assert [g[1] for g in got] == [0] * 8, got
+    j8, c8 = _counters(eight)
+    assert j8["n_gpus"] == 8 and j8["process_group"] == {"backend": "gloo", "world": 8}
+    assert c8 == c1
+    for r in range(1, 8):
+        assert os.path.exists(os.path.join(eight, f"ckpt_scan.json.rank{r}"))

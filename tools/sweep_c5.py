@@ -91,6 +91,9 @@ def main(argv=None, make_decoder=None):
 
     backend = os.environ.get("LDPC_SWEEP_BACKEND", "nccl")
     dev = init_rank_group(backend, local)
+    if launched:
+        from ldpc_error_floor_amd.launch import fail_hook
+        fail_hook(rank, "sweep_c5.py")
     os.makedirs(a.out, exist_ok=True)
     cfg = bench.CONFIGS[a.config]
     proto, g, W, cp = bench.load_problem(config=a.config)
