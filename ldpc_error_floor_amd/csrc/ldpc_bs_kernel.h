@@ -443,6 +443,9 @@ __device__ __forceinline__ void alpha_fixed(uint32_t (&p)[4], uint32_t (&q)[4], 
 #ifndef BS_DPP_BC
 #define BS_DPP_BC true
 #endif
+#ifndef BS_PRIO
+#define BS_PRIO 0
+#endif
 
 // lane permutation inside each group of 4 lanes (DPP quad_perm, a VALU move).  bound_ctrl on:
 // every lane of a quad_perm / row mirror has a source lane, so the "old" operand is dead — with
@@ -1378,6 +1381,10 @@ k_bs(BsArgs a) {
     }
     __syncthreads();
 
+    // wave priorities (A/B switch BS_PRIO: 1 the younger half of the workgroup at priority 1
+    // for the whole decode; 2 the check phase at priority 1, the variable phase at 0; 3 the
+    // reverse)
+    if (BS_PRIO == 1 && wave >= (nwv >> 1)) __builtin_amdgcn_s_setprio(1);
     for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
         PH("top", 0);
         if ((BS_TIDFREE ? wave == 0 : tid == 0) && t > 0) {   // fold iteration t-1's frame flags
@@ -1438,6 +1445,8 @@ k_bs(BsArgs a) {
             }
         }
         // ======== check nodes ===================================================================
+        if (BS_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+        if (BS_PRIO == 3) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const bool active = (CPL == 1) ? (BS_TIDFREE ? wave * 64 < a.cn_lanes : tid < a.cn_lanes)
@@ -1706,6 +1715,8 @@ k_bs(BsArgs a) {
         }
         __syncthreads();
         // ======== variable nodes ================================================================
+        if (BS_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+        if (BS_PRIO == 3) __builtin_amdgcn_s_setprio(1);
         const uint32_t bslice = a.off_blut + (uint32_t)(nx * BL * 4);
         if (t == a.T - 1) vn_phase(false, true, bslice, t + 1);
         else vn_phase(false, false, bslice, t + 1);
