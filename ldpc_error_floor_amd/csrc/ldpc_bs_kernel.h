@@ -443,8 +443,13 @@ __device__ __forceinline__ void alpha_fixed(uint32_t (&p)[4], uint32_t (&q)[4], 
 #ifndef BS_DPP_BC
 #define BS_DPP_BC true
 #endif
+// wave priorities (A/B switch): 2 runs each check phase at priority 1 and each variable phase at
+// 0, so that the check phase — the one with idle waves (C3: 7 of 12 waves hold check lanes) —
+// wins issue slots from the other resident workgroups' variable phases; -1 (default) picks 2 for
+// the one-chunk instances (several workgroups per CU; same box, r5j: C2 4.71 -> 4.64 ms, C3
+// 13.56 -> 12.99) and 0 for the multi-chunk ones (one workgroup per CU: C4 11.32 against 11.38)
 #ifndef BS_PRIO
-#define BS_PRIO 0
+#define BS_PRIO -1
 #endif
 
 // lane permutation inside each group of 4 lanes (DPP quad_perm, a VALU move).  bound_ctrl on:
@@ -1381,10 +1386,11 @@ k_bs(BsArgs a) {
     }
     __syncthreads();
 
-    // wave priorities (A/B switch BS_PRIO: 1 the younger half of the workgroup at priority 1
-    // for the whole decode; 2 the check phase at priority 1, the variable phase at 0; 3 the
-    // reverse)
-    if (BS_PRIO == 1 && wave >= (nwv >> 1)) __builtin_amdgcn_s_setprio(1);
+    // wave priorities (BS_PRIO: 1 the younger half of the workgroup at priority 1 for the whole
+    // decode; 2 the check phase at priority 1, the variable phase at 0; 3 the reverse; 4 the
+    // check phase at 2, the variable phase at 1 on the waves whose first place has degree >= DV - 1)
+    constexpr int PRIO = BS_PRIO >= 0 ? BS_PRIO : ((VPL == 1 && CPL == 1) ? 2 : 0);
+    if (PRIO == 1 && wave >= (nwv >> 1)) __builtin_amdgcn_s_setprio(1);
     for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
         PH("top", 0);
         if ((BS_TIDFREE ? wave == 0 : tid == 0) && t > 0) {   // fold iteration t-1's frame flags
@@ -1445,8 +1451,9 @@ k_bs(BsArgs a) {
             }
         }
         // ======== check nodes ===================================================================
-        if (BS_PRIO == 2) __builtin_amdgcn_s_setprio(1);
-        if (BS_PRIO == 3) __builtin_amdgcn_s_setprio(0);
+        if (PRIO == 2) __builtin_amdgcn_s_setprio(1);
+        if (PRIO == 3) __builtin_amdgcn_s_setprio(0);
+        if (PRIO == 4) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const bool active = (CPL == 1) ? (BS_TIDFREE ? wave * 64 < a.cn_lanes : tid < a.cn_lanes)
@@ -1715,8 +1722,12 @@ k_bs(BsArgs a) {
         }
         __syncthreads();
         // ======== variable nodes ================================================================
-        if (BS_PRIO == 2) __builtin_amdgcn_s_setprio(0);
-        if (BS_PRIO == 3) __builtin_amdgcn_s_setprio(1);
+        if (PRIO == 2) __builtin_amdgcn_s_setprio(0);
+        if (PRIO == 3) __builtin_amdgcn_s_setprio(1);
+        if (PRIO == 4) {                     // the waves of the heaviest variables first
+            if (dw[0] >= DV - 1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         const uint32_t bslice = a.off_blut + (uint32_t)(nx * BL * 4);
         if (t == a.T - 1) vn_phase(false, true, bslice, t + 1);
         else vn_phase(false, false, bslice, t + 1);
