@@ -73,10 +73,10 @@ constexpr BsInst kBsInst[] = {
 constexpr int kBsNInst = sizeof(kBsInst) / sizeof(kBsInst[0]);
 
 // The QMS channel generated in the kernel's prologue (Q8 builds; ldpc_decode_awgn, SURVEY 8 f
-// rank 1): the byte each LLR would have in k_awgn_q8's byte channel, from the same Philox stream
-// and level sampler (ldpc_awgn.h), so the decode is bit-identical to ldpc_channel_awgn +
-// ldpc_decode.  The sampler's tables (awgn_gen_table, 8.25 KB) are copied into LDS at `lds`, a
-// region the kernel writes only after the prologue.
+// rank 1): the byte each LLR would have on the q-bit grid (level + 16 + kmin), from the same
+// Philox stream and level sampler as ldpc_channel_awgn (ldpc_awgn.h), so the decode is
+// bit-identical to ldpc_channel_awgn + ldpc_decode.  The sampler's tables (awgn_gen_table,
+// 8.25 KB) are copied into LDS at `lds`, a region the kernel writes only after the prologue.
 struct BsGen {
     const uint32_t* tab;         // [AWGN_TAB_W] (awgn_gen_table)
     uint32_t k0, k1;             // Philox key (the seed)
@@ -740,7 +740,7 @@ __device__ __forceinline__ int pack_channel(const float (&xv)[PACK], float inv, 
 }
 // The bytes of variable v for the 32 codewords of pack pk, generated (Q8 builds): byte r of
 // D[r / 4] = level + 16 + kmin of codeword offset + 32 pk + r (a shortened bit: 48 - qmax, a
-// punctured one: 16), exactly k_awgn_q8's words.  Four codewords per Philox call; a batch offset
+// punctured one: 16; oracle/philox_oracle.py awgn_q8).  Four codewords per Philox call; a batch offset
 // off the quads takes two quads per word and a byte funnel shift (wave-uniform).
 typedef unsigned int v2u_g __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const v2u_g LdsU2;

@@ -170,13 +170,14 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
     holds the channel stream (``CHANNEL_STREAM``), the decoder and the partition, so a resume
     with anything else is refused.
 
-    ``overlap``: when the decoding kernel reads its LLRs from HBM (the bit-sliced kernels: the
-    channel is a kernel of its own), generate batch j + 1 on a second stream while batch j
-    decodes (``pipelined_channel_decode``); the counters are the same either way.  Off by
-    default: measured on one MI355X (``tools/overlap_probe.py``, ``profiles/r3/overlap``), it
-    gained nothing (C2 6.36 against 6.29 ms per 2^20-codeword step, C4 / C5 equal, C3 1.6 %
-    slower) — the channel kernel is VALU-bound too and finds no idle issue slots beside the
-    decode's waves."""
+    ``overlap``: when the decoding kernel reads its LLRs from HBM (the float modes' ffl and
+    flood: their channel is a kernel of its own; the QMS bit-sliced and v5 kernels generate it in
+    their prologue), generate batch j + 1 on a second stream while batch j decodes
+    (``pipelined_channel_decode``); the counters are the same either way.  Off by default:
+    measured on one MI355X when the bit-sliced kernels still read HBM LLRs
+    (``tools/overlap_probe.py``, ``profiles/r3/overlap``), it gained nothing (C2 6.36 against
+    6.29 ms per 2^20-codeword step, C4 / C5 equal, C3 1.6 % slower) — the channel kernel is
+    VALU-bound too and finds no idle issue slots beside the decode's waves."""
     import torch
     import torch.distributed as dist
     dist_on = dist.is_available() and dist.is_initialized()
@@ -301,8 +302,8 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
 
 def _pipelines(decoder, T, kernel) -> bool:
     """Whether ``decoder`` runs on a GPU and ``ldpc_decode_awgn`` would generate its LLRs with
-    the channel kernel into HBM (every kernel but the fused v5, which generates in its
-    prologue)."""
+    the channel kernel into HBM (flood and ffl; the fused v5 and the QMS bit-sliced kernels
+    generate in their prologue)."""
     dev = getattr(decoder, "device", None)
     if getattr(dev, "type", None) != "cuda" or not hasattr(decoder, "generates_channel_in_kernel"):
         return False

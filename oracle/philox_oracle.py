@@ -187,7 +187,8 @@ def awgn_qms_llr(B, n_vars, sigma, seed, offset=0, q_bit=5, punct=(0, 0), short=
 
 
 def awgn_q8(B, n_vars, sigma, seed, offset=0, q_bit=5, punct=(0, 0), short=(0, 0)):
-    """ldpc_decode_awgn's byte channel (k_awgn_q8) uint8 [ceil(B/32)][n_vars][32]: byte r of
+    """ldpc_decode_awgn's byte channel (the bytes the bit-sliced kernels' prologue generates,
+    gen_bytes in ldpc_bs_kernel.h) uint8 [ceil(B/32)][n_vars][32]: byte r of
     (pack, v) = grid value + 16 of codeword 32 pack + r (rows past B generated too), 16 on a
     punctured bit, 48 - qmax on a shortened one (the bit-sliced kernels' marker)."""
     npk = (B + 31) // 32

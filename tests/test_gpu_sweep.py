@@ -87,16 +87,19 @@ def test_sweep_resume_on_gpu(cuda_device, tmp_path):
 @pytest.mark.parametrize("cfg", ["C2", "C5"])
 def test_sweep_overlapped_channel_equals_inline(cuda_device, cfg):
     """fer_sweep's pipelined path (batch j + 1's channel kernel on a second stream while batch j
-    decodes, for the kernels that read their LLRs from HBM) decodes exactly the codewords of the
-    in-line path: several SNR points and a ragged last batch."""
+    decodes, for the kernels that read their LLRs from HBM: the float modes' ffl / flood) decodes
+    exactly the codewords of the in-line path: several SNR points and a ragged last batch.  The
+    QMS bit-sliced decodes generate their channel in the kernel's prologue and do not pipeline."""
     import bench
     from ldpc_error_floor_amd.decoder import NMSDecoder
     from ldpc_error_floor_amd.fer import fer_sweep, _pipelines
     c = bench.CONFIGS[cfg]
     proto, g, W, cp = bench.load_problem(T=12, config=cfg)
-    dec = NMSDecoder(proto, c["z"], W, 2, 5, device=cuda_device)
+    qms = NMSDecoder(proto, c["z"], W, 2, 5, device=cuda_device)
+    assert qms.kernel_info()[1].startswith(("bsl[", "bsc[")) and not _pipelines(qms, None, None)
+    dec = NMSDecoder(proto, c["z"], W, 1, 5, device=cuda_device)        # min-sum fp32
     dec.punct, dec.short = c.get("punct", (0, 0)), c.get("short", (0, 0))
-    assert _pipelines(dec, None, None) and dec.kernel_info()[1].startswith(("bsl[", "bsc["))
+    assert _pipelines(dec, None, None)
     sig = [float(cp.sigma(c["snr"] - 1.0)), float(cp.sigma(c["snr"] - 0.5))]
     key = lambda rs: [(r.bit_err_last, r.frame_err_last, r.frame_err_all, r.loss2) for r in rs]  # noqa: E731
     inline = key(fer_sweep(dec, sig, 9000, 2048, seed=4))

@@ -103,7 +103,8 @@ def test_qms_sampler_matches_reference_channel_frequencies():
 
 def test_qms_stream_sharding_and_layout():
     """Global-codeword indexing (any offset, unaligned quads included) and the byte layout of
-    the bit-sliced kernels' channel (k_awgn_q8)."""
+    the bytes the bit-sliced kernels' prologue generates per variable and codeword (gen_bytes,
+    ldpc_bs_kernel.h) before packing them into planes."""
     sig, seed = 0.7, (1 << 35) + 5
     whole = awgn_qms_llr(77, 130, sig, seed, offset=1001)
     for off in (1002, 1004, 1037):
