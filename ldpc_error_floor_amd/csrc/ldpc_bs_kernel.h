@@ -608,6 +608,22 @@ __device__ __forceinline__ void min2_bits(uint32_t (&m1)[4], uint32_t (&m2)[4], 
 #ifndef BS_BSMIN_MC
 #define BS_BSMIN_MC 1   // ... on the multi-chunk instances too (A/B switch)
 #endif
+// The switch over a chunk's real positions (1 <= gmc <= EPL for every active chunk, by
+// construction: ceil(degree / lanes per check) of its widest check) may mark every other count
+// unreachable (U), and zero the tie words of the positions past it (Z).  Without U the compiler
+// keeps the search's inputs and outputs alive through the empty cases and copies them at the join
+// (C4, static: 39 v_mov per chunk, 2.47 -> 2.28 VALU per pack-edge-iteration) — yet the bsl C4
+// build ran slower with it (same box, r5o: 11.41-11.49 ms against 11.29-11.32 for U, Z, U+Z),
+// while bsc's C5 gains (48.4 -> 47.9 ms): U on for bsc (BSC_MIN2_U), off for bsl
+#ifndef BS_MIN2_U
+#define BS_MIN2_U 0
+#endif
+#ifndef BS_MIN2_Z
+#define BS_MIN2_Z 0
+#endif
+#ifndef BSC_MIN2_U
+#define BSC_MIN2_U 1
+#endif
 
 template <int CTRL>
 __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]) {
@@ -1180,7 +1196,7 @@ k_bs(BsArgs a) {
 #pragma unroll
                 for (int f = 0; f < DV; ++f) {
                     if (f < dwu) {
-                        PH("vn_sum", (last ? 100 : 0) + f);
+                        PH("vn_sum", (last ? 100 : 0) + 10 * u + f);
                         uint32_t M[4], n, b[4];
                         read_slot(n, M, vaddr(f));
 #pragma unroll
@@ -1253,7 +1269,7 @@ k_bs(BsArgs a) {
                 for (int f = 0; f < DV; ++f) {
                     if (f < dwu) {
                         if (ABL(4)) continue;
-                        PH("vn_vc", (last ? 100 : 0) + f);
+                        PH("vn_vc", (last ? 100 : 0) + 10 * u + f);
                         uint32_t x[7], X[4], n, b[4];
                         if (f < KEEP) {
                             n = mn[f < KEEP ? f : 0];
@@ -1564,12 +1580,22 @@ k_bs(BsArgs a) {
                     switch (gmc) {                   // wave-uniform: the chunk's real positions
 #define BS_MIN2_CASE(k)                                                                            \
     case k:                                                                                        \
-        if constexpr (k <= EPL) min2_bits<k, LPC>(m1, m2, cand, Xs);                               \
+        if constexpr (k <= EPL) {                                                                  \
+            PH("ck_mink", 16 * c + k);                                                             \
+            min2_bits<k, LPC>(m1, m2, cand, Xs);                                                   \
+            if (BS_MIN2_Z) {                                                                       \
+                _Pragma("unroll") for (int m = k; m < EPL; ++m) cand[m] = 0u;                      \
+            }                                                                                      \
+        } else if (BS_MIN2_U) {                                                                    \
+            __builtin_unreachable();                                                               \
+        }                                                                                          \
         break;
                         BS_MIN2_CASE(1) BS_MIN2_CASE(2) BS_MIN2_CASE(3) BS_MIN2_CASE(4) BS_MIN2_CASE(5)
                         BS_MIN2_CASE(6) BS_MIN2_CASE(7) BS_MIN2_CASE(8)
 #undef BS_MIN2_CASE
-                        default: break;
+                        default:
+                            if (BS_MIN2_U) __builtin_unreachable();   // (an active chunk: 1 <= gmc <= EPL)
+                            break;
                     }
                 } else {
                     min2_bits<EPL, LPC>(m1, m2, cand, Xs);
@@ -1692,9 +1718,9 @@ k_bs(BsArgs a) {
             // (if it is not the only one, the two minima are equal), the others the minimum
 #pragma unroll
             for (int m = 0; m < EPL; ++m) {
-                if (m == 0) PH8("ck_pass2", 0, q1, q2);
+                if (m == 0) PH8("ck_pass2", 16 * c, q1, q2);
                 if (real2(m)) {
-                    if (m > 0) PH("ck_pass2", m);
+                    if (m > 0) PH("ck_pass2", 16 * c + m);
                     const uint32_t addr = ALDS ? caddr(m) : cbase + m * cstride;
                     uint32_t Mg[4];
                     if constexpr (BSM) {

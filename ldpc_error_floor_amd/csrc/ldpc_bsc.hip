@@ -503,12 +503,21 @@ k_bsc(BscArgs a) {
                 switch (gmc) {
 #define BSC_MIN2_CASE(k)                                                                           \
     case k:                                                                                        \
-        if constexpr (k <= EPL) min2_bits<k, L>(m1, m2, cand, Xs);                                 \
+        if constexpr (k <= EPL) {                                                                  \
+            min2_bits<k, L>(m1, m2, cand, Xs);                                                     \
+            if (BS_MIN2_Z) {                                                                       \
+                _Pragma("unroll") for (int m = k; m < EPL; ++m) cand[m] = 0u;                      \
+            }                                                                                      \
+        } else if (BSC_MIN2_U) {                                                                   \
+            __builtin_unreachable();                                                               \
+        }                                                                                          \
         break;
                     BSC_MIN2_CASE(1) BSC_MIN2_CASE(2) BSC_MIN2_CASE(3) BSC_MIN2_CASE(4) BSC_MIN2_CASE(5)
                     BSC_MIN2_CASE(6) BSC_MIN2_CASE(7) BSC_MIN2_CASE(8) BSC_MIN2_CASE(9) BSC_MIN2_CASE(10)
 #undef BSC_MIN2_CASE
-                    default: break;
+                    default:
+                        if (BSC_MIN2_U) __builtin_unreachable();  // (an active chunk: 1 <= gmc <= EPL)
+                        break;
                 }
                 par ^= qperm<QP_X1>(par);
                 if (L == 4) par ^= qperm<QP_X2>(par);

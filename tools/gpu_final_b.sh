@@ -2,7 +2,7 @@
 # modes on C2
 set -o pipefail
 export TMPDIR=/tmp
-TAG=${TAG:-r4f}
+TAG=${TAG:-r5z}
 OUT=gpurun_out/ev_$TAG; mkdir -p $OUT
 CONFIGS="C3 C4 C5" bash tools/bench_configs.sh > $OUT/bench_configs.log 2>&1 || { tail -20 $OUT/bench_configs.log; exit 1; }
 cp gpurun_out/bench_C3.json gpurun_out/bench_C4.json gpurun_out/bench_C5.json $OUT/

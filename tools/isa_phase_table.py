@@ -184,6 +184,7 @@ def analyse(path, want):
             c = classify(x)
             if c:
                 counts[ph][c] += 1
+                DUMP[ph.rsplit(".", 1)[0]][x.split()[0] + ("/" + c if c != "v2" else "")] += 1
             elif x.startswith("ds_"):
                 other[ph]["lds"] += 1
             elif x.startswith("s_swappc"):
@@ -204,6 +205,38 @@ def analyse(path, want):
     return name, counts, other, tables
 
 
+DUMP = defaultdict(lambda: defaultdict(int))   # phase -> mnemonic/form -> static count (--dump)
+
+
+def deal_chunks(cost, nw, cap):
+    """ldpc_bs.hip deal_chunks (LPT): slot[w * cap + u] = chunk or -1"""
+    n = len(cost)
+    order = sorted(range(n), key=lambda c: -cost[c])
+    vch, vload = [[] for _ in range(nw)], [0] * nw
+    for c in order:
+        best = -1
+        for w in range(nw):
+            if len(vch[w]) < cap and (best < 0 or vload[w] < vload[best] or
+                                      (vload[w] == vload[best] and len(vch[w]) < len(vch[best]))):
+                best = w
+        vch[best].append(c)
+        vload[best] += cost[c]
+    vorder = sorted(range(nw), key=lambda w: -vload[w])
+    sload, nxt = [0] * 4, list(range(4))
+    slot = [-1] * (nw * cap)
+    for v in vorder:
+        sm = -1
+        for q in range(4):
+            if nxt[q] < nw and (sm < 0 or sload[q] < sload[sm]):
+                sm = q
+        w = nxt[sm]
+        nxt[sm] += 4
+        sload[sm] += vload[v]
+        for u, c in enumerate(vch[v]):
+            slot[w * cap + u] = c
+    return slot
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("asm")
@@ -214,17 +247,47 @@ def main():
     ap.add_argument("--product", help="the product (unmarked) build's .s, for the totals")
     ap.add_argument("--alt", default="vn_beta_fix=1,vn_beta_id=0,vn_beta_sg=0,vn_beta_lds=0",
                     help="weights of the alternative paths (the share of iterations taking each)")
+    ap.add_argument("--mc", help="multi-chunk instances: NW,VPL,CPL; with --vchunks / --cchunks the "
+                    "weights come from the host's dealing of the chunks to (wave, place) slots")
+    ap.add_argument("--vchunks", help="--mc: each variable chunk's largest degree, in chunk order")
+    ap.add_argument("--cchunks", help="--mc: each check chunk's real edge positions per lane (gm)")
+    ap.add_argument("--dump", help="print the static VALU mnemonics of these phases (comma list)")
     ap.add_argument("--json")
     a = ap.parse_args()
     alt = {kv.split("=")[0]: float(kv.split("=")[1]) for kv in a.alt.split(",") if kv}
     dw = [int(x) for x in a.dw.split(",")]
     name, counts, other, tables = analyse(a.asm, a.kernel)
+    mc = None
+    if a.mc:
+        nw, vpl, cpl = (int(x) for x in a.mc.split(","))
+        vd = [int(x) for x in a.vchunks.split(",")]
+        cg = [int(x) for x in a.cchunks.split(",")]
+        vs, cs = deal_chunks([3 + d for d in vd], nw, vpl), deal_chunks([2 + g for g in cg], nw, cpl)
+        # places[u] = degrees of the chunks at place u; cplaces[c] = gm of the chunks at place c
+        places = [[vd[vs[w * vpl + u]] for w in range(nw) if vs[w * vpl + u] >= 0] for u in range(vpl)]
+        cplaces = [[cg[cs[w * cpl + c]] for w in range(nw) if cs[w * cpl + c] >= 0] for c in range(cpl)]
+        mc = (nw, places, cplaces)
 
     def weight(ph):
         base, k = ph.rsplit(".", 1)
         k = int(k, 0)
         last = k >= 100
         k %= 100
+        if mc:
+            nw, places, cplaces = mc
+            if base == "ck_mink":
+                return "ck_min", last, sum(1 for g in cplaces[k // 16] if g == k % 16)
+            if base == "ck_pass2":            # K = 16 c + position m
+                return base, last, sum(1 for g in cplaces[k // 16] if g > k % 16)
+            if base.startswith("ck_"):
+                return base, last, len(cplaces[k])
+            if base in ("vn_sum", "vn_vc"):
+                return base, last, sum(1 for d in places[k // 10] if d > k % 10)
+            if base in alt:
+                return "vn_beta", last, alt[base] * len(places[k])
+            if base.startswith("vn_") and base != "vn_flags":
+                return base, last, len(places[k])
+            return base, last, nw
         if base in alt:
             return "vn_beta", last, alt[base] * len(dw)
         if base.startswith(("ck_", "top")):
@@ -270,9 +333,15 @@ def main():
     lv = sum(rows_last[b][f] for b in rows_last for f in FORMS)
     print(f"(the last iteration's variable phase instead: {lv:.3f} VALU per pack-edge)")
     if a.product:
+        saved = {k: dict(v) for k, v in DUMP.items()}
         _, pc, _, _ = analyse(a.product, a.kernel)
+        DUMP.clear()
+        DUMP.update({k: defaultdict(int, v) for k, v in saved.items()})
         print("product build (unmarked), by the same propagation from the loop head (one phase):",
               {f: sum(c[f] for c in pc.values()) for f in FORMS})
+    for phn in (a.dump.split(",") if a.dump else []):
+        hist = sorted(DUMP[phn].items(), key=lambda kv: -kv[1])
+        print(f"{phn}: " + ", ".join(f"{k} {v}" for k, v in hist))
     if a.json:
         json.dump({"kernel": name, "edges": a.edges, "dw": dw, "cwaves": a.cwaves,
                    "per_pack_edge_iter": out, "cost_cycles": COST}, open(a.json, "w"), indent=1)
