@@ -30,6 +30,7 @@
 // Packs with any other LLR off the quantizer grid are flagged in `bad` and decoded by the v5
 // kernel instead, so the result is exact for any input.
 #pragma once
+#include <type_traits>
 #include <cstdint>
 
 #include "ldpc_beta_tabs.h"
@@ -624,6 +625,13 @@ __device__ __forceinline__ void min2_bits(uint32_t (&m1)[4], uint32_t (&m2)[4], 
 #ifndef BSC_MIN2_U
 #define BSC_MIN2_U 1
 #endif
+// the variable phase at the fewest planes of S for each place's largest degree: 7 where
+// 15 dw + 15 <= 63, 8 where <= 127, else 9 (one copy of the phase per plane count).  -1 (default):
+// on the one-chunk instances (same box, r5p: C2 4.66 -> 4.61 ms, C3 12.99 -> 12.60), off on the
+// multi-chunk ones (C4 11.31 -> 11.74: the 128-VGPR build then spills 17 VGPRs); 0 off, 1 on
+#ifndef BS_SBV
+#define BS_SBV -1
+#endif
 
 template <int CTRL>
 __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]) {
@@ -1187,105 +1195,118 @@ k_bs(BsArgs a) {
             // 14.48 -> 14.41 ms same box (r3zh); wman and 5G BG2 keep BS_KEEP = 4 of 6 / 8)
             constexpr int KEEP0 = ((VPL > 1 || CPL > 1) && !UCN) ? BS_KEEP_MC : BS_KEEP;
             constexpr int KEEP = KEEP0 < DV ? KEEP0 : DV - 1;
-            uint32_t mn[KEEP > 0 ? KEEP : 1], mb[KEEP > 0 ? KEEP : 1][4];
-            uint32_t S[SB];
-#pragma unroll
-            for (int i = 0; i < SB; ++i) S[i] = 0u;
             const int dwu = dw[u];
-            if (!first) {
+            // the rest at SBX planes of S: the fewest that hold 15 dw + 15 for the place's largest
+            // degree dw (wave-uniform), BS_SBV
+            auto vbody = [&](auto sbc) __attribute__((always_inline)) {
+                constexpr int SB = decltype(sbc)::value;
+                uint32_t mn[KEEP > 0 ? KEEP : 1], mb[KEEP > 0 ? KEEP : 1][4];
+                uint32_t S[SB];
 #pragma unroll
-                for (int f = 0; f < DV; ++f) {
-                    if (f < dwu) {
-                        PH("vn_sum", (last ? 100 : 0) + 10 * u + f);
-                        uint32_t M[4], n, b[4];
-                        read_slot(n, M, vaddr(f));
+                for (int i = 0; i < SB; ++i) S[i] = 0u;
+                if (!first) {
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) b[i] = M[i] ^ n;
-                        if (f == 0) set_b<SB>(S, b, n);
-                        else add_b<SB>(S, b, n);
-                        if (f < KEEP) {
-                            mn[f < KEEP ? f : 0] = n;
-#pragma unroll
-                            for (int i = 0; i < 4; ++i) mb[f < KEEP ? f : 0][i] = b[i];
-                        }
-                    }
-                }
-                if constexpr (SB == 8) PH8("vn_app", (last ? 100 : 0) + u, S, (S + 4));
-                // APP_t = Q(ch) + S: the sign (hard decision) from the carry chain alone, the full
-                // sum only in the last iteration (APP > 0 for the loss counter)
-                uint32_t hd, nz = 0u;
-                const uint32_t c_s = cs[u];
-                if (last) {
-                    uint32_t A[SB];
-#pragma unroll
-                    for (int i = 0; i < SB; ++i) A[i] = S[i];
-                    const uint32_t cb[4] = {cmu[0] ^ c_s, cmu[1] ^ c_s, cmu[2] ^ c_s, cmu[3] ^ c_s};
-                    add_b<SB>(A, cb, c_s);
-                    hd = ~A[SB - 1];
-#pragma unroll
-                    for (int i = 0; i < SB; ++i) nz |= A[i];
-                } else {
-                    uint32_t c = c_s;
-#pragma unroll
-                    for (int i = 0; i < SB - 1; ++i) c = B3(T_MAJ, S[i], i < 4 ? (cmu[i] ^ c_s) : c_s, c);
-                    hd = B3(T_XNOR3, S[SB - 1], c_s, c);
-                }
-                if (UCN && !last && v >= 0 && ucn_on(tb)) lds_put(hda, hd);   // HD[v] (Main_Functions.py:184-188)
-                hd &= valid;                                     // APP >= 0 -> hard decision 1
-                if constexpr (XP) {                              // iteration tb - 1's hard decisions
-                    if (v >= 0) a.hdx[((size_t)(tb - 1) * (size_t)((a.B + 31) >> 5) + blockIdx.x) * nv + v] = hd;
-                }
-                if (ABL(8)) hd = 0u;
-                if (counted) {
-                    wr |= hd;
-                    if (last) {
-                        apos |= hd & nz;
-                        nb += (uint32_t)__popc(hd);
-                    }
-                }
-            }
-            if (last) continue;
-            if constexpr (SB == 8) PH8("vn_tv", (last ? 100 : 0) + u, S, (S + 4));
-            // Tv = clamp(Q(beta ch) + S): the table gives |Q(beta ch)|, the channel the sign
-            uint32_t lb[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) lb[i] = lw[0][i] ^ cs[u];
-            add_b<SB>(S, lb, cs[u]);
-            uint32_t Tv[6];
-            clamp6<SB>(Tv, S);
-            const int dwm = dwmin[u];
-            if (first) {
-                // UCN at t = 0: the hard decision of x~ = Q(beta_0 ch) (Main_Functions.py:181-182)
-                if (UCN && v >= 0 && ucn_on(0)) lds_put(hda, ~Tv[5]);
-                uint32_t x[7], X[4];
-#pragma unroll
-                for (int i = 0; i < 7; ++i) x[i] = Tv[i < 6 ? i : 5];
-                abs_sat(X, x);
-#pragma unroll
-                for (int f = 0; f < DV; ++f)
-                    if (f < dwu && (f < dwm || vaddr(f) != a.off_zero)) write_slot(vaddr(f), x[6], X);
-            } else {
-#pragma unroll
-                for (int f = 0; f < DV; ++f) {
-                    if (f < dwu) {
-                        if (ABL(4)) continue;
-                        PH("vn_vc", (last ? 100 : 0) + 10 * u + f);
-                        uint32_t x[7], X[4], n, b[4];
-                        if (f < KEEP) {
-                            n = mn[f < KEEP ? f : 0];
-#pragma unroll
-                            for (int i = 0; i < 4; ++i) b[i] = mb[f < KEEP ? f : 0][i];
-                        } else {
-                            uint32_t M[4];
+                    for (int f = 0; f < DV; ++f) {
+                        if (f < dwu) {
+                            PH("vn_sum", (last ? 100 : 0) + 10 * u + f);
+                            uint32_t M[4], n, b[4];
                             read_slot(n, M, vaddr(f));
 #pragma unroll
                             for (int i = 0; i < 4; ++i) b[i] = M[i] ^ n;
+                            if (f == 0) set_b<SB>(S, b, n);
+                            else add_b<SB>(S, b, n);
+                            if (f < KEEP) {
+                                mn[f < KEEP ? f : 0] = n;
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) mb[f < KEEP ? f : 0][i] = b[i];
+                            }
                         }
-                        sub_tv(x, Tv, b, n);
-                        abs_sat(X, x);
-                        if (f < dwm || vaddr(f) != a.off_zero) write_slot(vaddr(f), x[6], X);
+                    }
+                    if constexpr (SB == 8) PH8("vn_app", (last ? 100 : 0) + u, S, (S + 4));
+                    // APP_t = Q(ch) + S: the sign (hard decision) from the carry chain alone, the full
+                    // sum only in the last iteration (APP > 0 for the loss counter)
+                    uint32_t hd, nz = 0u;
+                    const uint32_t c_s = cs[u];
+                    if (last) {
+                        uint32_t A[SB];
+#pragma unroll
+                        for (int i = 0; i < SB; ++i) A[i] = S[i];
+                        const uint32_t cb[4] = {cmu[0] ^ c_s, cmu[1] ^ c_s, cmu[2] ^ c_s, cmu[3] ^ c_s};
+                        add_b<SB>(A, cb, c_s);
+                        hd = ~A[SB - 1];
+#pragma unroll
+                        for (int i = 0; i < SB; ++i) nz |= A[i];
+                    } else {
+                        uint32_t c = c_s;
+#pragma unroll
+                        for (int i = 0; i < SB - 1; ++i) c = B3(T_MAJ, S[i], i < 4 ? (cmu[i] ^ c_s) : c_s, c);
+                        hd = B3(T_XNOR3, S[SB - 1], c_s, c);
+                    }
+                    if (UCN && !last && v >= 0 && ucn_on(tb)) lds_put(hda, hd);   // HD[v] (Main_Functions.py:184-188)
+                    hd &= valid;                                     // APP >= 0 -> hard decision 1
+                    if constexpr (XP) {                              // iteration tb - 1's hard decisions
+                        if (v >= 0) a.hdx[((size_t)(tb - 1) * (size_t)((a.B + 31) >> 5) + blockIdx.x) * nv + v] = hd;
+                    }
+                    if (ABL(8)) hd = 0u;
+                    if (counted) {
+                        wr |= hd;
+                        if (last) {
+                            apos |= hd & nz;
+                            nb += (uint32_t)__popc(hd);
+                        }
                     }
                 }
+                if (last) return;
+                if constexpr (SB == 8) PH8("vn_tv", (last ? 100 : 0) + u, S, (S + 4));
+                // Tv = clamp(Q(beta ch) + S): the table gives |Q(beta ch)|, the channel the sign
+                uint32_t lb[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) lb[i] = lw[0][i] ^ cs[u];
+                add_b<SB>(S, lb, cs[u]);
+                uint32_t Tv[6];
+                clamp6<SB>(Tv, S);
+                const int dwm = dwmin[u];
+                if (first) {
+                    // UCN at t = 0: the hard decision of x~ = Q(beta_0 ch) (Main_Functions.py:181-182)
+                    if (UCN && v >= 0 && ucn_on(0)) lds_put(hda, ~Tv[5]);
+                    uint32_t x[7], X[4];
+#pragma unroll
+                    for (int i = 0; i < 7; ++i) x[i] = Tv[i < 6 ? i : 5];
+                    abs_sat(X, x);
+#pragma unroll
+                    for (int f = 0; f < DV; ++f)
+                        if (f < dwu && (f < dwm || vaddr(f) != a.off_zero)) write_slot(vaddr(f), x[6], X);
+                } else {
+#pragma unroll
+                    for (int f = 0; f < DV; ++f) {
+                        if (f < dwu) {
+                            if (ABL(4)) continue;
+                            PH("vn_vc", (last ? 100 : 0) + 10 * u + f);
+                            uint32_t x[7], X[4], n, b[4];
+                            if (f < KEEP) {
+                                n = mn[f < KEEP ? f : 0];
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) b[i] = mb[f < KEEP ? f : 0][i];
+                            } else {
+                                uint32_t M[4];
+                                read_slot(n, M, vaddr(f));
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) b[i] = M[i] ^ n;
+                            }
+                            sub_tv(x, Tv, b, n);
+                            abs_sat(X, x);
+                            if (f < dwm || vaddr(f) != a.off_zero) write_slot(vaddr(f), x[6], X);
+                        }
+                    }
+                }
+            };
+            constexpr bool SBV = BS_SBV < 0 ? (VPL == 1 && CPL == 1) : BS_SBV != 0;
+            if constexpr (SBV && SB >= 8) {
+                if (dwu * QMAX + QMAX <= 63) vbody(std::integral_constant<int, 7>{});
+                else if (SB == 9 && dwu * QMAX + QMAX <= 127) vbody(std::integral_constant<int, (SB == 9 ? 8 : SB)>{});
+                else vbody(std::integral_constant<int, SB>{});
+            } else {
+                vbody(std::integral_constant<int, SB>{});
             }
         }
         if (!first) {
