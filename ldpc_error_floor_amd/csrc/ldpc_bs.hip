@@ -882,6 +882,8 @@ static int bs_bounds_check(const DevGraph& g, const BsPlan& p, const BsHostTable
                     any |= (1u << ((gdeg + LPC - 1) / LPC)) - 1u;
                 }
                 gm = __builtin_popcount(any);
+                // the kernels' switch over the real positions covers 1 .. EPL (BS_MIN2_CASE)
+                if (active) r.in("real positions - 1 (the min2 switch)", gm - 1, EPL);
             }
             for (int l = 0; l < 64; ++l) {
                 const int ql = std::max(gchunk, 0) * 64 + l, cc = ql / LPC, cj = l % LPC;
