@@ -26,6 +26,12 @@
 namespace ldpc {
 namespace bs {
 
+// the variable phase at the fewest planes of S for each place's largest degree (bsl's BS_SBV;
+// A/B switch)
+#ifndef BSC_SBV
+#define BSC_SBV 1
+#endif
+
 // instances: D = check-degree bound, DVH / DVL = variable-degree bound of a lane's first /
 // other variables, LPC lanes per check, VPL variables and CPL check chunks per lane
 // (a wman-sized instance — one variable and one check chunk per lane, 64 VGPRs — was measured
@@ -262,68 +268,86 @@ k_bsc(BscArgs a) {
                     lw[0][3] = mux(bg[u], gb.w, lw[0][3]);
                 }
             }
-            uint32_t S[SB];
-#pragma unroll
-            for (int i = 0; i < SB; ++i) S[i] = 0u;
             const int dwu = dw[u];
-            if (!first) {
+            // the rest at SBX planes of S: the fewest that hold 15 dw + 15 for the place's largest
+            // degree (bsl's BS_SBV; the places past the first hold at most DVL edges)
+            auto vbody = [&](auto sbc) __attribute__((always_inline)) {
+                constexpr int SB = decltype(sbc)::value;
+                uint32_t S[SB];
 #pragma unroll
-                for (int f = 0; f < DVH; ++f) {
-                    if (f < dvu && f < dwu) {
-                        const uint32_t wd = va[u][f];
-                        const uint32_t sa = (wd & 0xFFFFu) << 2;
-                        const uint32_t ra = a.off_rec + ((wd >> 16) << 4);
-                        const uint32_t n = lds_w(sa), am = lds_w(sa + a.off_a);
-                        const v4u q1 = lds_q(ra), q2 = lds_q(ra + REC_Q2);
-                        uint32_t b[4];
-                        b[0] = mux(am, q2.x, q1.x) ^ n;
-                        b[1] = mux(am, q2.y, q1.y) ^ n;
-                        b[2] = mux(am, q2.z, q1.z) ^ n;
-                        b[3] = mux(am, q2.w, q1.w) ^ n;
-                        if (f == 0) set_b<SB>(S, b, n);
-                        else add_b<SB>(S, b, n);
+                for (int i = 0; i < SB; ++i) S[i] = 0u;
+                if (!first) {
+#pragma unroll
+                    for (int f = 0; f < DVH; ++f) {
+                        if (f < dvu && f < dwu) {
+                            const uint32_t wd = va[u][f];
+                            const uint32_t sa = (wd & 0xFFFFu) << 2;
+                            const uint32_t ra = a.off_rec + ((wd >> 16) << 4);
+                            const uint32_t n = lds_w(sa), am = lds_w(sa + a.off_a);
+                            const v4u q1 = lds_q(ra), q2 = lds_q(ra + REC_Q2);
+                            uint32_t b[4];
+                            b[0] = mux(am, q2.x, q1.x) ^ n;
+                            b[1] = mux(am, q2.y, q1.y) ^ n;
+                            b[2] = mux(am, q2.z, q1.z) ^ n;
+                            b[3] = mux(am, q2.w, q1.w) ^ n;
+                            if (f == 0) set_b<SB>(S, b, n);
+                            else add_b<SB>(S, b, n);
+                        }
                     }
-                }
-                uint32_t hd, nz = 0u;
-                const uint32_t c_s = cs[u];
-                if (last) {
-                    uint32_t A[SB];
-#pragma unroll
-                    for (int i = 0; i < SB; ++i) A[i] = S[i];
-                    const uint32_t cb[4] = {cm[u][0] ^ c_s, cm[u][1] ^ c_s, cm[u][2] ^ c_s, cm[u][3] ^ c_s};
-                    add_b<SB>(A, cb, c_s);
-                    hd = ~A[SB - 1];
-#pragma unroll
-                    for (int i = 0; i < SB; ++i) nz |= A[i];
-                } else {
-                    uint32_t c = c_s;
-#pragma unroll
-                    for (int i = 0; i < SB - 1; ++i) c = B3(T_MAJ, S[i], i < 4 ? (cm[u][i] ^ c_s) : c_s, c);
-                    hd = B3(T_XNOR3, S[SB - 1], c_s, c);
-                }
-                hd &= valid;
-                if constexpr (XP) {                              // iteration tb - 1's hard decisions
-                    if (v >= 0) a.hdx[((size_t)(tb - 1) * (size_t)((a.B + 31) >> 5) + blockIdx.x) * nv + v] = hd;
-                }
-                if (counted) {
-                    wr |= hd;
+                    uint32_t hd, nz = 0u;
+                    const uint32_t c_s = cs[u];
                     if (last) {
-                        apos |= hd & nz;
-                        nb += (uint32_t)__popc(hd);
+                        uint32_t A[SB];
+#pragma unroll
+                        for (int i = 0; i < SB; ++i) A[i] = S[i];
+                        const uint32_t cb[4] = {cm[u][0] ^ c_s, cm[u][1] ^ c_s, cm[u][2] ^ c_s, cm[u][3] ^ c_s};
+                        add_b<SB>(A, cb, c_s);
+                        hd = ~A[SB - 1];
+#pragma unroll
+                        for (int i = 0; i < SB; ++i) nz |= A[i];
+                    } else {
+                        uint32_t c = c_s;
+#pragma unroll
+                        for (int i = 0; i < SB - 1; ++i) c = B3(T_MAJ, S[i], i < 4 ? (cm[u][i] ^ c_s) : c_s, c);
+                        hd = B3(T_XNOR3, S[SB - 1], c_s, c);
+                    }
+                    hd &= valid;
+                    if constexpr (XP) {                              // iteration tb - 1's hard decisions
+                        if (v >= 0) a.hdx[((size_t)(tb - 1) * (size_t)((a.B + 31) >> 5) + blockIdx.x) * nv + v] = hd;
+                    }
+                    if (counted) {
+                        wr |= hd;
+                        if (last) {
+                            apos |= hd & nz;
+                            nb += (uint32_t)__popc(hd);
+                        }
                     }
                 }
-            }
-            if (last || v < 0) continue;
-            uint32_t lb[4];
+                if (last || v < 0) return;
+                uint32_t lb[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) lb[i] = lw[0][i] ^ cs[u];
-            add_b<SB>(S, lb, cs[u]);
-            uint32_t Tv[6];
-            clamp6<SB>(Tv, S);
-            const uint32_t ta = a.off_tv + 24u * ((uint32_t)vv[u] >> 16);     // the Tv index
-            lds_dput(ta, Tv[0], Tv[1]);
-            lds_dput(ta + 8, Tv[2], Tv[3]);
-            lds_dput(ta + 16, Tv[4], Tv[5]);
+                for (int i = 0; i < 4; ++i) lb[i] = lw[0][i] ^ cs[u];
+                add_b<SB>(S, lb, cs[u]);
+                uint32_t Tv[6];
+                clamp6<SB>(Tv, S);
+                const uint32_t ta = a.off_tv + 24u * ((uint32_t)vv[u] >> 16);     // the Tv index
+                lds_dput(ta, Tv[0], Tv[1]);
+                lds_dput(ta + 8, Tv[2], Tv[3]);
+                lds_dput(ta + 16, Tv[4], Tv[5]);
+            };
+            if constexpr (BSC_SBV) {
+                auto dispatch = [&](auto smax) __attribute__((always_inline)) {
+                    constexpr int SM = decltype(smax)::value;
+                    if (dwu * QMAX + QMAX <= 63) vbody(std::integral_constant<int, 7>{});
+                    else if (SM == 9 && dwu * QMAX + QMAX <= 127) vbody(std::integral_constant<int, (SM == 9 ? 8 : SM)>{});
+                    else vbody(std::integral_constant<int, SM>{});
+                };
+                constexpr int SBL = (DVL * QMAX + QMAX <= 127) ? 8 : 9;    // places past the first
+                if (u == 0) dispatch(std::integral_constant<int, SB>{});
+                else dispatch(std::integral_constant<int, SBL>{});
+            } else {
+                vbody(std::integral_constant<int, SB>{});
+            }
         }
         if (!first) {
             wr = wave_or(wr);
