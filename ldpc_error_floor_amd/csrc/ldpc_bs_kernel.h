@@ -626,11 +626,16 @@ __device__ __forceinline__ void min2_bits(uint32_t (&m1)[4], uint32_t (&m2)[4], 
 #define BSC_MIN2_U 1
 #endif
 // the variable phase at the fewest planes of S for each place's largest degree: 7 where
-// 15 dw + 15 <= 63, 8 where <= 127, else 9 (one copy of the phase per plane count).  -1 (default):
-// on the one-chunk instances (same box, r5p: C2 4.66 -> 4.61 ms, C3 12.99 -> 12.60), off on the
-// multi-chunk ones (C4 11.31 -> 11.74: the 128-VGPR build then spills 17 VGPRs); 0 off, 1 on
+// 15 dw + 15 <= 63, 8 where <= 127, else 9 (one copy of the phase per plane count; BS_SBV 0 off).
+// BS_SBV_SET: the plane counts below the instance's that get a copy (1 seven, 2 eight); -1
+// (default): both on the one-chunk instances (same box, r5p: C2 4.66 -> 4.61 ms, C3 12.99 ->
+// 12.60), eight only on the multi-chunk ones (r5r: C4 11.33 -> 11.20; with both its 128-VGPR
+// build spilled 17 VGPRs and ran 11.74)
 #ifndef BS_SBV
-#define BS_SBV -1
+#define BS_SBV 1
+#endif
+#ifndef BS_SBV_SET
+#define BS_SBV_SET -1
 #endif
 
 template <int CTRL>
@@ -1300,10 +1305,10 @@ k_bs(BsArgs a) {
                     }
                 }
             };
-            constexpr bool SBV = BS_SBV < 0 ? (VPL == 1 && CPL == 1) : BS_SBV != 0;
-            if constexpr (SBV && SB >= 8) {
-                if (dwu * QMAX + QMAX <= 63) vbody(std::integral_constant<int, 7>{});
-                else if (SB == 9 && dwu * QMAX + QMAX <= 127) vbody(std::integral_constant<int, (SB == 9 ? 8 : SB)>{});
+            constexpr int SBSET = BS_SBV_SET >= 0 ? BS_SBV_SET : ((VPL == 1 && CPL == 1) ? 3 : 2);
+            if constexpr (BS_SBV && SB >= 8) {
+                if ((SBSET & 1) && dwu * QMAX + QMAX <= 63) vbody(std::integral_constant<int, 7>{});
+                else if ((SBSET & 2) && SB == 9 && dwu * QMAX + QMAX <= 127) vbody(std::integral_constant<int, (SB == 9 ? 8 : SB)>{});
                 else vbody(std::integral_constant<int, SB>{});
             } else {
                 vbody(std::integral_constant<int, SB>{});
