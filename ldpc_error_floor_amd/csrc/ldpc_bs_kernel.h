@@ -637,6 +637,10 @@ __device__ __forceinline__ void min2_bits(uint32_t (&m1)[4], uint32_t (&m2)[4], 
 #ifndef BS_SBV_SET
 #define BS_SBV_SET -1
 #endif
+// keep all DV C->V messages when BS_KEEP >= DV (A/B switch; 0: DV - 1, one read again)
+#ifndef BS_KEEP_DV
+#define BS_KEEP_DV 0
+#endif
 
 template <int CTRL>
 __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]) {
@@ -1199,7 +1203,7 @@ k_bs(BsArgs a) {
             // (at most DV - 1: 802.11n, DV = 4, keeps three and reads its fourth edge again,
             // 14.48 -> 14.41 ms same box (r3zh); wman and 5G BG2 keep BS_KEEP = 4 of 6 / 8)
             constexpr int KEEP0 = ((VPL > 1 || CPL > 1) && !UCN) ? BS_KEEP_MC : BS_KEEP;
-            constexpr int KEEP = KEEP0 < DV ? KEEP0 : DV - 1;
+            constexpr int KEEP = KEEP0 < DV ? KEEP0 : (BS_KEEP_DV ? DV : DV - 1);
             const int dwu = dw[u];
             // the rest at SBX planes of S: the fewest that hold 15 dw + 15 for the place's largest
             // degree dw (wave-uniform), BS_SBV
