@@ -637,9 +637,11 @@ __device__ __forceinline__ void min2_bits(uint32_t (&m1)[4], uint32_t (&m2)[4], 
 #ifndef BS_SBV_SET
 #define BS_SBV_SET -1
 #endif
-// keep all DV C->V messages when BS_KEEP >= DV (A/B switch; 0: DV - 1, one read again)
+// keep all DV C->V messages when BS_KEEP >= DV (0: DV - 1, one read again — 802.11n's choice
+// before the plane-count copies; with them the C3 build keeps all four at the same 69-75 VGPRs:
+// same box, r5s, 12.60 -> 12.40 ms)
 #ifndef BS_KEEP_DV
-#define BS_KEEP_DV 0
+#define BS_KEEP_DV 1
 #endif
 
 template <int CTRL>
@@ -1200,8 +1202,8 @@ k_bs(BsArgs a) {
             }
             // C->V of the first KEEP edges stay in registers for the V->C pass, the others are read
             // again (BS_KEEP: 4 measured best within the 64-register budget)
-            // (at most DV - 1: 802.11n, DV = 4, keeps three and reads its fourth edge again,
-            // 14.48 -> 14.41 ms same box (r3zh); wman and 5G BG2 keep BS_KEEP = 4 of 6 / 8)
+            // (802.11n, DV = 4: all four since round 5 (BS_KEEP_DV), three and its fourth read
+            // again before (14.48 -> 14.41 ms, r3zh); wman and 5G BG2 keep BS_KEEP = 4 of 6 / 8)
             constexpr int KEEP0 = ((VPL > 1 || CPL > 1) && !UCN) ? BS_KEEP_MC : BS_KEEP;
             constexpr int KEEP = KEEP0 < DV ? KEEP0 : (BS_KEEP_DV ? DV : DV - 1);
             const int dwu = dw[u];
