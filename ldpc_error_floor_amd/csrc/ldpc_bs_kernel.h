@@ -637,11 +637,11 @@ __device__ __forceinline__ void min2_bits(uint32_t (&m1)[4], uint32_t (&m2)[4], 
 #ifndef BS_SBV_SET
 #define BS_SBV_SET -1
 #endif
-// keep all DV C->V messages when BS_KEEP >= DV (0: DV - 1, one read again — 802.11n's choice
-// before the plane-count copies; with them the C3 build keeps all four at the same 69-75 VGPRs:
-// same box, r5s, 12.60 -> 12.40 ms)
+// instances whose variables have at most BS_KEEP_DV edges keep all of them (0: none — 802.11n's
+// choice before the plane-count copies, three of four and the fourth read again; with them the C3
+// build keeps all four at the same 69-75 VGPRs: same box, r5s, 12.60 -> 12.40 ms)
 #ifndef BS_KEEP_DV
-#define BS_KEEP_DV 1
+#define BS_KEEP_DV 4
 #endif
 
 template <int CTRL>
@@ -683,7 +683,8 @@ __device__ __forceinline__ void merge_lanes(uint32_t (&m1)[4], uint32_t (&m2)[4]
 // the V->C pass (the others are read from their slots again).  Measured per instance, same box,
 // 2 rounds (tools/bs_variant.sh -DBS_KEEP=k): C2 5.79 (0) / 5.70 (1) / 5.58 (2) / 5.56 (3) /
 // 5.55 (4) / 5.71 ms (6); C3 18.75 / 18.53 / 18.25 / 17.80 / 17.76 / 17.75; C4 18.15 / 17.97 /
-// 17.81 / 17.76 / 17.67 / 17.62 ms.
+// 17.81 / 17.76 / 17.67 / 17.62 ms (round 3; round 5 with the plane-count copies: C2 takes 3,
+// C3 all four, profiles/r5/ab_sbv.log).
 // the channel's 4 magnitude planes of each variable kept in LDS (one ds_read_b128 per variable
 // and iteration) instead of 4 registers held through the whole decode (A/B switch)
 #ifndef BS_CH_LDS
@@ -868,7 +869,10 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 #define BS_KEEP_MC 7
 #endif
 #ifndef BS_KEEP
-#define BS_KEEP 4
+#define BS_KEEP 3       // (wman: 3 against 4, same box r5u, 4.63 -> 4.59 ms over five pairs)
+#endif
+#ifndef BS_KEEP_MCU
+#define BS_KEEP_MCU 4
 #endif
 // variable places without a chunk skipped (A/B switch: -DBS_VSKIP=0 runs their table work)
 #ifndef BS_VSKIP
@@ -1201,11 +1205,11 @@ k_bs(BsArgs a) {
                 }
             }
             // C->V of the first KEEP edges stay in registers for the V->C pass, the others are read
-            // again (BS_KEEP: 4 measured best within the 64-register budget)
-            // (802.11n, DV = 4: all four since round 5 (BS_KEEP_DV), three and its fourth read
-            // again before (14.48 -> 14.41 ms, r3zh); wman and 5G BG2 keep BS_KEEP = 4 of 6 / 8)
-            constexpr int KEEP0 = ((VPL > 1 || CPL > 1) && !UCN) ? BS_KEEP_MC : BS_KEEP;
-            constexpr int KEEP = KEEP0 < DV ? KEEP0 : (BS_KEEP_DV ? DV : DV - 1);
+            // again: wman 3 of 6 (BS_KEEP), 802.11n all four (BS_KEEP_DV; three and the fourth
+            // read again before round 5, 14.48 -> 14.41 ms, r3zh), 5G BG2 7 of 8 (BS_KEEP_MC), 4
+            // with UCN (BS_KEEP_MCU)
+            constexpr int KEEP0 = (VPL > 1 || CPL > 1) ? (UCN ? BS_KEEP_MCU : BS_KEEP_MC) : BS_KEEP;
+            constexpr int KEEP = DV <= BS_KEEP_DV ? DV : (KEEP0 < DV ? KEEP0 : DV - 1);
             const int dwu = dw[u];
             // the rest at SBX planes of S: the fewest that hold 15 dw + 15 for the place's largest
             // degree dw (wave-uniform), BS_SBV
