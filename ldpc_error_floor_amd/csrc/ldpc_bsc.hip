@@ -31,6 +31,9 @@ namespace bs {
 #ifndef BSC_SBV
 #define BSC_SBV 1
 #endif
+#ifndef BSC_SBV_SET
+#define BSC_SBV_SET 3   // the lower plane counts that get a copy: 1 seven, 2 eight (A/B)
+#endif
 
 // instances: D = check-degree bound, DVH / DVL = variable-degree bound of a lane's first /
 // other variables, LPC lanes per check, VPL variables and CPL check chunks per lane
@@ -338,8 +341,9 @@ k_bsc(BscArgs a) {
             if constexpr (BSC_SBV) {
                 auto dispatch = [&](auto smax) __attribute__((always_inline)) {
                     constexpr int SM = decltype(smax)::value;
-                    if (dwu * QMAX + QMAX <= 63) vbody(std::integral_constant<int, 7>{});
-                    else if (SM == 9 && dwu * QMAX + QMAX <= 127) vbody(std::integral_constant<int, (SM == 9 ? 8 : SM)>{});
+                    if ((BSC_SBV_SET & 1) && dwu * QMAX + QMAX <= 63) vbody(std::integral_constant<int, 7>{});
+                    else if ((BSC_SBV_SET & 2) && SM == 9 && dwu * QMAX + QMAX <= 127)
+                        vbody(std::integral_constant<int, (SM == 9 ? 8 : SM)>{});
                     else vbody(std::integral_constant<int, SM>{});
                 };
                 constexpr int SBL = (DVL * QMAX + QMAX <= 127) ? 8 : 9;    // places past the first
