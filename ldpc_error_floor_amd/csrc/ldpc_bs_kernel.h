@@ -613,14 +613,15 @@ __device__ __forceinline__ void min2_bits(uint32_t (&m1)[4], uint32_t (&m2)[4], 
 // construction: ceil(degree / lanes per check) of its widest check) may mark every other count
 // unreachable (U), and zero the tie words of the positions past it (Z).  Without U the compiler
 // keeps the search's inputs and outputs alive through the empty cases and copies them at the join
-// (C4, static: 39 v_mov per chunk, 2.47 -> 2.28 VALU per pack-edge-iteration) — yet the bsl C4
-// build ran slower with it (same box, r5o: 11.41-11.49 ms against 11.29-11.32 for U, Z, U+Z),
-// while bsc's C5 gains (48.4 -> 47.9 ms): U on for bsc (BSC_MIN2_U), off for bsl
+// (C4, static: 39 v_mov per chunk, 2.47 -> 2.28 VALU per pack-edge-iteration).  bsc's C5 gains
+// (48.4 -> 47.9 ms, r5o); the bsl C4 build ran slower with U+Z before the plane-count copies
+// (r5o: 11.48 against 11.30 ms) and equal after them (r5w: 11.17-11.22 against 11.21-11.22), for
+// fewer instructions: on for both
 #ifndef BS_MIN2_U
-#define BS_MIN2_U 0
+#define BS_MIN2_U 1
 #endif
 #ifndef BS_MIN2_Z
-#define BS_MIN2_Z 0
+#define BS_MIN2_Z 1
 #endif
 #ifndef BSC_MIN2_U
 #define BSC_MIN2_U 1
