@@ -1224,7 +1224,7 @@ k_bs(BsArgs a) {
 #pragma unroll
                     for (int f = 0; f < DV; ++f) {
                         if (f < dwu) {
-                            PH("vn_sum", (last ? 100 : 0) + 10 * u + f);
+                            PH("vn_sum", 1000 * (SB - 6) + (last ? 100 : 0) + 10 * u + f);
                             uint32_t M[4], n, b[4];
                             read_slot(n, M, vaddr(f));
 #pragma unroll
@@ -1238,7 +1238,8 @@ k_bs(BsArgs a) {
                             }
                         }
                     }
-                    if constexpr (SB == 8) PH8("vn_app", (last ? 100 : 0) + u, S, (S + 4));
+                    if constexpr (SB == 8) PH8("vn_app", 1000 * (SB - 6) + (last ? 100 : 0) + u, S, (S + 4));
+                    else PH("vn_app", 1000 * (SB - 6) + (last ? 100 : 0) + u);
                     // APP_t = Q(ch) + S: the sign (hard decision) from the carry chain alone, the full
                     // sum only in the last iteration (APP > 0 for the loss counter)
                     uint32_t hd, nz = 0u;
@@ -1273,7 +1274,8 @@ k_bs(BsArgs a) {
                     }
                 }
                 if (last) return;
-                if constexpr (SB == 8) PH8("vn_tv", (last ? 100 : 0) + u, S, (S + 4));
+                if constexpr (SB == 8) PH8("vn_tv", 1000 * (SB - 6) + (last ? 100 : 0) + u, S, (S + 4));
+                else PH("vn_tv", 1000 * (SB - 6) + (last ? 100 : 0) + u);
                 // Tv = clamp(Q(beta ch) + S): the table gives |Q(beta ch)|, the channel the sign
                 uint32_t lb[4];
 #pragma unroll
@@ -1297,7 +1299,7 @@ k_bs(BsArgs a) {
                     for (int f = 0; f < DV; ++f) {
                         if (f < dwu) {
                             if (ABL(4)) continue;
-                            PH("vn_vc", (last ? 100 : 0) + 10 * u + f);
+                            PH("vn_vc", 1000 * (SB - 6) + (last ? 100 : 0) + 10 * u + f);
                             uint32_t x[7], X[4], n, b[4];
                             if (f < KEEP) {
                                 n = mn[f < KEEP ? f : 0];

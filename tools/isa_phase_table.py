@@ -251,6 +251,8 @@ def main():
                     "weights come from the host's dealing of the chunks to (wave, place) slots")
     ap.add_argument("--vchunks", help="--mc: each variable chunk's largest degree, in chunk order")
     ap.add_argument("--cchunks", help="--mc: each check chunk's real edge positions per lane (gm)")
+    ap.add_argument("--sbv", help="MAX,SET: the instance's planes of S and its BS_SBV_SET (the "
+                    "plane-count copies' markers carry 1000 (planes - 6))")
     ap.add_argument("--dump", help="print the static VALU mnemonics of these phases (comma list)")
     ap.add_argument("--json")
     a = ap.parse_args()
@@ -268,11 +270,40 @@ def main():
         cplaces = [[cg[cs[w * cpl + c]] for w in range(nw) if cs[w * cpl + c] >= 0] for c in range(cpl)]
         mc = (nw, places, cplaces)
 
+    def planes(d):        # the variable-phase copy a place of largest degree d runs (BS_SBV)
+        if not a.sbv:
+            return None
+        smax, sset = (int(x) for x in a.sbv.split(","))
+        if (sset & 1) and 15 * d + 15 <= 63:
+            return 7
+        if (sset & 2) and smax == 9 and 15 * d + 15 <= 127:
+            return 8
+        return smax
+
     def weight(ph):
         base, k = ph.rsplit(".", 1)
         k = int(k, 0)
+        sb = 6 + k // 1000 if k >= 1000 else None    # the plane-count copy of the variable phase
+        k %= 1000
         last = k >= 100
         k %= 100
+        w = weight1(base, k, last)
+        if sb is None or not a.sbv:
+            return w
+        # only the places that run this copy
+        if mc:
+            nw, places, cplaces = mc
+            u = k // 10 if base in ("vn_sum", "vn_vc") else k
+            f = k % 10 if base in ("vn_sum", "vn_vc") else -1
+            n = sum(1 for d in places[u] if planes(d) == sb and d > f)
+        else:
+            f = k if base in ("vn_sum", "vn_vc") else -1
+            n = sum(1 for d in dw if planes(d) == sb and d > f)
+        if base in alt:
+            n *= alt[base]
+        return w[0], w[1], n
+
+    def weight1(base, k, last):
         if mc:
             nw, places, cplaces = mc
             if base == "ck_mink":
