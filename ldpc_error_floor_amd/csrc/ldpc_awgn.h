@@ -117,6 +117,9 @@ __device__ __forceinline__ void awgn_pair(const AwgnParams& a, int64_t b, int pr
 // the low word decides (awgn_tie_scan), drawn only then -- kept out of this loop so that the
 // compiler cannot hoist the second Philox in front of it.
 constexpr int AWGN_KB = 10;                 // bucket bits (1024 buckets, 2 KB of LDS)
+#ifndef AWGN_FAST
+#define AWGN_FAST 1     // awgn_levels4b's branch-free common case (A/B switch)
+#endif
 static_assert(AWGN_TAB_W == 2 * (1 << AWGN_KB) + 2 * AWGN_NB_MAX, "awgn_gen_table layout");
 template <typename P16, typename P32>
 __device__ __forceinline__ int awgn_level_hi(P16 bucket, P32 thi, uint32_t u, bool& tie) {
@@ -194,7 +197,7 @@ __device__ __forceinline__ void awgn_levels4(const AwgnParams& a, P16 bucket, P3
 
 // ---- the channel kernels' form: each bucket carries its first threshold -----------------------
 // (ldpc_channel.hip: 8 KB of LDS per workgroup).  A bucket entry is {base | count << 8, the high
-// word of threshold `base` (0 if count = 0)}: one ds_read_b64 decides U's level whenever its
+// word of threshold `base` (2^32 - 1 if count = 0)}: one ds_read_b64 decides U's level whenever its
 // bucket holds at most one threshold (all but the few buckets where the CDF climbs by more than
 // one level within 2^-10: the far tails); the others scan on from there.  Same levels as
 // awgn_levels4.
@@ -221,8 +224,8 @@ __device__ __forceinline__ void awgn_bucket_fill2(const AwgnParams& a, uint2* bu
             }
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (b0 + k * n < NB) bucket[b0 + k * n] = make_uint2(base[k] | cnt[k] << 8, first[k]);
+        for (int k = 0; k < 4; ++k)     // (an empty bucket's first: 2^32 - 1, above every U's high word but one)
+            if (b0 + k * n < NB) bucket[b0 + k * n] = make_uint2(base[k] | cnt[k] << 8, cnt[k] ? first[k] : ~0u);
     }
 }
 
@@ -231,17 +234,30 @@ __device__ __forceinline__ void awgn_bucket_fill2(const AwgnParams& a, uint2* bu
 // first threshold), and only then the rare scans: buckets holding more thresholds, high-word ties
 // (A: anything with the key k0, k1 and the boundary count nb: AwgnParams, or the bit-sliced
 // kernels' in-prologue generator; PB / P32: the tables in LDS or global memory)
+// (awgn_levels4b_c: the levels from the high words c = Philox(v, gq, 'LDQ4') already drawn)
 template <typename A, typename PB, typename P32>
-__device__ __forceinline__ void awgn_levels4b(const A& a, PB bucket, P32 thi, P32 tlo,
-                                              uint32_t v, uint64_t gq, int (&lv)[4]) {
-    uint32_t c[4] = {v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_Q};
-    Philox::gen(c, a.k0, a.k1);
+__device__ __forceinline__ void awgn_levels4b_c(const A& a, PB bucket, P32 thi, P32 tlo, uint32_t v,
+                                                uint64_t gq, const uint32_t (&c)[4], int (&lv)[4]) {
     uint2 e[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const auto ej = bucket[c[j] >> (32 - AWGN_KB)];
         e[j] = make_uint2(ej.x, ej.y);
     }
+#if AWGN_FAST
+    // the common case, branch-free: level = base + [U > first] (an empty bucket's first is
+    // 2^32 - 1, so nothing exceeds it).  A bucket holding two or more thresholds (count field
+    // >= 2: the far tails) or a high word equal to a bucket's first threshold (a tie, or U = 2^32
+    // - 1 in an empty bucket) sends the quad through the exact path below, which gives the same
+    // levels in every other case
+    {
+        const uint32_t ex = e[0].x | e[1].x | e[2].x | e[3].x;
+        const uint32_t dm = min(min(c[0] ^ e[0].y, c[1] ^ e[1].y), min(c[2] ^ e[2].y, c[3] ^ e[3].y));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lv[j] = (int)(e[j].x & 0xFFu) + (c[j] > e[j].y ? 1 : 0);
+        if (ex < 2u << 8 && dm != 0u) return;
+    }
+#endif
     uint32_t ties = 0u, more = 0u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -274,6 +290,13 @@ __device__ __forceinline__ void awgn_levels4b(const A& a, PB bucket, P32 thi, P3
         for (int j = 0; j < 4; ++j)
             if ((ties >> j) & 1u) lv[j] = awgn_tie_scan(a.nb, thi, tlo, c[j], r[j], lv[j]);
     }
+}
+template <typename A, typename PB, typename P32>
+__device__ __forceinline__ void awgn_levels4b(const A& a, PB bucket, P32 thi, P32 tlo,
+                                              uint32_t v, uint64_t gq, int (&lv)[4]) {
+    uint32_t c[4] = {v, (uint32_t)gq, (uint32_t)(gq >> 32), AWGN_TAG_Q};
+    Philox::gen(c, a.k0, a.k1);
+    awgn_levels4b_c(a, bucket, thi, tlo, v, gq, c, lv);
 }
 
 // what a QMS element at 1-based bit `bit` is: 0 random, 1 punctured (LLR 0), 2 shortened (-clip)

@@ -101,7 +101,7 @@ void awgn_gen_table(const AwgnParams& a, uint32_t* out) {
             }
         }
         out[2 * b] = base | cnt << 8;
-        out[2 * b + 1] = first;
+        out[2 * b + 1] = cnt ? first : ~0u;     // (awgn_bucket_fill2's entries)
     }
     for (int i = 0; i < AWGN_NB_MAX; ++i) {
         out[2 * NB + i] = i < a.nb ? a.thr_hi[i] : 0u;
