@@ -1444,7 +1444,11 @@ k_bs(BsArgs a) {
     // wave priorities (BS_PRIO: 1 the younger half of the workgroup at priority 1 for the whole
     // decode; 2 the check phase at priority 1, the variable phase at 0; 3 the reverse; 4 the
     // check phase at 2, the variable phase at 1 on the waves whose first place has degree >= DV - 1)
-    constexpr int PRIO = BS_PRIO >= 0 ? BS_PRIO : ((VPL == 1 && CPL == 1) ? 2 : 0);
+    // (default: 4 on the one-chunk instances with DV >= 6 — wman, whose three degree-6 waves hold
+    // twice the variable work of the other six: same box, r5aa, 4.59 -> 4.52 ms — 2 on the other
+    // one-chunk instances — 802.11n, where nearly every wave is that heavy: 12.37 against 12.70 —
+    // and 0 on the multi-chunk ones)
+    constexpr int PRIO = BS_PRIO >= 0 ? BS_PRIO : ((VPL == 1 && CPL == 1) ? (DV >= 6 ? 4 : 2) : 0);
     if (PRIO == 1 && wave >= (nwv >> 1)) __builtin_amdgcn_s_setprio(1);
     for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
         PH("top", 0);
