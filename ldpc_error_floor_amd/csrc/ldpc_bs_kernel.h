@@ -1443,13 +1443,40 @@ k_bs(BsArgs a) {
 
     // wave priorities (BS_PRIO: 1 the younger half of the workgroup at priority 1 for the whole
     // decode; 2 the check phase at priority 1, the variable phase at 0; 3 the reverse; 4 the
-    // check phase at 2, the variable phase at 1 on the waves whose first place has degree >= DV - 1)
+    // check phase at 2, the variable phase at 1 on the waves whose first place has degree >= DV - 1
+    // and 0 on the others; 6 as 4 with the check phase at 1; 8 as 6 with those waves at 2; 9 the
+    // waves with more than the mean work of each phase at 1)
     // (default: 4 on the one-chunk instances with DV >= 6 — wman, whose three degree-6 waves hold
     // twice the variable work of the other six: same box, r5aa, 4.59 -> 4.52 ms — 2 on the other
     // one-chunk instances — 802.11n, where nearly every wave is that heavy: 12.37 against 12.70 —
     // and 0 on the multi-chunk ones)
     constexpr int PRIO = BS_PRIO >= 0 ? BS_PRIO : ((VPL == 1 && CPL == 1) ? (DV >= 6 ? 4 : 2) : 0);
     if (PRIO == 1 && wave >= (nwv >> 1)) __builtin_amdgcn_s_setprio(1);
+    // PRIO 9: in each phase the waves with more than the mean work at priority 1 (variable phase:
+    // 3 + the degree of each chunk the wave holds, from the dealing table; check phase: its chunks)
+    bool heavy_v = false, heavy_c = false;
+    if constexpr (PRIO == 9) {
+        int own = 0, sum = 0, cown = 0, csum = 0;
+        for (int w = 0; w < nwv; ++w) {      // (wave-uniform: scalar loads)
+            int cw = 0, cc = 0;
+#pragma unroll
+            for (int u = 0; u < VPL; ++u) {
+                const int d = __builtin_amdgcn_readfirstlane(a.vn_wdeg[3 * (u * nwv + w)]);
+                cw += d >= 0 ? 3 + d : 0;
+            }
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+                cc += (CPL == 1 ? w * 64 < a.cn_lanes : __builtin_amdgcn_readfirstlane(a.cn_chunk[w * CPL + c]) >= 0) ? 1 : 0;
+            sum += cw;
+            csum += cc;
+            if (w == wave) {
+                own = cw;
+                cown = cc;
+            }
+        }
+        heavy_v = own * nwv > sum;
+        heavy_c = cown * nwv > csum;
+    }
     for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
         PH("top", 0);
         if ((BS_TIDFREE ? wave == 0 : tid == 0) && t > 0) {   // fold iteration t-1's frame flags
@@ -1513,6 +1540,11 @@ k_bs(BsArgs a) {
         if (PRIO == 2) __builtin_amdgcn_s_setprio(1);
         if (PRIO == 3) __builtin_amdgcn_s_setprio(0);
         if (PRIO == 4) __builtin_amdgcn_s_setprio(2);
+        if (PRIO == 6 || PRIO == 8) __builtin_amdgcn_s_setprio(1);
+        if (PRIO == 9) {
+            if (heavy_c) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const bool active = (CPL == 1) ? (BS_TIDFREE ? wave * 64 < a.cn_lanes : tid < a.cn_lanes)
@@ -1793,8 +1825,12 @@ k_bs(BsArgs a) {
         // ======== variable nodes ================================================================
         if (PRIO == 2) __builtin_amdgcn_s_setprio(0);
         if (PRIO == 3) __builtin_amdgcn_s_setprio(1);
-        if (PRIO == 4) {                     // the waves of the heaviest variables first
-            if (dw[0] >= DV - 1) __builtin_amdgcn_s_setprio(1);
+        if (PRIO == 9) {
+            if (heavy_v) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+        if (PRIO == 4 || PRIO == 6 || PRIO == 8) {   // the waves of the heaviest variables first
+            if (dw[0] >= DV - 1) __builtin_amdgcn_s_setprio(PRIO == 8 ? 2 : 1);
             else __builtin_amdgcn_s_setprio(0);
         }
         const uint32_t bslice = a.off_blut + (uint32_t)(nx * BL * 4);
