@@ -28,6 +28,20 @@ boundaries, so the marked build's totals are compared with the product build's (
 the split is the marked build's, the totals of both are printed.  The last iteration's copy of
 the variable phase (markers K >= 100) is reported separately; the table is one non-last
 iteration, i.e. per pack-edge-iteration for T >> 1.
+
+  --sbv MAX,SET   the plane-count copies of the variable phase (BS_SBV: markers carry
+                  1000 (planes - 6)) weighted by the places that run each: MAX the instance's
+                  planes of S, SET its BS_SBV_SET (1 seven, 2 eight)
+  --mc NW,VPL,CPL --vchunks D,... --cchunks G,...
+                  multi-chunk instances: the host's dealing of the variable chunks (largest
+                  degree each) and check chunks (real positions each) to (wave, place) slots is
+                  replayed (deal_chunks), and each marker is weighted by the slots that run it
+                  (check markers K = 16 c + position, variable markers K = 10 u + edge)
+  --dump P,...    the static VALU mnemonics of these phases (where the forms come from)
+
+    python3 tools/isa_phase_table.py c4.s Li4ELb0ELi1024ELb0E --dw 1 --cwaves 1 --edges 4288 \
+        --mc 16,2,2 --vchunks 8,7,7,5,5,4,4,4,3,3,3,3,3,2,1,1,1,1,1,1 \
+        --cchunks 4,4,5,5,4,4,5,5,2,2,3,3,3,3,3,3,2,2,3,3 --sbv 9,2
 """
 import argparse
 import json
