@@ -69,8 +69,8 @@ def test_c5_floor_is_degree1_saturation_over_ten_decades():
     T = 50): BG1's 432 degree-1 bits (columns 26-31) get at most Q(0.75 x 7.5) = 5.5 from their
     check, so a channel LLR that rounds to >= 5.5 (raw >= 5.25) leaves APP >= 0, a frame error.
     FER = 1 - (1 - Q(5.25 sigma / 2 + 1 / sigma))^432 predicts every committed C5 sweep point
-    (profiles/r2/sweep_c5*, 4.2e6 to 1.07e10 codewords per point, 3 to 15 dB, FER 0.22 down to
-    1.9e-9) within Poisson noise."""
+    (profiles/r2/sweep_c5*, profiles/r5/sweep_c5: 4.2e6 to 1.7e10 codewords per point, 3 to 15
+    dB, FER 0.22 down to 1.7e-10) within Poisson noise."""
     import sys
     from scipy.special import ndtr
     sys.path.insert(0, ROOT)
@@ -83,12 +83,13 @@ def test_c5_floor_is_degree1_saturation_over_ten_decades():
     assert _q5(np.float32(0.75) * np.float32(7.5)) == 5.5
     n_bits = len(cols) * 72
     pts = []
-    for f in ("sweep_c5/sweep_c5.json", "sweep_c5_deep/sweep_c5_14.5dB.json",
-              "sweep_c5_deep/sweep_c5_15dB.json"):
-        with open(os.path.join(ROOT, "profiles", "r2", f)) as fh:
+    for f in ("r2/sweep_c5/sweep_c5.json", "r2/sweep_c5_deep/sweep_c5_14.5dB.json",
+              "r2/sweep_c5_deep/sweep_c5_15dB.json",
+              "r5/sweep_c5/sweep_c5.json"):       # (round 5: 1.7e10 codewords at 15 dB, 3 frames)
+        with open(os.path.join(ROOT, "profiles", f)) as fh:
             d = json.load(fh)
-        pts += d["scan"] + d["deep"]
-    assert len(pts) >= 15
+        pts += d.get("scan", []) + d["deep"]
+    assert len(pts) >= 16
     for r in pts:
         s, n = r["sigma"], r["codewords"]
         p_bit = ndtr(-(5.25 * s / 2 + 1 / s))
