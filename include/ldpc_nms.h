@@ -160,6 +160,15 @@ int ldpc_decode_awgn(ldpc_ctx* ctx, int64_t B, const ldpc_decode_params* params,
                      const ldpc_channel_params* channel, const ldpc_decode_outputs* outputs,
                      void* stream);
 
+/* Whether ldpc_decode_awgn with these parameters generates the channel inside the decoding
+   kernel (the v5 prologue for APP exports, the bit-sliced kernels' prologue for counters-only QMS
+   decodes): 1, else 0 (the channel kernel writes float LLRs to the context's buffer first), or a
+   negative status.  has_short: the channel has shortened bits; app: an APP export is asked for.
+   The decision ldpc_decode_awgn itself takes; a decode it served in-kernel also reports its
+   kernel through ldpc_ctx_last_kernel with the suffix "+gen". */
+int ldpc_awgn_in_kernel(const ldpc_ctx* ctx, const ldpc_decode_params* params, int32_t has_short,
+                        int32_t app);
+
 /* Uncorrected-frame collection for the on-device sweep (replaces the host selection in
    compute_results -> write_uncor_file, Print_Functions.py:155-156 and :120-126).
    Writes the indices b < B with (frame_flags[b] & mask) == want into idx_dev[0..cap) (order

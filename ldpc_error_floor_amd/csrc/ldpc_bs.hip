@@ -783,7 +783,33 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // -DBS_DIAG builds
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
     static const auto kLaunch = launch_table(std::make_integer_sequence<int, kBsNInst>{});
-    return kLaunch[p.inst](a, nblocks, p.nw, p.lds, s, b.q8 != nullptr);
+    // (A/B: LDPC_BS_LDS_MIN=bytes requests at least that much dynamic LDS per workgroup, fewer
+    // workgroups per CU -- the occupancy experiment; the kernel uses only its own layout)
+    static const size_t lds_min = [] { const char* e = getenv("LDPC_BS_LDS_MIN"); return e ? (size_t)atol(e) : 0; }();
+    const size_t lds = std::min(std::max(p.lds, lds_min), (size_t)BS_LDS_MAX);
+#ifdef BS_STAMP
+    // diagnostic build: per-wave phase clocks of this decode, printed to stderr
+    static unsigned long long* dst = nullptr;
+    if (!dst && hipMalloc(reinterpret_cast<void**>(&dst), 128 * 8) != hipSuccess) return LDPC_ERR_OOM;
+    if (hipMemsetAsync(dst, 0, 128 * 8, s) != hipSuccess) return LDPC_ERR_HIP;
+    a.stamps = dst;
+    st = kLaunch[p.inst](a, nblocks, p.nw, lds, s, b.q8 != nullptr);
+    unsigned long long hst[128];
+    if (st != LDPC_OK || hipMemcpyAsync(hst, dst, sizeof(hst), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return st != LDPC_OK ? st : LDPC_ERR_HIP;
+    fprintf(stderr, "bs_stamp inst %d T %d: per pack, shader clocks [check, check-barrier, var, var-barrier, prologue, epilogue]\n",
+            p.inst, b.T);
+    for (int w = 0; w < p.nw && w < 16; ++w) {
+        const double n = (double)(hst[8 * w + 6] ? hst[8 * w + 6] : 1);
+        fprintf(stderr, "  wave %2d:", w);
+        for (int i = 0; i < 6; ++i) fprintf(stderr, " %9.0f", hst[8 * w + i] / n);
+        fprintf(stderr, "\n");
+    }
+    return st;
+#else
+    return kLaunch[p.inst](a, nblocks, p.nw, lds, s, b.q8 != nullptr);
+#endif
 }
 
 }  // namespace ldpc
@@ -834,6 +860,9 @@ static int bs_bounds_check(const DevGraph& g, const BsPlan& p, const BsHostTable
     const bool SKIPM = CPL > 1;
     const bool GBL = BS_GBLDS && CPL == 1 && !BS_CH_LDS;
     const bool HDL = BS_HDLDS && UCN && CPL == 1;
+    // (ALDS: GW words per lane, the slot base and then the packed slot addresses)
+    const int HWA = (EPL + 1) / 2;
+    const int GW = (GBL && k.PK && BS_ALDS) ? ((1 + HWA) | 1) : 1;
     // the allocations
     r.in("lds size", lds, (long long)BS_LDS_MAX + 1);
     if ((long long)t.vn.size() != (long long)VPL * NT * VNW) r.fail("vn_tab size", (long long)t.vn.size(), (long long)VPL * NT * VNW);
@@ -842,6 +871,11 @@ static int bs_bounds_check(const DevGraph& g, const BsPlan& p, const BsHostTable
     r.lds("BLUT", p.off_blut, 4 * 2 * BL, 0, lds);
     r.lds("PAD+ZERO", p.off_pad, 2 * SLOT_B, p.off_slots, p.off_red);
     if (UCN) r.lds("HD", 0, 4LL * (nv + 1), 0, p.off_slots);
+    // the in-prologue channel's sampler tables (Q8 builds, gen.lds = off_slots): inside the slot
+    // region, which the kernel writes only after the prologue, and clear of PAD / ZERO / RED /
+    // the tables the prologue writes -- whenever bs_q8_ok lets the Q8 build run on this plan
+    if ((size_t)(p.off_pad - p.off_slots) >= sizeof(uint32_t) * AWGN_TAB_W)
+        r.lds("channel tables", p.off_slots, 4LL * AWGN_TAB_W, p.off_slots, p.off_pad);
     // ---- variable phase: per (u, lane)
     for (int u = 0; u < VPL; ++u)
         for (int w = 0; w < nwv; ++w) {
@@ -850,6 +884,13 @@ static int bs_bounds_check(const DevGraph& g, const BsPlan& p, const BsHostTable
             if (wi + 2 >= (long long)t.wdeg.size()) continue;
             const int dw = t.wdeg[(size_t)wi], pcol = t.wdeg[(size_t)wi + 2];
             if (pcol >= 0) r.in("btid column", pcol, h.N);
+            // channel-table ids: the variable phase of iteration t reads btid[(t + 1) N + col]
+            // for t + 1 < T (col = 0 with one column table), and beta_tid holds [T_w][N] rows,
+            // T <= T_w by host::check_decode
+            if (dw >= 0 && T > 1) {
+                const long long col = p.bcols == 1 ? 0 : pcol;
+                if (col >= 0) r.in("btid", (long long)(T - 1) * h.N + col, (long long)T * h.N);
+            }
             for (int l = 0; l < 64; ++l) {
                 const long long ti = ((long long)u * NT + 64LL * w + l) * VNW;
                 r.in("vn_tab", ti + VNA, (long long)t.vn.size());
@@ -897,7 +938,7 @@ static int bs_bounds_check(const DevGraph& g, const BsPlan& p, const BsHostTable
                     if (ucn && gchunk >= 0 && guard)
                         for (int pp = 0; pp < HDW; ++pp) r.in("cn_hd", (long long)ql * HDW + pp, (long long)t.chd.size());
                 }
-                if (GBL) r.lds("per-lane word", p.off_ch + 4LL * (64 * w + l), 4, p.off_ch, lds);
+                if (GBL) r.lds("per-lane words", p.off_ch + 4LL * GW * (64 * w + l), 4LL * GW, p.off_ch, lds);
                 if (HDL)
                     for (int pp = 0; pp < HDW; ++pp) r.lds("HD addresses", p.off_hdl + 4LL * (pp * NT + 64 * w + l), 4, p.off_hdl, lds);
                 if (!active) continue;
@@ -922,7 +963,6 @@ static int bs_bounds_check(const DevGraph& g, const BsPlan& p, const BsHostTable
                 r.lds("alpha table (odd t, alpha')", last, 16, p.off_alut, p.off_alut + 4 * 2 * AL);
             }
         }
-    // channel-table ids: a.btid[(t + 1) btid_n + col], t + 1 < T, col < N (beta_tid is [T_w][N])
     return r.violations;
 }
 }  // namespace bs
@@ -970,6 +1010,18 @@ extern "C" int ldpc_debug_bs_bounds(const int32_t* proto, int32_t M, int32_t N, 
             }
             *violations += r.violations;
         }
+    // the compressed kernel (bsc, no UCN): its plan with and without the beta = 1 build's
+    // mixed-lane instances
+    for (int b1 = 0; b1 < 2; ++b1) {
+        if (b1 && !beta_uniform) continue;
+        g.w_beta_one = b1;
+        BoundsReport r;
+        const int n = bsc_debug_bounds(g, mode, clip, T, r.violations, r.first);
+        if (n <= 0) continue;
+        ++checked;
+        if (r.violations && first.empty()) first = std::string(b1 ? "bsc beta=1: " : "bsc: ") + r.first;
+        *violations += r.violations;
+    }
     if (msg && msg_len > 0) {
         std::strncpy(msg, first.c_str(), (size_t)msg_len - 1);
         msg[msg_len - 1] = 0;

@@ -134,6 +134,9 @@ struct BsArgs {
                                  // hard-decision addresses, [HDW][lane] words
     uint32_t pad_;
     BsGen gen;                   // Q8 builds: the in-prologue channel
+    unsigned long long* stamps;  // -DBS_STAMP builds only: [16 waves][8] shader-clock sums per
+                                 // phase (0 check, 1 check barrier, 2 variable, 3 variable barrier,
+                                 // 4 prologue, 5 epilogue, 6 packs), timing diagnostics
 };
 
 // ---- bit-plane arithmetic ---------------------------------------------------------------------
@@ -938,6 +941,20 @@ k_bs(BsArgs a) {
     constexpr bool RR = BS_REREAD && EPL >= 6;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();          // slots are LDS-absolute
+#ifdef BS_STAMP
+    // per-wave phase times (wave-uniform, s_memtime shader clocks): where a wave's time goes,
+    // barrier waits included (diagnostic builds only)
+    uint64_t sacc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t sts = __builtin_amdgcn_s_memtime();
+#define BS_ST(i)                                                                                   \
+    do {                                                                                           \
+        const uint64_t tn_ = __builtin_amdgcn_s_memtime();                                         \
+        sacc[i] += tn_ - sts;                                                                      \
+        sts = tn_;                                                                                 \
+    } while (0)
+#else
+#define BS_ST(i) ((void)0)
+#endif
     const int tid = threadIdx.x;
     const int NT = blockDim.x;
     const int lane = tid & 63;
@@ -1477,6 +1494,7 @@ k_bs(BsArgs a) {
         heavy_v = own * nwv > sum;
         heavy_c = cown * nwv > csum;
     }
+    BS_ST(4);
     for (int t = 0; t < (ABL(16) ? 0 : a.T); ++t) {
         PH("top", 0);
         if ((BS_TIDFREE ? wave == 0 : tid == 0) && t > 0) {   // fold iteration t-1's frame flags
@@ -1821,7 +1839,9 @@ k_bs(BsArgs a) {
                 }
             }
         }
+        BS_ST(0);
         __syncthreads();
+        BS_ST(1);
         // ======== variable nodes ================================================================
         if (PRIO == 2) __builtin_amdgcn_s_setprio(0);
         if (PRIO == 3) __builtin_amdgcn_s_setprio(1);
@@ -1836,7 +1856,9 @@ k_bs(BsArgs a) {
         const uint32_t bslice = a.off_blut + (uint32_t)(nx * BL * 4);
         if (t == a.T - 1) vn_phase(false, true, bslice, t + 1);
         else vn_phase(false, false, bslice, t + 1);
+        BS_ST(2);
         __syncthreads();
+        BS_ST(3);
     }
     if (tid == 0) {
         const uint32_t wl = RED[0] & valid;
@@ -1863,6 +1885,15 @@ k_bs(BsArgs a) {
             for (int t = tid; t < a.T; t += NT)
                 a.iter_wrong[(size_t)t * (size_t)((a.B + 31) >> 5) + blockIdx.x] = RED[16 + t] & valid;
     }
+#ifdef BS_STAMP
+    BS_ST(5);
+    if (a.stamps && lane == 0 && wave < 16) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) atomicAdd(a.stamps + 8 * wave + i, (unsigned long long)sacc[i]);
+        atomicAdd(a.stamps + 8 * wave + 6, 1ull);
+    }
+#endif
+#undef BS_ST
 }
 
 template <int I, bool XP, bool Q8>

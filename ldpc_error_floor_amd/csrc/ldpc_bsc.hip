@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <type_traits>
 #include <vector>
 
@@ -967,6 +968,46 @@ static int bsc_launch(const BscArgs& a, int nblocks, int nw, size_t lds, hipStre
 }  // namespace bs
 
 using namespace bs;
+
+// Host-side bounds check of the bsc plan for this graph (test infrastructure, through
+// ldpc_debug_bs_bounds): the in-prologue channel's tables at LDS byte 0 end inside the SGN
+// region they borrow, and every check chunk's count of real edge positions -- the kernel's
+// wave_or / popc over its lanes, restated -- is in 1 .. EPL, the range the min2 switch covers
+// (its other cases are marked unreachable: BSC_MIN2_U).  Returns 1 if a plan was checked, 0 if
+// none serves the graph; violations / first as BoundsReport.
+int bsc_debug_bounds(const DevGraph& g, int mode, float clip, int T, int& violations, std::string& first) {
+    const BscPlan p = bsc_plan(g, mode, false, false, clip, T);
+    if (!p.ok) return 0;
+    auto fail = [&](const char* what, long long idx, long long lo, long long hi) {
+        if (violations++ == 0) {
+            char buf[160];
+            snprintf(buf, sizeof(buf), "%s: %lld outside [%lld, %lld)", what, idx, lo, hi);
+            first = buf;
+        }
+    };
+    const host::GraphTables& h = *g.host;
+    const BscInst& k = kBscInst[p.inst];
+    const int LPC = k.LPC, EPL = (k.D + LPC - 1) / LPC, z = h.z, nc = g.n_checks;
+    if ((size_t)p.off_a >= sizeof(uint32_t) * AWGN_TAB_W && 4LL * AWGN_TAB_W > (long long)p.off_a)
+        fail("channel tables", 4LL * AWGN_TAB_W, 0, p.off_a);
+    for (int ch = 0; ch < p.cn_lanes / 64; ++ch) {
+        const int32_t d0 = p.lanes[(size_t)ch * 64];
+        const int Lc = (!k.MIX || d0 < 0 || ((d0 >> 20) & 15) == LPC) ? LPC : LPC / 2;
+        uint32_t any = 0u;
+        for (int l = 0; l < 64; ++l) {
+            const int32_t d = p.lanes[(size_t)ch * 64 + l];
+            const int cc = d < 0 ? nc : (d & 0xFFFF);
+            const int ci = std::min(cc / z, nc / z - 1);
+            const int gdeg = cc < nc ? h.row_ptr[ci + 1] - h.row_ptr[ci] : 0;
+            const int npos = (gdeg + Lc - 1) / Lc;
+            if (npos > 31) { fail("real positions of a lane", npos, 0, 32); continue; }
+            any |= (1u << npos) - 1u;
+        }
+        const int gm = __builtin_popcount(any);
+        if (gm < 1 || gm > EPL) fail("real positions of a chunk (the min2 switch)", gm, 1, EPL + 1);
+    }
+    return 1;
+}
 
 bool bsc_q8_ok(const DevGraph& g, int mode, bool ucn, float clip, int T, bool has_short) {
     const BscPlan p = bsc_plan(g, mode, ucn, false, clip, T);

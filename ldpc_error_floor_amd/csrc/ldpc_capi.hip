@@ -50,6 +50,10 @@ struct ldpc_ctx {
     uint32_t* gen_tab = nullptr;
     uint32_t gen_host[AWGN_TAB_W] = {};
     bool gen_valid = false;
+    // recorded on the decode's stream after every decode that reads gen_tab: a table change
+    // waits for it, so a decode still running on another stream keeps the tables it started with
+    hipEvent_t gen_done = nullptr;
+    bool gen_pending = false;
     char last_kernel[64] = {0};   // ldpc_ctx_last_kernel
 };
 
@@ -391,7 +395,9 @@ int ldpc_ctx_destroy(ldpc_ctx* c) {
     dev_free(c->wrong); dev_free(c->anypos); dev_free(c->biterr);
     fused_free(c->fused);
     if (c->llr_scratch) (void)hipFree(c->llr_scratch);
+    if (c->gen_done) (void)hipEventSynchronize(c->gen_done);
     if (c->gen_tab) (void)hipFree(c->gen_tab);
+    if (c->gen_done) (void)hipEventDestroy(c->gen_done);
     delete c;
     return LDPC_OK;
 }
@@ -412,6 +418,33 @@ int ldpc_decode(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_decode_
     return decode_impl(c, llr_dev, B, p, o, stream, nullptr);
 }
 
+// ldpc_decode_awgn's byte channel in the bit-sliced kernels' prologue (their Q8 build) serves a
+// counters-only decode with these parameters (LDPC_AWGN_Q8=0: never, an A/B and test switch)
+static bool q8_serves(const ldpc_ctx* c, const ldpc_decode_params* p, bool has_short) {
+    static const bool q8_on = [] { const char* e = getenv("LDPC_AWGN_Q8"); return !(e && atoi(e) == 0); }();
+    const ldpc_graph* g = c->g;
+    return q8_on && p->decoding_type == LDPC_DEC_QMS && p->kernel != LDPC_KERNEL_FLOOD &&
+           fused_q8_ok(g->dev, mode_of(p->decoding_type, p->q_bit), p->T, p->clip_llr,
+                       g->d_alpha_ucn != nullptr, g->per_edge_w != 0, has_short);
+}
+
+int ldpc_awgn_in_kernel(const ldpc_ctx* c, const ldpc_decode_params* p, int32_t has_short, int32_t app) {
+    if (!c || !p) return LDPC_ERR_ARG;
+    const ldpc_graph* g = c->g;
+    const int mode = mode_of(p->decoding_type, p->q_bit);
+    if (mode < 0) return LDPC_ERR_ARG;
+    if (!app && q8_serves(c, p, has_short != 0)) return 1;
+    // decode_impl with a generator: the fused v5 kernel's prologue, unless the counters-only
+    // decode is the bit-sliced kernels' (which read LLRs when Q8 does not serve) or the kernel
+    // is flood / ffl (the channel kernel first)
+    if (ffl_mode(mode) || !fused_supported(g->dev, mode, p->T, p->clip_llr)) return 0;
+    int kern = p->kernel;
+    if (kern == LDPC_KERNEL_AUTO) kern = auto_fused(mode) ? LDPC_KERNEL_FUSED : LDPC_KERNEL_FLOOD;
+    if (kern != LDPC_KERNEL_FUSED) return 0;
+    return fused_awgn_v5(g->dev, mode, p->T, p->clip_llr, g->d_alpha_ucn != nullptr, g->per_edge_w != 0,
+                         app != 0) ? 1 : 0;
+}
+
 int ldpc_decode_awgn(ldpc_ctx* c, int64_t B, const ldpc_decode_params* p,
                      const ldpc_channel_params* ch, const ldpc_decode_outputs* o, void* stream) {
     if (!c || !p || !ch || !(ch->sigma > 0.0) || ch->offset < 0) return LDPC_ERR_ARG;
@@ -425,14 +458,9 @@ int ldpc_decode_awgn(ldpc_ctx* c, int64_t B, const ldpc_decode_params* p,
     // counters-only QMS decodes the bit-sliced kernels serve: the channel generated in their
     // prologue (SURVEY 8 f rank 1) -- the LLRs never touch HBM (oracle/philox_oracle.awgn_q8); the
     // sampler's tables (8.25 KB) are uploaded when the channel parameters change
-    const int mode = mode_of(p->decoding_type, p->q_bit);
-    static const bool q8_on = [] { const char* e = getenv("LDPC_AWGN_Q8"); return !(e && atoi(e) == 0); }();
     // (counters / flags / iter_wrong only: hard-bit and syndrome exports take the export build,
     // which reads its LLRs)
-    if (q8_on && p->decoding_type == LDPC_DEC_QMS && (!o || (!o->app_all && !o->hard_bits && !o->synd_bits)) &&
-        p->kernel != LDPC_KERNEL_FLOOD &&
-        fused_q8_ok(g->dev, mode, p->T, p->clip_llr, g->d_alpha_ucn != nullptr, g->per_edge_w != 0,
-                    ch->short_start > 0)) {
+    if ((!o || (!o->app_all && !o->hard_bits && !o->synd_bits)) && q8_serves(c, p, ch->short_start > 0)) {
         DeviceGuard dg(g->device);
         if (!c->gen_tab) {
             if (hipMalloc(reinterpret_cast<void**>(&c->gen_tab), sizeof(c->gen_host)) != hipSuccess) {
@@ -443,10 +471,18 @@ int ldpc_decode_awgn(ldpc_ctx* c, int64_t B, const ldpc_decode_params* p,
         }
         uint32_t tab[AWGN_TAB_W];
         awgn_gen_table(a, tab);
+        if (!c->gen_done && hipEventCreateWithFlags(&c->gen_done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            c->gen_done = nullptr;
+            return LDPC_ERR_HIP;
+        }
         if (!c->gen_valid || std::memcmp(tab, c->gen_host, sizeof(tab)) != 0) {
+            // a decode still reading the previous tables may run on another stream: wait for the
+            // last one that used them (gen_done) before the copy overwrites them; the stream wait
+            // keeps the host copy stable until the transfer has read it
+            if (c->gen_pending && hipEventSynchronize(c->gen_done) != hipSuccess) return LDPC_ERR_HIP;
+            c->gen_pending = false;
             std::memcpy(c->gen_host, tab, sizeof(tab));
-            // (stream-ordered behind any decode still reading the previous tables; the wait
-            // keeps the host copy stable until the transfer has read it)
             c->gen_valid = false;
             if (hipMemcpyAsync(c->gen_tab, c->gen_host, sizeof(tab), hipMemcpyHostToDevice,
                                reinterpret_cast<hipStream_t>(stream)) != hipSuccess ||
@@ -455,6 +491,10 @@ int ldpc_decode_awgn(ldpc_ctx* c, int64_t B, const ldpc_decode_params* p,
             c->gen_valid = true;
         }
         st = decode_impl(c, nullptr, B, p, o, stream, nullptr, c->gen_tab, &a);
+        if (st == LDPC_OK) {
+            if (hipEventRecord(c->gen_done, reinterpret_cast<hipStream_t>(stream)) != hipSuccess) return LDPC_ERR_HIP;
+            c->gen_pending = true;
+        }
         if (st != LDPC_ERR_UNSUPPORTED) return st;
     }
     // this kernel reads its LLRs: generate them into the context's buffer, then decode
@@ -615,7 +655,10 @@ static int decode_impl(ldpc_ctx* c, const float* llr_dev, int64_t B, const ldpc_
     const char* served = kern == LDPC_KERNEL_FLOOD ? "flood"
                          : fl ? ffl_kernel_name(g->dev, mode, ucn, g->per_edge_w != 0)
                               : c->fused.last_kernel;
-    std::strncpy(c->last_kernel, served, sizeof(c->last_kernel) - 1);
+    // (a channel generated inside the decoding kernel -- the bit-sliced Q8 build or the v5
+    // prologue -- is marked "+gen", so a caller can tell it from a decode of LLRs in HBM)
+    std::snprintf(c->last_kernel, sizeof(c->last_kernel), "%s%s", served,
+                  (q8 || (gen && kern == LDPC_KERNEL_FUSED)) ? "+gen" : "");
 
     if (count && kern == LDPC_KERNEL_FLOOD) {
         hipLaunchKernelGGL(k_finalize, dim3(std::min(1024, (ntiles + 255) / 256)), dim3(256), 0, s, b,

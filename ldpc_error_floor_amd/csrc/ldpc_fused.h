@@ -1,5 +1,7 @@
 // ldpc_fused.h — fused (all iterations in one launch, LDS/register-resident) decoder.
 #pragma once
+#include <string>
+
 #include "ldpc_internal.h"
 
 namespace ldpc {
@@ -64,8 +66,12 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
 // in the channel, has the shortened-bit marker (a BIG instance)
 bool bs_q8_ok(const DevGraph& g, int mode, bool ucn, float clip, int T, bool has_short);
 bool bsc_q8_ok(const DevGraph& g, int mode, bool ucn, float clip, int T, bool has_short);
+// host-side bounds check of the bsc plan (test infrastructure, ldpc_debug_bs_bounds)
+int bsc_debug_bounds(const DevGraph& g, int mode, float clip, int T, int& violations, std::string& first);
 // (fused_decode with it: the bit-sliced kernel or LDPC_ERR_UNSUPPORTED)
 bool fused_q8_ok(const DevGraph& g, int mode, int T, float clip, bool ucn, bool per_edge_w, bool has_short);
+// a decode with an in-kernel generator (Bufs::awgn) runs the v5 kernel's prologue channel
+bool fused_awgn_v5(const DevGraph& g, int mode, int T, float clip, bool ucn, bool per_edge_w, bool app);
 // compressed bit-sliced kernel (ldpc_bsc.hip): the graphs whose per-edge slots exceed the LDS
 bool bsc_supported(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T);
 const char* bsc_kernel_name(const DevGraph& g, int mode, bool ucn, bool per_edge_w, float clip, int T);

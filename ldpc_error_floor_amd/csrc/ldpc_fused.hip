@@ -66,6 +66,12 @@ bool fused_q8_ok(const DevGraph& g, int mode, int T, float clip, bool ucn, bool 
            bs_q8_ok(g, mode, ucn, clip, T, has_short);
 }
 
+bool fused_awgn_v5(const DevGraph& g, int mode, int T, float clip, bool ucn, bool per_edge_w, bool app) {
+    // fused_decode with a generator: the v5 prologue, except counters-only decodes the
+    // bit-sliced kernels serve (UNSUPPORTED there: ldpc_decode_awgn then generates into HBM)
+    return fused_supported(g, mode, T, clip) && (app || !use_bs(g, mode, T, ucn, per_edge_w, clip));
+}
+
 int64_t fused_bytes_per_cw(const DevGraph& g, int T) {
     (void)T;
     // compulsory: the channel LLRs are read once; outputs are counters only

@@ -201,6 +201,18 @@ PYBIND11_MODULE(_ldpc_nms, m) {
         py::arg("ctx"), py::arg("T"), py::arg("decoding_type"), py::arg("q_bit"),
         py::arg("target_bits"), py::arg("kernel"), py::arg("clip_llr") = 20.0f);
     m.def(
+        "awgn_in_kernel",
+        [](Ctx& c, int T, int decoding_type, int q_bit, int target_bits, int kernel, float clip,
+           bool has_short, bool app) {
+            ldpc_decode_params p = make_params(T, decoding_type, q_bit, target_bits, clip, kernel);
+            const int r = ldpc_awgn_in_kernel(c.h, &p, has_short ? 1 : 0, app ? 1 : 0);
+            check(r < 0 ? r : 0, "ldpc_awgn_in_kernel");
+            return r == 1;
+        },
+        py::arg("ctx"), py::arg("T"), py::arg("decoding_type"), py::arg("q_bit"),
+        py::arg("target_bits"), py::arg("kernel"), py::arg("clip_llr") = 20.0f,
+        py::arg("has_short") = false, py::arg("app") = false);
+    m.def(
         "last_kernel",
         [](Ctx& c) {
             char name[64] = {0};

@@ -184,13 +184,18 @@ class NMSDecoder:
                          ptr(res.flags), stream.cuda_stream, ptr(res.iter_wrong))
         return res
 
-    def generates_channel_in_kernel(self, T=None, kernel=None) -> bool:
-        """Whether ``decode_awgn`` generates the LLRs inside the decoding kernel (the prologue of
-        the fused v5 kernel, and of the bit-sliced kernels for QMS counters-only decodes);
-        otherwise ``ldpc_decode_awgn`` runs the channel kernel into HBM and then the decoder
-        (flood, ffl)."""
-        name = self.kernel_info(T, kernel)[1]
-        return name.startswith("fused5") or (self.decoding_type == DECODING_QMS and name.startswith(("bsl[", "bsc[")))
+    def generates_channel_in_kernel(self, T=None, kernel=None, app: bool = False) -> bool:
+        """Whether a counters-only ``decode_awgn`` (``app``: one with an APP export) generates
+        the LLRs inside the decoding kernel (the prologue of the fused v5 kernel, and of the
+        bit-sliced kernels for QMS counters-only decodes); otherwise ``ldpc_decode_awgn`` runs
+        the channel kernel into HBM and then the decoder (flood, ffl).  The C ABI's own decision
+        (``ldpc_awgn_in_kernel``), with this decoder's shortened range."""
+        T = self.T if T is None else T
+        ctx = self._ensure_ctx(1, T)
+        short = getattr(self, "short", (0, 0)) or (0, 0)
+        return bool(self._ext.awgn_in_kernel(ctx, T, self.decoding_type, self.q_bit, self.target_bits,
+                                             KERNELS[kernel or self.kernel], self.clip,
+                                             has_short=short[0] > 0, app=app))
 
     def last_kernel(self) -> str:
         """The kernel that served this decoder's last decode (``ldpc_ctx_last_kernel``)."""

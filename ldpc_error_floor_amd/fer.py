@@ -75,8 +75,10 @@ def shard_range(total: int, rank: int, world: int):
     return begin, begin + per + (1 if rank < rem else 0)
 
 
-CKPT_VERSION = 2        # 2: key holds point_seeds and the decoder fingerprint; rank 0's file
-                        # is <path> at every world size
+CKPT_VERSION = 3        # 2: key holds point_seeds and the decoder fingerprint; rank 0's file
+                        # is <path> at every world size; 3: the key holds the channel stream
+                        # (CHANNEL_STREAM) and the state the uncorrected-word file's per-point
+                        # marks (the multi-rank merge)
 # The on-GPU channel's stream (csrc/ldpc_awgn.h, oracle/philox_oracle.py), part of a checkpoint's
 # key: a resume across a change of the generator (round 4 replaced QMS Box-Muller by the exact
 # level sampler) would add counters from another codeword stream.  Bump it with the stream.
@@ -104,13 +106,18 @@ class SweepCheckpoint:
         with open(self.path) as f:
             st = json.load(f)
         if st.get("version") != CKPT_VERSION:
-            raise ValueError(f"{self.path}: checkpoint version {st.get('version')} != {CKPT_VERSION}")
+            why = (" (version 3 keys the on-GPU channel stream, "
+                   f"{CHANNEL_STREAM!r}: an older checkpoint cannot say which codewords it decoded)"
+                   if st.get("version") in (1, 2) else "")
+            raise ValueError(f"{self.path}: checkpoint version {st.get('version')} != {CKPT_VERSION}{why}")
         return st
 
-    def save(self, key, si, pos, counters, uncor_bytes=None, done=False):
+    def save(self, key, si, pos, counters, uncor_bytes=None, done=False, uncor_marks=None,
+             uncor_base=None):
         st = {"version": CKPT_VERSION, "key": key, "si": int(si), "pos": int(pos),
               "counters": [[int(v) for v in row] for row in counters],
-              "uncor_bytes": uncor_bytes, "done": bool(done), "time": time.time()}
+              "uncor_bytes": uncor_bytes, "uncor_marks": uncor_marks, "uncor_base": uncor_base,
+              "done": bool(done), "time": time.time()}
         tmp = self.path + ".tmp"
         with open(tmp, "w") as f:
             json.dump(st, f)
@@ -158,7 +165,11 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
 
     ``uncor_path``: append the frames wrong at every iteration to this file in the
     ``Uncor.txt`` format (``sampling_type == 2``, ``Print_Functions.py:155-156``), collected on
-    the GPU; with several ranks each rank writes ``<uncor_path>.rank<r>``.  The file is
+    the GPU.  With several ranks each rank writes ``<uncor_path>.rank<r>`` during the sweep and
+    records where each SNR point's rows end in it; after the final all-reduce rank 0 appends
+    them to ``uncor_path`` point by point, ranks in order -- the shards are contiguous, so the
+    file is byte for byte the one a single process writes (global codeword order), the one file
+    ``main_Post.py`` reads (``Main_Functions.py:529-532``).  The file is
     appended to, as the reference appends (``Print_Functions.py:122``): a fresh start
     (``resume=False``) keeps whatever the file already holds, including the rows of an attempt
     that died before its first checkpoint -- delete it first for a clean run.  A resume
@@ -199,6 +210,15 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
                                                  device=dev)
     flags = torch.empty(batch, dtype=torch.uint8, device=dev) if uncor_path else None
     upath = uncor_path if (uncor_path is None or world == 1) else f"{uncor_path}.rank{rank}"
+    fsize = lambda path: os.path.getsize(path) if os.path.exists(path) else 0   # noqa: E731
+    # the multi-rank merge: marks[si + 1] = this rank's file length after point si (marks[0]: at
+    # the sweep's start); base = the merged file's length at the start (rank 0)
+    marks = [None] * (sigmas.size + 1)
+    base = None
+    if upath is not None:
+        marks[0] = fsize(upath)
+        if world > 1 and rank == 0:
+            base = fsize(uncor_path)
     ck = None
     si0, pos0 = 0, begin
     if checkpoint is not None:
@@ -230,10 +250,14 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
             if upath is not None and st.get("uncor_bytes") is not None and os.path.exists(upath):
                 with open(upath, "r+b") as f:
                     f.truncate(int(st["uncor_bytes"]))
+            if upath is not None and st.get("uncor_marks") is not None:
+                marks = list(st["uncor_marks"])
+            if st.get("uncor_base") is not None:
+                base = int(st["uncor_base"])
 
     def save(si, pos, done=False):
-        ub = (os.path.getsize(upath) if upath and os.path.exists(upath) else 0) if upath else None
-        ck.save(key, si, pos, counters.cpu().tolist(), ub, done)
+        ub = fsize(upath) if upath else None
+        ck.save(key, si, pos, counters.cpu().tolist(), ub, done, marks if upath else None, base)
 
     if ck is not None and st is None:
         # a fresh start records the uncorrected-word file's current length at once: a resume
@@ -290,14 +314,54 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
                 save(si, pos)
             if progress:
                 progress(si, pos - begin, end - begin)
+        if upath is not None:
+            marks[si + 1] = fsize(upath)
         if ck is not None:
             save(si + 1, begin, done=(si + 1 == sigmas.size))
     if dist_on:
         # (a world of one included: the same collective the multi-GPU job runs)
         dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
+    if upath is not None and world > 1:
+        _merge_uncor_files(uncor_path, marks, base, rank, world, group, counters.device)
     host = counters.cpu().numpy()
     return [Counters.from_array(host[i], int(n_codewords), decoder.n_vars)
             for i in range(sigmas.size)]
+
+
+def _merge_uncor_files(uncor_path, marks, base, rank, world, group, device):
+    """The multi-rank uncorrected-word collection's last step: every rank's per-point marks
+    (byte offsets into ``<uncor_path>.rank<r>``) to rank 0, which appends point by point, ranks
+    in order, the rows each rank wrote for it to ``uncor_path`` (truncated back to its length at
+    the sweep's start first, so a resumed finished sweep merges again to the same file).  The
+    shards are contiguous in global codeword order (``shard_range``), so the result is the
+    single-process file byte for byte.  One all_gather of an int64 tensor (gloo and RCCL alike)
+    and a barrier, so no rank leaves before the file is complete."""
+    import torch
+    import torch.distributed as dist
+    mine = torch.tensor([-1 if m is None else int(m) for m in marks], dtype=torch.int64, device=device)
+    allm = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allm, mine, group=group)
+    if rank == 0:
+        rows = [m.cpu().tolist() for m in allm]
+        if any(x < 0 for r in rows for x in r):
+            raise RuntimeError("uncorrected-word merge: a rank did not finish every SNR point")
+        with open(uncor_path, "ab") as out:
+            out.truncate(int(base or 0))
+            out.seek(0, os.SEEK_END)
+            srcs = [open(f"{uncor_path}.rank{r}", "rb") if os.path.exists(f"{uncor_path}.rank{r}") else None
+                    for r in range(world)]
+            try:
+                for si in range(len(marks) - 1):
+                    for r, f in enumerate(srcs):
+                        a, b = rows[r][si], rows[r][si + 1]
+                        if b > a:
+                            f.seek(a)
+                            out.write(f.read(b - a))
+            finally:
+                for f in srcs:
+                    if f is not None:
+                        f.close()
+    dist.barrier(group=group)
 
 
 def _pipelines(decoder, T, kernel) -> bool:

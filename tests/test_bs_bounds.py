@@ -83,3 +83,15 @@ def test_pre_guard_read_is_caught(lib):
     # the graphs whose UCN instances have no waves past their check lanes stay clean
     n, v, msg = bounds(lib, "wman_N0576_R34_z24", 24, 20, flags=PRE_GUARD)
     assert v == 0, msg
+
+
+def test_bsc_plan_checked(lib):
+    """5G BG1 (C5) is the compressed kernel's (bsc): its plan is checked too -- the channel tables
+    inside the SGN region they borrow, and every check chunk's real-position count inside the
+    1 .. EPL range its min2 switch covers (the other counts are marked unreachable)."""
+    name, z = GRAPHS[3]
+    # (one channel weight per iteration: the uniform-lane plan and the beta = 1 mixed-lane one;
+    # per-column channel tables do not fit BG1's LDS, so no kernel of the bit-sliced family
+    # serves that case)
+    n, v, msg = bounds(lib, name, z, 50, au=1, bu=1)
+    assert n == 2 and v == 0, (n, msg)

@@ -49,6 +49,55 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _uncor_worker(rank, world, port, q, path, ck, resume):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        res = fer_sweep(_make_decoder(), SIGMAS, N_CW, BATCH, seed=1076, uncor_path=path,
+                        checkpoint=ck, resume=resume, checkpoint_every=2)
+        q.put((rank, [c.frame_err_all for c in res]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_world(world, target, extra):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + extra) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+def test_gloo_world2_uncorrected_file_equals_single_process(tmp_path):
+    """The multi-rank uncorrected-word collection ends in ONE file, byte-identical to the
+    single-process sweep's (global codeword order, SNR point by point): each rank writes
+    <path>.rank<r> with per-point marks, rank 0 merges after the all-reduce
+    (Print_Functions.py:120-126 writes the file main_Post.py reads, Main_Functions.py:529-532).
+    Rows already in the file stay in front (the reference appends); a resume of the finished
+    sweep merges again to the same bytes."""
+    single = tmp_path / "single.txt"
+    res1 = fer_sweep(_make_decoder(), SIGMAS, N_CW, BATCH, seed=1076, uncor_path=str(single))
+    assert res1[0].frame_err_all > 0
+    path = tmp_path / "Uncor.txt"
+    path.write_bytes(b"earlier\trow\n")
+    ck = str(tmp_path / "u.ckpt")
+    got = _run_world(2, _uncor_worker, (str(path), ck, False))
+    assert got[0] == got[1] == [c.frame_err_all for c in res1]
+    assert path.read_bytes() == b"earlier\trow\n" + single.read_bytes()
+    assert os.path.exists(f"{path}.rank1")
+    # a resumed finished sweep: the same file, not the rows twice
+    _run_world(2, _uncor_worker, (str(path), ck, True))
+    assert path.read_bytes() == b"earlier\trow\n" + single.read_bytes()
+    rows = np.loadtxt(path, delimiter="\t", ndmin=2, skiprows=1)
+    assert rows.shape == (sum(c.frame_err_all for c in res1), 3 + 576)
+
+
 def test_shard_range_partitions():
     for total in (0, 1, 7, 45, 1 << 20):
         for world in (1, 2, 3, 8):

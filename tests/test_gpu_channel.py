@@ -81,9 +81,14 @@ def test_decode_awgn_equals_decoding_oracle_llrs(cuda_device):
                      (got.iter_wrong, want.iter_wrong)):
             assert np.array_equal(a.cpu().numpy(), b.cpu().numpy()), k
         if k == "fused":
-            assert dec.last_kernel().startswith("bsl["), dec.last_kernel()
+            assert dec.last_kernel().startswith("bsl[") and dec.last_kernel().endswith("+gen"), dec.last_kernel()
+            assert dec.generates_channel_in_kernel(kernel=k)
+        else:
+            assert dec.last_kernel() == "flood" and not dec.generates_channel_in_kernel(kernel=k)
     # the v5 prologue channel (APP export)
     got = dec.decode_awgn(64, sigma, seed, offset=off + 5, app=True)
+    assert dec.last_kernel().startswith("fused5[") and dec.last_kernel().endswith("+gen"), dec.last_kernel()
+    assert dec.generates_channel_in_kernel(app=True)
     want = dec.decode(ref_t[5:69], app=True)
     assert np.array_equal(got.app.cpu().numpy(), want.app.cpu().numpy())
     W = dec.weights
@@ -114,7 +119,11 @@ def test_byte_channel_equals_float_channel(config, off, cuda_device):
     k_float = dec.last_kernel()
     got = dec.decode_awgn(B, sigma, 17, offset=1000 + off, punct=punct, short=short,
                           counters=True, flags=True, iter_wrong=True)
-    assert dec.last_kernel() == k_float and k_float.startswith(("bsl[", "bsc[")), k_float
+    # (the "+gen" marker: the channel was generated in the kernel's prologue, not read from HBM
+    # -- a quiet fallback to the float path would decode the same LLRs to the same counters)
+    assert dec.last_kernel() == k_float + "+gen" and k_float.startswith(("bsl[", "bsc[")), (k_float, dec.last_kernel())
+    dec.short = short
+    assert dec.generates_channel_in_kernel()
     for a, b in ((got.flags, want.flags), (got.counters, want.counters),
                  (got.iter_wrong, want.iter_wrong)):
         assert np.array_equal(a.cpu().numpy(), b.cpu().numpy())
@@ -145,7 +154,7 @@ def test_qms_high_word_tie_bit_exact(cuda_device, off):
         assert np.array_equal(app, want)
         # the bit-sliced kernel's in-prologue channel (counters-only): the same tie resolution
         got = dec.decode_awgn(B, s, seed, offset=off, counters=True, flags=True, iter_wrong=True)
-        assert dec.last_kernel().startswith("bsl["), dec.last_kernel()
+        assert dec.last_kernel().startswith("bsl[") and dec.last_kernel().endswith("+gen"), dec.last_kernel()
         exp = dec.decode(torch.from_numpy(ref).to(cuda_device), app=False, counters=True, flags=True,
                          iter_wrong=True)
         for x, y in ((got.flags, exp.flags), (got.counters, exp.counters), (got.iter_wrong, exp.iter_wrong)):

@@ -49,6 +49,24 @@ def test_bench_world8_gloo_equals_world1(cuda_device):
     assert o1["counters"]["frame_err_last"] > 0
 
 
+def test_bench_world8_c4_gloo_equals_world1(cuda_device):
+    """BASELINE configs[3]'s own workload (5G BG2 n1024, T=20, puncture / shorten, the batch
+    sharded over 8 ranks): world-8 counters equal world 1 and the rank offsets tile [0, 8B)."""
+    B, steps = 2048, 1
+    base = ["--config", "C4", "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline"]
+    r8 = _bench(base + ["--gpus", "8", "--batch", str(B)], _env(LDPC_BENCH_BACKEND="gloo"))
+    assert r8.returncode == 0, r8.stderr[-3000:]
+    o8 = json.loads([l for l in r8.stdout.splitlines() if l.startswith("{")][-1])
+    assert o8["n_gpus"] == 8 and o8["process_group"] == {"backend": "gloo", "world": 8}
+    assert o8["counters"]["rank_offsets"] == [r * B for r in range(8)]
+    r1 = _bench(base + ["--batch", str(8 * B)], _env())
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    o1 = json.loads([l for l in r1.stdout.splitlines() if l.startswith("{")][-1])
+    keys = ("bit_err_last", "frame_err_last", "frame_err_all", "loss2")
+    assert [o8["counters"][k] for k in keys] == [o1["counters"][k] for k in keys]
+    assert o1["counters"]["frame_err_last"] > 0
+
+
 def test_bench_world8_rank_failure_stops_the_job(cuda_device):
     r = _bench(["--gpus", "8", "--batch", "4096", "--steps", "1", "--warmup", "1", "--no-cpu-baseline"],
                _env(LDPC_BENCH_BACKEND="gloo", LDPC_TEST_FAIL_RANK="5"))
@@ -78,3 +96,25 @@ def test_sweep_c5_world8_gloo_equals_world1(tmp_path):
     assert outs["w1"]["scan"][0]["frame_err_last"] > 0 and outs["w1"]["deep"]
     for r in range(1, 8):
         assert os.path.exists(os.path.join(str(tmp_path / "w8"), f"ckpt_scan.json.rank{r}"))
+
+
+def test_sweep_uncor_world2_file_equals_world1(tmp_path):
+    """The multi-rank uncorrected-word collection on the GPU (gloo world 2 on one card, C2 at
+    1.5 dB): the one merged Uncor file is byte-identical to world 1's, and the JSON rates give
+    the collection sweep's throughput."""
+    args = [sys.executable, os.path.join(ROOT, "tools", "sweep_c5.py"), "--config", "C2",
+            "--deep-snrs", "1.5,2.0", "--deep", "20000", "--batch", "8192", "--uncor"]
+    outs = {}
+    for name, extra, env in (("w1", [], _env()),
+                             ("w2", ["--gpus", "2"], _env(LDPC_SWEEP_BACKEND="gloo"))):
+        out = str(tmp_path / name)
+        r = subprocess.run(args + extra + ["--out", out], env=env, capture_output=True, text=True,
+                           timeout=600, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        with open(os.path.join(out, "sweep_c2.json")) as f:
+            outs[name] = json.load(f)
+    w1 = open(os.path.join(str(tmp_path / "w1"), "Uncor_deep.txt"), "rb").read()
+    w2 = open(os.path.join(str(tmp_path / "w2"), "Uncor_deep.txt"), "rb").read()
+    n = sum(r["frame_err_any_iter"] for r in outs["w1"]["deep"])
+    assert n > 0 and w1.count(b"\n") == n
+    assert w2 == w1

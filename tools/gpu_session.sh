@@ -11,6 +11,7 @@
 #   ablate:CFG:LIB:SET         -DBS_DIAG build, LDPC_DIAG_ABLATE over SET (comma list), timing only
 #   trace                      rocprofv3 kernel-trace summary of the default bench command
 #   prof:CFG                   tools/profile.sh kernel trace + PMC passes of one config
+#   stamp:CFG:LIB[:NAME=VALUE] per-wave phase clocks of a -DBS_STAMP build (optionally with an env switch)
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -64,6 +65,12 @@ for step in "$@"; do
         echo -n "$a1 ablate=$ab: "; LDPC_DIAG_ABLATE=$ab bench_ms $a1 || { restore; exit 1; }
       done
       restore ;;
+    stamp)
+      # stamp:CFG:LIB[:NAME=VALUE]  a -DBS_STAMP build's per-wave phase clocks (stderr) -> stamp_CFG*.log
+      cp $a2 $L || exit 1
+      log=$OUT/stamp_${a1}${a3:+_${a3//[=]/_}}.log
+      ( [ -n "$a3" ] && export "$a3"; timeout -k 10 300 python bench.py --config $a1 --steps 3 --warmup 1 --no-cpu-baseline > $log.json 2> $log ) || { restore; tail -5 $log; exit 1; }
+      restore; grep -A17 "bs_stamp" $log | tail -18 ;;
     trace)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/bench_trace -o bench --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/bench_c2_traced.json 2> $OUT/bench_c2_traced.err || { tail $OUT/bench_c2_traced.err; exit 1; }
       cat $OUT/bench_c2_traced.json ;;

@@ -47,6 +47,9 @@ def parse(argv=None):
     ap.add_argument("--deep", type=int, default=1 << 30)
     ap.add_argument("--deep-below", type=float, default=1e-3)
     ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per rank per decode")
+    ap.add_argument("--uncor", action="store_true",
+                    help="collect the frames wrong at every iteration into <out>/Uncor_<stage>.txt "
+                         "(the Uncor.txt format main_Post.py reads; one merged file at any --gpus)")
     ap.add_argument("--deep-snrs", default="",
                     help="skip the scan: decode --deep codewords at each of these SNRs only")
     a = ap.parse_args(argv)
@@ -130,7 +133,8 @@ def main(argv=None, make_decoder=None):
         # deep stage and separate --deep-snrs runs of different SNRs never share noise
         res = fer_sweep(dec, [sig[i] for i in idx], n, a.batch, seed=1076, progress=progress,
                         checkpoint=os.path.join(a.out, f"ckpt_{stage}.json"), checkpoint_every=16,
-                        resume=True, point_seeds=[point_seed(snrs[i], stage) for i in idx])
+                        resume=True, point_seeds=[point_seed(snrs[i], stage) for i in idx],
+                        uncor_path=os.path.join(a.out, f"Uncor_{stage}.txt") if a.uncor else None)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         dt = stage_time(time.time() - t0)
@@ -167,6 +171,8 @@ def main(argv=None, make_decoder=None):
                "seconds": {"scan": round(t_scan, 1), "deep": round(t_deep, 1)},
                "codewords_total": n_total,
                "codewords_per_s": round(n_total / max(t_scan + t_deep, 1e-9), 1),
+               "uncor_files": ([f"Uncor_{st}.txt" for st, rows in (("scan", scan), ("deep", deep)) if rows]
+                               if a.uncor else None),
                "note": "FER counters from fer_sweep (device int64 counters summed over the ranks, "
                        "calc_ber_fer semantics: fer_last = frames wrong at the last iteration, "
                        "fer = frames wrong at every iteration); e2e includes the channel kernel; "
