@@ -25,7 +25,7 @@ ARCH = os.environ.get("LDPC_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["ldpc_capi.hip", "ldpc_flood.hip", "ldpc_fused.hip", "ldpc_fused5.hip",
                "ldpc_bs.hip", "ldpc_bsc.hip", "ldpc_ffl.hip", "ldpc_channel.hip", "ldpc_collect.hip"]
-HEADERS = ["ldpc_internal.h", "ldpc_fused.h", "ldpc_fused5_kernel.h", "ldpc_bs_kernel.h", "ldpc_awgn.h",
+HEADERS = ["ldpc_internal.h", "ldpc_fused.h", "ldpc_fused5_kernel.h", "ldpc_bs_kernel.h", "ldpc_bitplane.h", "ldpc_awgn.h",
            "ldpc_host.h", "ldpc_quant.h"]
 # host-only C++ (no HIP): also built with g++ -fsanitize=address,undefined by
 # tests/test_host_sanitized.py

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <utility>
 #include <vector>
@@ -296,6 +297,9 @@ namespace bs {
 // to the SIMD with the smallest total and a free wave slot.  A wave's chunks are in descending
 // cost (the first place takes the heaviest: bsc's heavy-degree place).  LDPC_BS_DEAL=0: the
 // previous dealing (heaviest chunk to the least-loaded SIMD, on its emptiest wave).
+#ifndef BS_DEAL_DEFAULT
+#define BS_DEAL_DEFAULT 1
+#endif
 std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap) {
     const int n = (int)cost.size();
     std::vector<int> order(n), slot((size_t)nw * cap, -1);
@@ -315,6 +319,52 @@ std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap) {
             slot[(size_t)bw * cap + used[bw]] = c;
             ++used[bw];
             load[best] += cost[c];
+        }
+        return slot;
+    }
+    // one chunk per wave (the one-chunk instances, up to 16 waves): the exact assignment of the
+    // chunks to the SIMDs' wave slots that minimises the largest SIMD total (LDPC_BS_DEAL=2).
+    // LPT is not optimal where the SIMDs hold different numbers of waves: wman's 9 chunks
+    // (3 + degree: 9 9 9 6 6 6 6 6 5) go 9 6 5 / 9 6 / 9 6 / 6 6 under LPT, a largest total of
+    // 20 on the 3-wave SIMD (which also runs 3 of the 9 check waves), and 6 6 5 / 9 6 / 9 6 /
+    // 9 6 exactly, 17.
+    const int deal_mode = e ? atoi(e) : BS_DEAL_DEFAULT;
+    if (deal_mode == 2 && cap == 1 && n <= nw && nw <= 16) {
+        int slots[4] = {0, 0, 0, 0};
+        for (int w = 0; w < nw; ++w) ++slots[w % 4];
+        std::vector<int> cur(n, -1), best(n, -1);
+        int load[4] = {0, 0, 0, 0}, used[4] = {0, 0, 0, 0};
+        long long best_key = -1;
+        // key: largest SIMD total, then the sum of squares (spread the rest)
+        std::function<void(int)> rec = [&](int i) {
+            const int mx = std::max(std::max(load[0], load[1]), std::max(load[2], load[3]));
+            if (best_key >= 0 && (long long)mx * 1000000 > best_key) return;
+            if (i == n) {
+                const long long key = (long long)mx * 1000000 + (long long)load[0] * load[0] + (long long)load[1] * load[1] +
+                                      (long long)load[2] * load[2] + (long long)load[3] * load[3];
+                if (best_key < 0 || key < best_key) { best_key = key; best = cur; }
+                return;
+            }
+            for (int sm = 0; sm < 4; ++sm) {
+                if (used[sm] >= slots[sm]) continue;
+                bool dup = false;                  // (a SIMD in the same state as one tried)
+                for (int q = 0; q < sm; ++q)
+                    if (used[q] < slots[q] && load[q] == load[sm] && slots[q] - used[q] == slots[sm] - used[sm]) dup = true;
+                if (dup) continue;
+                load[sm] += cost[order[i]];
+                ++used[sm];
+                cur[i] = sm;
+                rec(i + 1);
+                load[sm] -= cost[order[i]];
+                --used[sm];
+            }
+        };
+        rec(0);
+        int next[4] = {0, 1, 2, 3};
+        for (int i = 0; i < n; ++i) {                  // heaviest first: the SIMD's oldest wave
+            const int sm = best[i];
+            slot[(size_t)next[sm]] = order[i];
+            next[sm] += 4;
         }
         return slot;
     }
@@ -790,20 +840,21 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
 #ifdef BS_STAMP
     // diagnostic build: per-wave phase clocks of this decode, printed to stderr
     static unsigned long long* dst = nullptr;
-    if (!dst && hipMalloc(reinterpret_cast<void**>(&dst), 128 * 8) != hipSuccess) return LDPC_ERR_OOM;
-    if (hipMemsetAsync(dst, 0, 128 * 8, s) != hipSuccess) return LDPC_ERR_HIP;
+    if (!dst && hipMalloc(reinterpret_cast<void**>(&dst), 256 * 8) != hipSuccess) return LDPC_ERR_OOM;
+    if (hipMemsetAsync(dst, 0, 256 * 8, s) != hipSuccess) return LDPC_ERR_HIP;
     a.stamps = dst;
     st = kLaunch[p.inst](a, nblocks, p.nw, lds, s, b.q8 != nullptr);
-    unsigned long long hst[128];
+    unsigned long long hst[256];
     if (st != LDPC_OK || hipMemcpyAsync(hst, dst, sizeof(hst), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return st != LDPC_OK ? st : LDPC_ERR_HIP;
-    fprintf(stderr, "bs_stamp inst %d T %d: per pack, shader clocks [check, check-barrier, var, var-barrier, prologue, epilogue]\n",
-            p.inst, b.T);
+    fprintf(stderr, "bs_stamp inst %d T %d q8 %d: per pack, shader clocks [check, check-barrier, var, var-barrier | "
+            "entry, channel, ch-barrier, tables, first-var, check-setup | epilogue]\n", p.inst, b.T, b.q8 != nullptr);
+    static const int order[] = {0, 1, 2, 3, 8, 9, 10, 11, 12, 4, 5};
     for (int w = 0; w < p.nw && w < 16; ++w) {
-        const double n = (double)(hst[8 * w + 6] ? hst[8 * w + 6] : 1);
+        const double n = (double)(hst[16 * w + 15] ? hst[16 * w + 15] : 1);
         fprintf(stderr, "  wave %2d:", w);
-        for (int i = 0; i < 6; ++i) fprintf(stderr, " %9.0f", hst[8 * w + i] / n);
+        for (const int i : order) fprintf(stderr, " %8.0f", hst[16 * w + i] / n);
         fprintf(stderr, "\n");
     }
     return st;

@@ -36,6 +36,7 @@
 #include "ldpc_beta_tabs.h"
 #include "ldpc_fused.h"
 #include "ldpc_fused5_kernel.h"
+#include "ldpc_bitplane.h"
 
 namespace ldpc {
 namespace bs {
@@ -134,107 +135,15 @@ struct BsArgs {
                                  // hard-decision addresses, [HDW][lane] words
     uint32_t pad_;
     BsGen gen;                   // Q8 builds: the in-prologue channel
-    unsigned long long* stamps;  // -DBS_STAMP builds only: [16 waves][8] shader-clock sums per
+    unsigned long long* stamps;  // -DBS_STAMP builds only: [16 waves][16] shader-clock sums per
                                  // phase (0 check, 1 check barrier, 2 variable, 3 variable barrier,
-                                 // 4 prologue, 5 epilogue, 6 packs), timing diagnostics
+                                 // 4 prologue's check setup, 5 epilogue, 8 entry, 9 channel, 10 its
+                                 // barrier, 11 tables, 12 first variable phase; 15 packs), timing
+                                 // diagnostics
 };
 
-// ---- bit-plane arithmetic ---------------------------------------------------------------------
-// Every 3-input function is one v_bitop3_b32 with an explicit truth table (the compiler's own
-// boolean synthesis often emits two or three ops for one such function); 2-input functions are
-// left to the compiler, which emits the 2-cycle VOP2 forms (v_and / v_or / v_xor / v_xnor).
-// Truth table of f: f(0xF0, 0xCC, 0xAA) for operands (a, b, c).
-#define B3(F, a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), (F))
-constexpr unsigned TA = 0xF0, TB = 0xCC, TC = 0xAA;
-constexpr unsigned T_XOR3 = (TA ^ TB ^ TC) & 0xFF;                       // a ^ b ^ c
-constexpr unsigned T_XNOR3 = ~(TA ^ TB ^ TC) & 0xFF;                     // ~(a ^ b ^ c)
-constexpr unsigned T_MAJ = ((TA & TB) | (TA & TC) | (TB & TC)) & 0xFF;   // maj(a, b, c)
-constexpr unsigned T_MAJNB = ((TA & ~TB) | (TA & TC) | (~TB & TC)) & 0xFF;   // maj(a, ~b, c)
-constexpr unsigned T_MUX = ((TA & TB) | (~TA & TC)) & 0xFF;              // a ? b : c
-constexpr unsigned T_LT = ((~TA & TB) | (~(TA ^ TB) & TC)) & 0xFF;       // a < b at this bit, else c
-constexpr unsigned T_ANDN = (~TA & TB) & 0xFF;                           // ~a & b
-constexpr unsigned T_LEAF = ((TA & TB) ^ TC) & 0xFF;                     // (a & b) ^ c
-constexpr unsigned T_AND3 = (TA & TB & TC) & 0xFF;                       // a & b & c
-constexpr unsigned T_SAT = ((TA & ~TB) | (~TA & TC)) & 0xFF;             // a ? ~b : c
-constexpr unsigned T_XAND = (TA ^ (TB & TC)) & 0xFF;                     // a ^ (b & c)
-constexpr unsigned T_ORXOR = (TA | (TB ^ TC)) & 0xFF;                    // a | (b ^ c)
-__device__ __forceinline__ uint32_t mux(uint32_t s, uint32_t a, uint32_t b) { return B3(T_MUX, s, a, b); }
-
-// S += m for m = (negative flag n, b) with b_i = M_i ^ n (M the 4 magnitude planes): the
-// two's complement of m is b sign-extended with n, plus n
-template <int SB>
-__device__ __forceinline__ void add_b(uint32_t (&S)[SB], const uint32_t (&b)[4], uint32_t n) {
-    // (the carry first: S[i]'s last use is then the instruction that redefines it, so the sum
-    // stays in S's registers; summed under a wave-uniform "edge f exists" branch, the other order
-    // left a copy of every plane at the branch's merge, 7 v_mov per edge)
-    uint32_t c = n;
-#pragma unroll
-    for (int i = 0; i < SB; ++i) {
-        const uint32_t bi = (i < 4) ? b[i] : n;
-        const uint32_t cn = (i + 1 < SB) ? B3(T_MAJ, S[i], bi, c) : 0u;
-        S[i] = B3(T_XOR3, S[i], bi, c);
-        c = cn;
-    }
-}
-// S = m (same operand form), S previously zero
-template <int SB>
-__device__ __forceinline__ void set_b(uint32_t (&S)[SB], const uint32_t (&b)[4], uint32_t n) {
-    uint32_t c = n;
-#pragma unroll
-    for (int i = 0; i < SB; ++i) {
-        const uint32_t bi = (i < 4) ? b[i] : n;
-        S[i] = bi ^ c;
-        c = bi & c;
-    }
-}
-
-// x = Tv - m (7 planes, two's complement; Tv in [-32, 31], |m| <= 15) with m = (n, b) as above:
-// -m is ~b sign-extended with ~n, plus ~n
-__device__ __forceinline__ void sub_tv(uint32_t (&x)[7], const uint32_t (&T)[6], const uint32_t (&b)[4],
-                                       uint32_t n) {
-    uint32_t c = ~n;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        const uint32_t t = T[i < 6 ? i : 5];
-        const uint32_t bi = (i < 4) ? b[i] : n;
-        x[i] = B3(T_XNOR3, t, bi, c);
-        if (i < 6) c = B3(T_MAJNB, t, bi, c);
-    }
-}
-
-// min(|x|, 15) (4 planes) of a 7-plane two's complement x in [-64, 63]; the sign is x[6].
-// For x < 0 the low bits of -x are x_i ^ OR(x_j, j < i); |x| >= 16 is x5 | x4 for x >= 0 and
-// "not (x5 & x4 & low 4 bits nonzero)" for x < 0.
-__device__ __forceinline__ void abs_sat(uint32_t (&X)[4], const uint32_t (&x)[7]) {
-    const uint32_t neg = x[6];
-    const uint32_t o2 = x[0] | x[1], o3 = o2 | x[2], o4 = o3 | x[3];
-    const uint32_t sat = B3(T_SAT, neg, B3(T_AND3, x[5], x[4], o4), x[5] | x[4]);
-    X[0] = x[0] | sat;
-    X[1] = B3(T_XAND, x[1], neg, x[0]) | sat;
-    X[2] = B3(T_XAND, x[2], neg, o2) | sat;
-    X[3] = B3(T_XAND, x[3], neg, o3) | sat;
-}
-
-// a < b for 4-plane unsigned values
-__device__ __forceinline__ uint32_t lt4(const uint32_t (&a)[4], const uint32_t (&b)[4]) {
-    uint32_t l = B3(T_ANDN, a[0], b[0], 0u);
-#pragma unroll
-    for (int i = 1; i < 4; ++i) l = B3(T_LT, a[i], b[i], l);
-    return l;
-}
-
-// SB-plane two's complement -> 6 planes, saturated to [-32, 31]
-template <int SB>
-__device__ __forceinline__ void clamp6(uint32_t (&T)[6], const uint32_t (&v)[SB]) {
-    uint32_t ovf = 0;
-#pragma unroll
-    for (int i = 5; i < SB - 1; ++i) ovf |= v[i] ^ v[i + 1];
-    const uint32_t s = v[SB - 1];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) T[i] = B3(T_SAT, ovf, s, v[i]);
-    T[5] = mux(ovf, s, v[5]);
-}
-
+// bit-plane arithmetic (B3, the truth tables, add_b / set_b / sub_tv / abs_sat / lt4 / clamp6):
+// ldpc_bitplane.h
 // LDS accesses by byte address (all slots and tables are LDS-absolute: the kernel's dynamic
 // LDS starts at 0, checked at entry)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -913,6 +822,24 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 #ifndef BS_BKPF
 #define BS_BKPF 1
 #endif
+// iteration 0's tables copied asynchronously behind the channel loads (A/B switch; 0: through
+// registers after the channel barrier, with a barrier of their own)
+#ifndef BS_T0ASYNC
+#define BS_T0ASYNC 1
+#endif
+// the prologue's first barrier after the first LLR loads are issued (A/B switch; 0: before them)
+#ifndef BS_EB
+#define BS_EB 1
+#endif
+// the prologue's wave priority (A/B switch): the channel, tables and first variable phase of a
+// new workgroup compete with the other resident workgroups' iterations, whose check phases run
+// at priority 1-2; at 0 the prologue takes the issue slots they leave
+#ifndef BS_VAO
+#define BS_VAO 1
+#endif
+#ifndef BS_PROPRIO
+#define BS_PROPRIO 0
+#endif
 
 // Register budget: the small instances run at 64 VGPRs (WPE 8: three 9-wave workgroups per CU).
 // At a 72-register budget only two were resident (the waves of a workgroup are not spread evenly
@@ -944,7 +871,7 @@ k_bs(BsArgs a) {
 #ifdef BS_STAMP
     // per-wave phase times (wave-uniform, s_memtime shader clocks): where a wave's time goes,
     // barrier waits included (diagnostic builds only)
-    uint64_t sacc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t sacc[13] = {};
     uint64_t sts = __builtin_amdgcn_s_memtime();
 #define BS_ST(i)                                                                                   \
     do {                                                                                           \
@@ -976,6 +903,7 @@ k_bs(BsArgs a) {
         return ucn && (t >= 64 || ((a.ucn_iter >> t) & 1));
     };
 
+    if (BS_PROPRIO > 0) __builtin_amdgcn_s_setprio(BS_PROPRIO);
     // ---- per-lane variables: slot addresses, variable index, degree bounds of the wave ----------
     uint32_t va[VPL][VNA];
     int vv[VPL], dw[VPL], dwmin[VPL], pcol[VPL];
@@ -1009,11 +937,29 @@ k_bs(BsArgs a) {
                             (uint32_t)a.stagger_n);
         for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(8);
     }
-    if (tid == 0) RED[7] = 0u;
+    // PAD slot (all ones: V->C negative, magnitude 15), ZERO slot (a zero C->V), the zero hard
+    // decision word of UCN padding edges, the counters and the off-grid flag RED[7]; iteration
+    // 0's tables are copied global -> LDS asynchronously (global_load_lds) behind the channel
+    // loads, retired by the channel barrier (through registers, each thread's loads waited in
+    // turn: three L2 round trips and a barrier of their own per pack)
+    if (tid < SLOT_W) {
+        reinterpret_cast<uint32_t*>(smem + a.off_pad)[tid] = 0xFFFFFFFFu;
+        reinterpret_cast<uint32_t*>(smem + a.off_zero)[tid] = 0u;
+    }
+    if (UCN && tid == 0) lds_put(a.off_hdz, 0u);
+    if (tid < 8) RED[tid] = (tid == 1) ? 0xFFFFFFFFu : 0u;
+    // (the barrier that orders these writes before the channel's flag updates: here when the
+    // channel is generated from the sampler's tables; else after the first variable's LLR loads
+    // are issued, so that it waits beside their HBM round trip, BS_EB)
     if constexpr (Q8) gen_tables(a.gen, tid, NT);
-    __syncthreads();
+    if (Q8 || !BS_EB) __syncthreads();
+    BS_ST(8);
     uint32_t cs[VPL], cm[VPL][4], bg[VPL];
     int off = 0;
+    if (BS_T0ASYNC) {                    // (retired by the channel barrier's vmcnt(0))
+        copy_async(a.off_alut, a.alut, AL, wave, NT);
+        copy_async(a.off_blut, a.blut, BL, wave, NT);
+    }
     // all 32 loads of a variable issued before any use: one HBM round trip per workgroup
     // prologue (with batches of 8 the LLR fetch cost 0.75 ms of a 6.5 ms C2 decode, with this
     // 0.44 ms: the workgroups stay in step, so every pack boundary is a chip-wide HBM burst; a
@@ -1058,6 +1004,15 @@ k_bs(BsArgs a) {
 #pragma unroll
         for (int r = 0; r < PACK; ++r) xv[0][r] = llr_at(r, var_of(0));
     }
+    if (BS_EB) {
+        // (a workgroup barrier without __syncthreads' fence, whose vmcnt(0) would wait for the
+        // loads just issued: the LDS writes above complete (lgkmcnt(0)) and the compiler keeps
+        // every memory access on its side)
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0), vmcnt / expcnt untouched
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    }
 #pragma unroll
     for (int u = 0; u < VPL; ++u) {
         cs[u] = 0u;
@@ -1097,7 +1052,9 @@ k_bs(BsArgs a) {
     }
     }
     if (off) atomicOr(&RED[7], 1u);
+    BS_ST(9);
     __syncthreads();
+    BS_ST(10);
     if (RED[7]) {                              // off the grid: the v5 fixup decodes this pack
         if (tid == 0) a.bad[blockIdx.x] = 1u;
         return;
@@ -1114,17 +1071,12 @@ k_bs(BsArgs a) {
             *reinterpret_cast<LdsQ*>(a.off_ch + 16u * (uint32_t)(tid * VPL + u)) = c4;
         }
     }
-    // PAD slot (all ones: V->C negative, magnitude 15), ZERO slot (a zero C->V), the zero hard
-    // decision word of UCN padding edges, counters, iteration 0's tables
-    if (tid < SLOT_W) {
-        reinterpret_cast<uint32_t*>(smem + a.off_pad)[tid] = 0xFFFFFFFFu;
-        reinterpret_cast<uint32_t*>(smem + a.off_zero)[tid] = 0u;
+    if (!BS_T0ASYNC) {
+        for (int w = tid; w < AL; w += NT) ALUT[w] = a.alut[w];
+        for (int w = tid; w < BL; w += NT) BLUT[w] = a.blut[w];
+        __syncthreads();
     }
-    if (UCN && tid == 0) lds_put(a.off_hdz, 0u);
-    if (tid < 8) RED[tid] = (tid == 1) ? 0xFFFFFFFFu : 0u;
-    for (int w = tid; w < AL; w += NT) ALUT[w] = a.alut[w];
-    for (int w = tid; w < BL; w += NT) BLUT[w] = a.blut[w];
-    __syncthreads();
+    BS_ST(11);
 
     // ---- variable phase -------------------------------------------------------------------------
     //   first: lw_0 as every edge's V->C (no C->V yet);
@@ -1145,7 +1097,13 @@ k_bs(BsArgs a) {
             if (BS_VSKIP && VPL > 1 && dw[u] < 0) continue;
             PH("vn_setup", (last ? 100 : 0) + u);
 #pragma unroll
-            for (int p = 0; p < VNA; ++p) asm volatile("" : "+v"(va[u][p]));   // unpacked per use
+            for (int p = 0; p < VNA; ++p) {
+                // (PK: unpacked per use, not hoisted as twice the registers; the 32-bit
+                // addresses of the multi-chunk instances need no unpacking, and the opaque copy
+                // made them loop-carried values the allocator moved at every iteration's end:
+                // 16 v_mov per wave on C4, BS_VAO)
+                if (PK || !BS_VAO) asm volatile("" : "+v"(va[u][p]));
+            }
             auto vaddr = [&](int f) __attribute__((always_inline)) -> uint32_t {
                 if constexpr (PK) return (f & 1) ? (va[u][f >> 1] >> 16) : (va[u][f >> 1] & 0xFFFFu);
                 else return va[u][f];
@@ -1370,6 +1328,7 @@ k_bs(BsArgs a) {
         }
     }
     vn_phase(true, false, a.off_blut, 0);
+    BS_ST(12);
     // check groups: chunk k of 64 check lanes; lane LPC c + j of it (check c = row i, index h)
     // takes edges k = LPC m + j, at slots first_i + j A_i + m z + h (a.row_lay); edges past the
     // degree read the all-ones PAD slot and are not written; idle lanes (c >= n_checks) read PAD
@@ -1889,8 +1848,8 @@ k_bs(BsArgs a) {
     BS_ST(5);
     if (a.stamps && lane == 0 && wave < 16) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) atomicAdd(a.stamps + 8 * wave + i, (unsigned long long)sacc[i]);
-        atomicAdd(a.stamps + 8 * wave + 6, 1ull);
+        for (int i = 0; i < 13; ++i) atomicAdd(a.stamps + 16 * wave + i, (unsigned long long)sacc[i]);
+        atomicAdd(a.stamps + 16 * wave + 15, 1ull);
     }
 #endif
 #undef BS_ST

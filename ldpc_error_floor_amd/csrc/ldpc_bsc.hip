@@ -24,6 +24,12 @@
 
 #include "ldpc_bs_kernel.h"
 
+// the variable places' edge words not made opaque per use (bsl's BS_VAO; A/B switch, off: the C5
+// build then spills 16-17 VGPRs instead of 7)
+#ifndef BSC_VAO
+#define BSC_VAO 0
+#endif
+
 namespace ldpc {
 namespace bs {
 
@@ -248,7 +254,7 @@ k_bsc(BscArgs a) {
             if (BS_VSKIP && dw[u] < 0) continue;   // no variable chunk at this (wave, u) place
 #pragma unroll
             for (int p = 0; p < DVH; ++p)
-                if (p < dvu) asm volatile("" : "+v"(va[u][p]));
+                if (p < dvu && !BSC_VAO) asm volatile("" : "+v"(va[u][p]));   // (as bsl's BS_VAO)
             const int v = vv[u] < 0 ? -1 : (vv[u] & 0xFFFF);
             const bool counted = v >= 0 && v < a.target_bits;
             uint32_t lw[1][4];

@@ -11,6 +11,7 @@
 #   ablate:CFG:LIB:SET         -DBS_DIAG build, LDPC_DIAG_ABLATE over SET (comma list), timing only
 #   trace                      rocprofv3 kernel-trace summary of the default bench command
 #   prof:CFG                   tools/profile.sh kernel trace + PMC passes of one config
+#   tscale:CFG:T1,T2,...       ms per decode at each iteration count
 #   stamp:CFG:LIB[:NAME=VALUE] per-wave phase clocks of a -DBS_STAMP build (optionally with an env switch)
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -65,6 +66,10 @@ for step in "$@"; do
         echo -n "$a1 ablate=$ab: "; LDPC_DIAG_ABLATE=$ab bench_ms $a1 || { restore; exit 1; }
       done
       restore ;;
+    tscale)
+      # tscale:CFG:T1,T2,...  ms per decode at each iteration count (slope = per iteration,
+      # intercept = the per-pack prologue / epilogue's throughput cost)
+      for T in ${a2//,/ }; do echo -n "$a1 T=$T: "; bench_ms $a1 "--iters $T" || exit 1; done ;;
     stamp)
       # stamp:CFG:LIB[:NAME=VALUE]  a -DBS_STAMP build's per-wave phase clocks (stderr) -> stamp_CFG*.log
       cp $a2 $L || exit 1
