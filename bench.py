@@ -185,6 +185,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--all-kernels", action="store_true",
                     help="also time the non-default kernel and report it under 'kernels'")
+    ap.add_argument("--no-companions", action="store_true",
+                    help="skip the SURVEY 8d companion workloads (C3, C4, C5) a default one-GPU run "
+                         "times after the headline and reports under 'companions'")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -391,12 +394,68 @@ def main():
     if (world == 1 and rank == 0 and not args.no_cpu_baseline and args.config == "C2"
             and args.decoding_type == 2 and args.q_bit == 5):
         out["cpu_baseline"] = cpu_baseline(proto, g, W, cp, T=T)
+    if (world == 1 and not dist_on and not args.no_companions and args.config == "C2"
+            and args.decoding_type == 2 and args.q_bit == 5 and args.kernel == "auto"
+            and args.iters is None and args.snr is None and args.batch == 1 << 20):
+        # the other SURVEY 8d workloads (BASELINE configs[2..4]) timed in the same run, so the
+        # driver's own bench line carries them: decode-only and with the channel generated in
+        # the kernel, each at its own T, weights, SNR and B = 2^20 on this one GPU
+        out["companions"] = {c: time_config(c, dev, steps=3, warmup=1) for c in ("C3", "C4", "C5")}
     if dist_on:
         out["process_group"] = {"backend": dist.get_backend(), "world": dist.get_world_size()}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()
+
+
+def time_config(config, dev, steps=3, warmup=1, B=1 << 20):
+    """One GPU, one SURVEY 8d workload at its own T / weights / SNR: the decode of B resident
+    codewords (HIP events on the decode stream) and the sweep step with the channel generated
+    inside the decoder (ldpc_decode_awgn), with the counters of the timed decodes."""
+    import torch
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    cfg = CONFIGS[config]
+    T, z, snr = cfg["T"], cfg["z"], cfg["snr"]
+    punct, short = cfg.get("punct", (0, 0)), cfg.get("short", (0, 0))
+    proto, g, W, cp = load_problem(T, config)
+    sigma = float(cp.sigma(snr))
+    dec = NMSDecoder(proto, z, W, 2, 5, device=dev, B_max=B)
+    llr = dec.awgn(B, sigma, seed=1076, punct=punct, short=short)
+    counters = torch.zeros(4, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    res = {"workload": f"{config}: {cfg['graph']} QMS q5 T={T} @ {snr} dB, B={B}",
+           "kernel": dec.kernel_info(T)[1]}
+    for mode in ("decode", "e2e_with_rng"):
+        for i in range(warmup):
+            if mode == "decode":
+                dec.decode(llr, T=T, app=False, counters=counters)
+            else:
+                dec.decode_awgn(B, sigma, seed=7 + i, punct=punct, short=short, T=T, counters=counters)
+        torch.cuda.synchronize(dev)
+        counters.zero_()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for i in range(steps):
+            if mode == "decode":
+                dec.decode(llr, T=T, app=False, counters=counters)
+            else:
+                dec.decode_awgn(B, sigma, seed=1077 + i, punct=punct, short=short, T=T, counters=counters)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        c = counters.cpu().tolist()
+        r = {"codewords_per_s": round(B * steps / wall, 1), "ms_per_step": round(1e3 * wall / steps, 3),
+             "kernel_ms": round(ev0.elapsed_time(ev1) / steps, 3),
+             "frame_err_last": c[1], "fer_last": c[1] / (B * steps)}
+        if mode == "decode":
+            res.update(r)
+        else:
+            res[mode] = r
+    del llr, dec
+    torch.cuda.empty_cache()
+    return res
 
 
 def load_profile(name, batch):

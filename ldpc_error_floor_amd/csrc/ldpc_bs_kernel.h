@@ -729,8 +729,17 @@ __device__ __forceinline__ void gen_bytes(const BsGen& g, int64_t pk, int v, int
         D[i] = w;
     }
 }
-// the generator's tables into LDS (every thread of the workgroup; the caller's barrier follows)
+// the generator's tables into LDS (every thread of the workgroup; the caller's barrier follows
+// and, with BS_GENASYNC, retires the global -> LDS copies by its vmcnt(0): one L2 round trip
+// instead of one per 64 NT words, each waited before its store)
+#ifndef BS_GENASYNC
+#define BS_GENASYNC 1
+#endif
 __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
+    if (BS_GENASYNC) {
+        copy_async(g.lds, g.tab, AWGN_TAB_W, __builtin_amdgcn_readfirstlane(tid >> 6), NT);
+        return;
+    }
     for (int w = tid; w < AWGN_TAB_W; w += NT) lds_put(g.lds + 4u * (uint32_t)w, g.tab[w]);
 }
 #ifndef BS_PACKT
@@ -837,6 +846,9 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 #ifndef BS_VAO
 #define BS_VAO 1
 #endif
+#ifndef BS_SKRD
+#define BS_SKRD 1
+#endif
 #ifndef BS_PROPRIO
 #define BS_PROPRIO 0
 #endif
@@ -866,6 +878,8 @@ k_bs(BsArgs a) {
     // pass 2 reads its slots again instead of holding all EPL of them from pass 1 (wide checks:
     // 30 registers at the check phase's peak, where the 80-register C3 build spilled)
     constexpr bool RR = BS_REREAD && EPL >= 6;
+    // the multi-chunk instances read the PAD slot at the positions past a chunk's real ones
+    constexpr bool SKRD = BS_SKRD && CPL > 1 && BS_BSMIN && BS_BSMIN_MC && !RR;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();          // slots are LDS-absolute
 #ifdef BS_STAMP
@@ -1576,7 +1590,11 @@ k_bs(BsArgs a) {
             PH("ck_read", c);
 #pragma unroll
             for (int m = 0; m < EPL; ++m) {
-                if (SKIPM && m >= gmc) {             // padding for the whole chunk
+                if (SKIPM && !SKRD && m >= gmc) {    // padding for the whole chunk
+                    // (SKRD: read like the others -- the PAD slot, every lane the same address,
+                    // a broadcast -- instead of a branch that fills 5 registers per position with
+                    // ~0 at every check phase: 54 v_mov per C4 chunk pair.  Left unset instead,
+                    // the 128-VGPR build spilled)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) Xs[m][i] = ~0u;
                     ns[m] = ~0u;
@@ -1626,8 +1644,9 @@ k_bs(BsArgs a) {
             constexpr bool BSM = BS_BSMIN && !RR && (!SKIPM || BS_BSMIN_MC);
             uint32_t cand[BSM ? EPL : 1];
             if constexpr (BSM) {
+                // (padding positions: ~0, an even count of them over the LPC lanes of a group)
 #pragma unroll
-                for (int m = 1; m < EPL; ++m) par ^= ns[m];     // (padding positions: ~0, an even count)
+                for (int m = 1; m < EPL; ++m) par ^= ns[m];
                 if constexpr (SKIPM) {
                     switch (gmc) {                   // wave-uniform: the chunk's real positions
 #define BS_MIN2_CASE(k)                                                                            \

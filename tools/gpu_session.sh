@@ -23,7 +23,7 @@ L=ldpc_error_floor_amd/libldpc_nms.so
 cp $L $OUT/.lib_default.so
 restore() { cp $OUT/.lib_default.so $L; }
 bench_ms() {   # config, extra args -> prints "ms kernel value"
-  timeout -k 10 300 python bench.py --config $1 --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline $2 > $OUT/.ab.json 2> $OUT/.ab.err || { tail -5 $OUT/.ab.err; return 1; }
+  timeout -k 10 300 python bench.py --config $1 --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-companions $2 > $OUT/.ab.json 2> $OUT/.ab.err || { tail -5 $OUT/.ab.err; return 1; }
   python -c "import json;d=json.load(open('$OUT/.ab.json'));print(d['ms_per_step'], d['config']['kernel'], d['value'], d['counters']['frame_err_last'])"
 }
 for step in "$@"; do
