@@ -297,8 +297,10 @@ namespace bs {
 // to the SIMD with the smallest total and a free wave slot.  A wave's chunks are in descending
 // cost (the first place takes the heaviest: bsc's heavy-degree place).  LDPC_BS_DEAL=0: the
 // previous dealing (heaviest chunk to the least-loaded SIMD, on its emptiest wave).
+// the exact dealing for the one-chunk instances (same box, r6c: C2 4.482 -> 4.458 ms over three
+// rounds; C3's chunks are all but two of one cost, its deal unchanged)
 #ifndef BS_DEAL_DEFAULT
-#define BS_DEAL_DEFAULT 1
+#define BS_DEAL_DEFAULT 2
 #endif
 std::vector<int> deal_chunks(const std::vector<int>& cost, int nw, int cap) {
     const int n = (int)cost.size();

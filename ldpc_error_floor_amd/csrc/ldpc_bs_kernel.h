@@ -849,8 +849,10 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 #ifndef BS_SKRD
 #define BS_SKRD 1
 #endif
+// (-1, default: 3 on the instances whose loop runs PRIO 4 -- wman: same box, r6c, 4.482 ->
+// 4.454 ms over three rounds -- 0 elsewhere: C3 12.71 against 12.75 ms)
 #ifndef BS_PROPRIO
-#define BS_PROPRIO 0
+#define BS_PROPRIO -1
 #endif
 
 // Register budget: the small instances run at 64 VGPRs (WPE 8: three 9-wave workgroups per CU).
@@ -917,7 +919,9 @@ k_bs(BsArgs a) {
         return ucn && (t >= 64 || ((a.ucn_iter >> t) & 1));
     };
 
-    if (BS_PROPRIO > 0) __builtin_amdgcn_s_setprio(BS_PROPRIO);
+    constexpr int PROPRIO = BS_PROPRIO >= 0 ? BS_PROPRIO
+                            : ((BS_PRIO < 0 && VPL == 1 && CPL == 1 && DV >= 6) || BS_PRIO == 4 ? 3 : 0);
+    if (PROPRIO > 0) __builtin_amdgcn_s_setprio(PROPRIO);
     // ---- per-lane variables: slot addresses, variable index, degree bounds of the wave ----------
     uint32_t va[VPL][VNA];
     int vv[VPL], dw[VPL], dwmin[VPL], pcol[VPL];
