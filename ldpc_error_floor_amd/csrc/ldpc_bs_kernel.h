@@ -832,25 +832,32 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 #define BS_BKPF 1
 #endif
 // iteration 0's tables copied asynchronously behind the channel loads (A/B switch; 0: through
-// registers after the channel barrier, with a barrier of their own)
+// registers after the channel barrier, with a barrier of their own; -1, default: on for the
+// one-chunk instances -- with BS_EB C2 4.519 -> 4.482 ms, r6c -- off for the multi-chunk ones,
+// one workgroup per CU, where the two together cost C4 2.2 %: 11.26 against 11.51 ms, r6d)
 #ifndef BS_T0ASYNC
-#define BS_T0ASYNC 1
+#define BS_T0ASYNC -1
 #endif
-// the prologue's first barrier after the first LLR loads are issued (A/B switch; 0: before them)
+// the prologue's first barrier after the first LLR loads are issued (A/B switch; 0: before them;
+// -1: as BS_T0ASYNC)
 #ifndef BS_EB
-#define BS_EB 1
+#define BS_EB -1
 #endif
-// the prologue's wave priority (A/B switch): the channel, tables and first variable phase of a
-// new workgroup compete with the other resident workgroups' iterations, whose check phases run
-// at priority 1-2; at 0 the prologue takes the issue slots they leave
+// the multi-chunk instances' 32-bit edge addresses not made opaque per use (A/B switch, off: 16
+// fewer v_mov per wave and iteration on C4, but 12.04 against 11.26 ms, r6d)
 #ifndef BS_VAO
-#define BS_VAO 1
+#define BS_VAO 0
 #endif
+// the multi-chunk instances read the PAD slot at the positions past a chunk's real ones instead
+// of filling their registers with ~0 behind a branch (C4 11.26 -> 10.84 ms, r6d)
 #ifndef BS_SKRD
 #define BS_SKRD 1
 #endif
-// (-1, default: 3 on the instances whose loop runs PRIO 4 -- wman: same box, r6c, 4.482 ->
-// 4.454 ms over three rounds -- 0 elsewhere: C3 12.71 against 12.75 ms)
+// the prologue's wave priority (A/B switch): the channel, tables and first variable phase of a
+// new workgroup compete with the other resident workgroups' iterations, whose check phases run
+// at priority 1-2, and at 0 take only the issue slots those leave (-1, default: 3 on the
+// instances whose loop runs PRIO 4 -- wman: same box, r6c, 4.482 -> 4.454 ms over three rounds --
+// 0 elsewhere: C3 12.71 against 12.75 ms)
 #ifndef BS_PROPRIO
 #define BS_PROPRIO -1
 #endif
@@ -882,6 +889,8 @@ k_bs(BsArgs a) {
     constexpr bool RR = BS_REREAD && EPL >= 6;
     // the multi-chunk instances read the PAD slot at the positions past a chunk's real ones
     constexpr bool SKRD = BS_SKRD && CPL > 1 && BS_BSMIN && BS_BSMIN_MC && !RR;
+    constexpr bool T0A = BS_T0ASYNC < 0 ? (VPL == 1 && CPL == 1) : BS_T0ASYNC != 0;
+    constexpr bool EBR = BS_EB < 0 ? T0A : BS_EB != 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if ((uint32_t)(uintptr_t)smem != 0u) __builtin_trap();          // slots are LDS-absolute
 #ifdef BS_STAMP
@@ -970,11 +979,11 @@ k_bs(BsArgs a) {
     // channel is generated from the sampler's tables; else after the first variable's LLR loads
     // are issued, so that it waits beside their HBM round trip, BS_EB)
     if constexpr (Q8) gen_tables(a.gen, tid, NT);
-    if (Q8 || !BS_EB) __syncthreads();
+    if (Q8 || !EBR) __syncthreads();
     BS_ST(8);
     uint32_t cs[VPL], cm[VPL][4], bg[VPL];
     int off = 0;
-    if (BS_T0ASYNC) {                    // (retired by the channel barrier's vmcnt(0))
+    if (T0A) {                           // (retired by the channel barrier's vmcnt(0))
         copy_async(a.off_alut, a.alut, AL, wave, NT);
         copy_async(a.off_blut, a.blut, BL, wave, NT);
     }
@@ -1022,7 +1031,7 @@ k_bs(BsArgs a) {
 #pragma unroll
         for (int r = 0; r < PACK; ++r) xv[0][r] = llr_at(r, var_of(0));
     }
-    if (BS_EB) {
+    if (EBR) {
         // (a workgroup barrier without __syncthreads' fence, whose vmcnt(0) would wait for the
         // loads just issued: the LDS writes above complete (lgkmcnt(0)) and the compiler keeps
         // every memory access on its side)
@@ -1089,7 +1098,7 @@ k_bs(BsArgs a) {
             *reinterpret_cast<LdsQ*>(a.off_ch + 16u * (uint32_t)(tid * VPL + u)) = c4;
         }
     }
-    if (!BS_T0ASYNC) {
+    if (!T0A) {
         for (int w = tid; w < AL; w += NT) ALUT[w] = a.alut[w];
         for (int w = tid; w < BL; w += NT) BLUT[w] = a.blut[w];
         __syncthreads();
