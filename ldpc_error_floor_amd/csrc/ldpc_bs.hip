@@ -214,7 +214,8 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
     p.off_red = (uint32_t)o;
     // + the per-iteration frame-error words, rounded to 16 B: the tables after them are read
     // with ds_read_b128 (T = 50 unrounded put them 8 B off: C3 17.8 -> 24.4 ms, C5 61 -> 81 ms)
-    o += 64 + (((size_t)4 * T + 15) & ~(size_t)15);
+    // and the 32 words the variable phases OR their frame-error words into (BS_FLOR)
+    o += 64 + (((size_t)4 * T + 15) & ~(size_t)15) + 4 * BS_FLORW;
     p.off_alut = (uint32_t)o;
     o += (size_t)2 * (k.UCN ? 2 : 1) * p.arows * LUT_W * 4;
     p.off_blut = (uint32_t)o;
@@ -919,7 +920,7 @@ static int bs_bounds_check(const DevGraph& g, const BsPlan& p, const BsHostTable
     // the allocations
     r.in("lds size", lds, (long long)BS_LDS_MAX + 1);
     if ((long long)t.vn.size() != (long long)VPL * NT * VNW) r.fail("vn_tab size", (long long)t.vn.size(), (long long)VPL * NT * VNW);
-    r.lds("RED", p.off_red, 4LL * (16 + T), 0, p.off_alut);
+    r.lds("RED", p.off_red, 4LL * (16 + ((T + 3) & ~3) + BS_FLORW), 0, p.off_alut);
     r.lds("ALUT", p.off_alut, 4 * 2 * AL, 0, p.off_blut);
     r.lds("BLUT", p.off_blut, 4 * 2 * BL, 0, lds);
     r.lds("PAD+ZERO", p.off_pad, 2 * SLOT_B, p.off_slots, p.off_red);

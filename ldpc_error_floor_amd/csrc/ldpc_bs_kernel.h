@@ -853,6 +853,15 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 #ifndef BS_SKRD
 #define BS_SKRD 1
 #endif
+// the variable phases' frame-error words: every lane ORs its word into one of BS_FLORW LDS words
+// (lane & 31: two lanes per word, distinct banks) and wave 0 folds them at the next iteration's
+// top, instead of a wave_or (4 DPP + 4 readlane, ~34 issue cycles) and a lane-0 atomic in every
+// wave (A/B switch; the last iteration keeps the wave reduction, with its APP and bit counts)
+#ifndef BS_FLOR
+#define BS_FLOR 1
+#endif
+static_assert(!BS_FLOR || BS_TIDFREE, "BS_FLOR: wave 0 folds the words with all its lanes");
+#define BS_FLORW 32
 // the prologue's wave priority (A/B switch): the channel, tables and first variable phase of a
 // new workgroup compete with the other resident workgroups' iterations, whose check phases run
 // at priority 1-2, and at 0 take only the issue slots those leave (-1, default: 3 on the
@@ -917,6 +926,7 @@ k_bs(BsArgs a) {
     const int nvalid = (int)min<int64_t>(PACK, a.B - b0);
     const uint32_t valid = (nvalid >= 32) ? 0xFFFFFFFFu : ((1u << nvalid) - 1u);
     uint32_t* RED = reinterpret_cast<uint32_t*>(smem + a.off_red);   // [0] wrong_t, [1] all t, [2] APP > 0, [3] bits
+    const int flor = 16 + ((a.T + 3) & ~3);                         // (BS_FLOR) the 32 OR words
     const int AR = UCN ? 2 * a.arows : a.arows;
     const int AL = AR * LUT_W, BL = a.bcols * BLUT_W;
     uint32_t* ALUT = reinterpret_cast<uint32_t*>(smem + a.off_alut);   // [2][AR][LUT_W]
@@ -975,6 +985,7 @@ k_bs(BsArgs a) {
     }
     if (UCN && tid == 0) lds_put(a.off_hdz, 0u);
     if (tid < 8) RED[tid] = (tid == 1) ? 0xFFFFFFFFu : 0u;
+    if (BS_FLOR && tid < BS_FLORW) RED[flor + tid] = 0u;
     // (the barrier that orders these writes before the channel's flag updates: here when the
     // channel is generated from the sampler's tables; else after the first variable's LLR loads
     // are issued, so that it waits beside their HBM round trip, BS_EB)
@@ -1329,7 +1340,13 @@ k_bs(BsArgs a) {
                 vbody(std::integral_constant<int, SB>{});
             }
         }
-        if (!first) {
+        if (!first && BS_FLOR && !last) {
+            PH("vn_flags", 0);
+            if (!ABL(8)) {
+                const uint32_t la = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 31u;
+                __hip_atomic_fetch_or(RED + flor + la, wr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else if (!first) {
             PH("vn_flags", last ? 100 : 0);
             if (!ABL(8)) wr = wave_or(wr);
             if (last) {
@@ -1487,10 +1504,18 @@ k_bs(BsArgs a) {
             // (every lane of wave 0 writes the same words: a wave-uniform branch, no thread
             // index kept live through the loop; kept in LDS for the iter_wrong export after the
             // loop: a global pointer held through it cost the 64-VGPR build 17 SGPR spill moves)
-            const uint32_t w0 = RED[0];
+            uint32_t w0;
+            if (BS_FLOR) {                    // (the 32 words of iteration t - 1, zeroed again)
+                const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+                uint32_t x = ln < 32u ? RED[flor + ln] : 0u;
+                if (ln < 32u) RED[flor + ln] = 0u;
+                w0 = wave_or(x);
+            } else {
+                w0 = RED[0];
+                RED[0] = 0u;
+            }
             RED[16 + t - 1] = w0;
             RED[1] &= w0;
-            RED[0] = 0u;
         }
         const int nx = (t + 1) & 1;
 #pragma unroll

@@ -151,6 +151,7 @@ k_bsc(BscArgs a) {
     const int nvalid = (int)min<int64_t>(PACK, a.B - b0);
     const uint32_t valid = (nvalid >= 32) ? 0xFFFFFFFFu : ((1u << nvalid) - 1u);
     uint32_t* RED = reinterpret_cast<uint32_t*>(smem + a.off_red);
+    const int flor = 16 + ((a.T + 3) & ~3);                         // (BS_FLOR) the 32 OR words
     const int AL = a.arows * LUT_W, BL = a.bcols * BLUT_W;
     uint32_t* ALUT = reinterpret_cast<uint32_t*>(smem + a.off_alut);
     uint32_t* BLUT = reinterpret_cast<uint32_t*>(smem + a.off_blut);
@@ -238,6 +239,7 @@ k_bsc(BscArgs a) {
     if (tid < 8)
         reinterpret_cast<uint32_t*>(smem + a.off_rec + rec_off((uint32_t)a.n_checks) + (tid >> 2) * REC_Q2)[tid & 3] = 0u;
     if (tid < 8) RED[tid] = (tid == 1) ? 0xFFFFFFFFu : 0u;
+    if (BS_FLOR && tid < BS_FLORW) RED[flor + tid] = 0u;
     for (int w = tid; w < AL; w += NT) ALUT[w] = a.alut[w];
     for (int w = tid; w < BL; w += NT) BLUT[w] = a.blut[w];
     __syncthreads();
@@ -360,7 +362,10 @@ k_bsc(BscArgs a) {
                 vbody(std::integral_constant<int, SB>{});
             }
         }
-        if (!first) {
+        if (!first && BS_FLOR && !last) {    // (bsl's BS_FLOR: one ds_or per lane into 32 words)
+            const uint32_t la = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 31u;
+            __hip_atomic_fetch_or(RED + flor + la, wr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (!first) {
             wr = wave_or(wr);
             if (last) {
                 apos = wave_or(apos);
@@ -435,10 +440,18 @@ k_bsc(BscArgs a) {
 
     for (int t = 0; t < a.T; ++t) {
         if (wave == 0 && t > 0) {               // (all lanes of wave 0, the same words: bsl)
-            const uint32_t w0 = RED[0];
+            uint32_t w0;
+            if (BS_FLOR) {                        // (the 32 words of iteration t - 1, zeroed again)
+                const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+                const uint32_t x = ln < 32u ? RED[flor + ln] : 0u;
+                if (ln < 32u) RED[flor + ln] = 0u;
+                w0 = wave_or(x);
+            } else {
+                w0 = RED[0];
+                RED[0] = 0u;
+            }
             RED[16 + t - 1] = w0;                     // (exported after the loop)
             RED[1] &= w0;
-            RED[0] = 0u;
         }
         const int nx = (t + 1) & 1;
 #pragma unroll
@@ -821,7 +834,8 @@ static BscPlan bsc_plan(const DevGraph& g, int mode, bool ucn, bool per_edge_w, 
         o += (size_t)nv * 24;
         o = (o + 15) & ~(size_t)15;
         q.off_red = (uint32_t)o;
-        o += 64 + (((size_t)4 * T + 15) & ~(size_t)15);   // + the frame-error words (16 B aligned)
+        o += 64 + (((size_t)4 * T + 15) & ~(size_t)15) + 4 * BS_FLORW;   // + the frame-error words
+                                                                       // (16 B aligned), the OR words
         q.off_alut = (uint32_t)o;
         o += (size_t)2 * q.arows * LUT_W * 4;
         q.off_blut = (uint32_t)o;

@@ -12,6 +12,7 @@
 #   trace                      rocprofv3 kernel-trace summary of the default bench command
 #   prof:CFG                   tools/profile.sh kernel trace + PMC passes of one config
 #   tscale:CFG:T1,T2,...       ms per decode at each iteration count
+#   uncor:CFG                  sweep rate with and without the uncorrected-word collection
 #   stamp:CFG:LIB[:NAME=VALUE] per-wave phase clocks of a -DBS_STAMP build (optionally with an env switch)
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -66,6 +67,15 @@ for step in "$@"; do
         echo -n "$a1 ablate=$ab: "; LDPC_DIAG_ABLATE=$ab bench_ms $a1 || { restore; exit 1; }
       done
       restore ;;
+    uncor)
+      # uncor:CFG  the collection sweep's rate against the plain sweep (tools/sweep_c5.py --uncor)
+      # (the Uncor files stay on the box's /tmp: only the sweep JSON comes back)
+      for u in "" "--uncor"; do
+        d=/tmp/r6uncor_$a1${u:+_u}; rm -rf $d
+        timeout -k 10 600 python tools/sweep_c5.py --config $a1 --deep-snrs ${UNCOR_SNRS:-3.0,3.5} --deep ${UNCOR_N:-4194304} --batch 1048576 $u --out $d > $OUT/uncor_$a1${u:+_u}.log 2>&1 || { tail -5 $OUT/uncor_$a1${u:+_u}.log; exit 1; }
+        cp $d/sweep_*.json $OUT/uncor_$a1${u:+_u}.json; ls -la $d >> $OUT/uncor_$a1${u:+_u}.log
+        tail -1 $OUT/uncor_$a1${u:+_u}.log
+      done ;;
     tscale)
       # tscale:CFG:T1,T2,...  ms per decode at each iteration count (slope = per iteration,
       # intercept = the per-pack prologue / epilogue's throughput cost)
