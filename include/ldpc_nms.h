@@ -183,6 +183,14 @@ int ldpc_collect_frames(const uint8_t* flags_dev, int64_t B, uint32_t mask, uint
 int ldpc_gather_rows(const float* src_dev, int64_t n_cols, const int64_t* idx_dev, int64_t n,
                      float* dst_dev, void* stream);
 
+/* Host: the text of write_uncor_file's rows (Print_Functions.py:120-126, np.savetxt with
+   fmt "%.1f", tab-delimited) for n float32 LLR rows of n_cols values: "0.0\t0.0\t0.0\t" then
+   the negated LLRs, byte-identical to np.savetxt's output.  cap must be at least
+   n * LDPC_UNCOR_ROW_BOUND(n_cols); *len = the bytes written. */
+#define LDPC_UNCOR_ROW_BOUND(n_cols) (13 + 48 * (int64_t)(n_cols))
+int ldpc_format_uncor_rows(const float* rows, int64_t n, int64_t n_cols, char* out, int64_t cap,
+                           int64_t* len);
+
 #ifdef __cplusplus
 }
 #endif

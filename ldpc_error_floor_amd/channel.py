@@ -82,9 +82,16 @@ def write_uncor_file(uncor_flag, training_received_data, code_length, path="Unco
                       path)
 
 
-def append_uncor_rows(llr_rows, path="Uncor.txt"):
+def append_uncor_rows(llr_rows, path="Uncor.txt", formatter=None):
     """The row format of ``write_uncor_file`` (``Print_Functions.py:120-126``) for LLR rows
-    [n, N*z] already selected (e.g. collected on the GPU by ``NMSDecoder.collect_uncorrected``)."""
+    [n, N*z] already selected (e.g. collected on the GPU by ``NMSDecoder.collect_uncorrected``).
+    ``formatter``: a callable rows -> the same text as bytes (the native
+    ``NMSDecoder.format_uncor_rows``, ~10x np.savetxt's rate); None = np.savetxt."""
+    if formatter is not None:
+        data = formatter(np.ascontiguousarray(llr_rows, np.float32))
+        with open(path, "ab") as f:
+            f.write(data)
+        return
     rows = np.asarray(llr_rows, np.float64)
     num = rows.shape[0]
     with open(path, "a") as f:

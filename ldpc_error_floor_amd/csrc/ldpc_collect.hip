@@ -8,6 +8,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
 
 #include "ldpc_nms.h"
 
@@ -54,6 +57,79 @@ extern "C" int ldpc_collect_frames(const uint8_t* flags_dev, int64_t B, uint32_t
     hipLaunchKernelGGL(ldpc::k_collect, dim3(grid), dim3(256), 0, s, flags_dev, B, mask, want,
                        idx_dev, cap, reinterpret_cast<unsigned long long*>(count_dev));
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+}
+
+// One value of write_uncor_file's row text: "%.1f" of v (Python's rendering, which is what
+// np.savetxt calls: nan without a sign).  v = -(double)x for a float32 x, so v * 10 is exact
+// in a double (24-bit significand x 10) and rounding it to an integer half to even (adding
+// and taking away 2^52 + 2^51 in the default rounding mode, exact below 2^51) gives the
+// correctly rounded tenths "%.1f" prints.  From 1e14 on (and for inf) the C library's
+// correctly rounded "%.1f" is used instead.
+constexpr uint64_t kTenthsLut = 10000;
+struct TenthsLut {
+    char s[kTenthsLut][8];
+    uint8_t len[kTenthsLut];
+    TenthsLut() {
+        for (uint64_t a = 0; a < kTenthsLut; ++a)
+            len[a] = (uint8_t)std::snprintf(s[a], 8, "%llu.%llu", (unsigned long long)(a / 10),
+                                            (unsigned long long)(a % 10));
+    }
+};
+static const TenthsLut& tenths_lut() {
+    static const TenthsLut lut;
+    return lut;
+}
+
+static inline char* put_tenths(char* p, double v) {
+    const double av = std::fabs(v);
+    if (!(av < 1e14)) {
+        if (std::isnan(v)) {
+            std::memcpy(p, "nan", 3);
+            return p + 3;
+        }
+        return p + std::snprintf(p, 48, "%.1f", v);
+    }
+    const double m = 6755399441055744.0;               // 2^52 + 2^51 (no -ffast-math here)
+    const double t = (av * 10.0 + m) - m;
+    if (std::signbit(v)) *p++ = '-';
+    uint64_t a = (uint64_t)t;
+    if (a < kTenthsLut) {                              // |v| < 1000: "ddd.d" from the table
+        std::memcpy(p, tenths_lut().s[a], 8);
+        return p + tenths_lut().len[a];
+    }
+    const char frac = (char)('0' + a % 10);
+    a /= 10;
+    char d[20];
+    int k = 0;
+    do {
+        d[k++] = (char)('0' + a % 10);
+        a /= 10;
+    } while (a);
+    while (k) *p++ = d[--k];
+    *p++ = '.';
+    *p++ = frac;
+    return p;
+}
+
+extern "C" int ldpc_format_uncor_rows(const float* rows, int64_t n, int64_t n_cols, char* out,
+                                      int64_t cap, int64_t* len) {
+    if (!len || n < 0 || n_cols <= 0 || (n > 0 && (!rows || !out))) return LDPC_ERR_ARG;
+    *len = 0;
+    if (cap < n * LDPC_UNCOR_ROW_BOUND(n_cols)) return LDPC_ERR_ARG;
+    char* p = out;
+    const TenthsLut& lut = tenths_lut();
+    (void)lut;
+    for (int64_t r = 0; r < n; ++r) {
+        std::memcpy(p, "0.0\t0.0\t0.0\t", 12);
+        p += 12;
+        const float* x = rows + r * n_cols;
+        for (int64_t c = 0; c < n_cols; ++c) {
+            p = put_tenths(p, -(double)x[c]);
+            *p++ = c + 1 < n_cols ? '\t' : '\n';
+        }
+    }
+    *len = (int64_t)(p - out);
+    return LDPC_OK;
 }
 
 extern "C" int ldpc_gather_rows(const float* src_dev, int64_t n_cols, const int64_t* idx_dev,

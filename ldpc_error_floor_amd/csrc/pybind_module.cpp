@@ -5,6 +5,7 @@
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -220,4 +221,28 @@ PYBIND11_MODULE(_ldpc_nms, m) {
             return std::string(name);
         },
         py::arg("ctx"));
+    m.def(
+        "format_uncor_rows",
+        [](py::array_t<float, py::array::c_style | py::array::forcecast> rows) {
+            if (rows.ndim() != 2 || rows.shape(1) <= 0)
+                throw std::invalid_argument("rows must be [n, n_cols] with n_cols > 0");
+            const int64_t n = rows.shape(0), nc = rows.shape(1);
+            const int64_t step = std::max<int64_t>(1, (64 << 20) / LDPC_UNCOR_ROW_BOUND(nc));
+            std::string out, buf;
+            out.reserve((size_t)(n * (12 + 6 * nc)));
+            buf.resize((size_t)(std::min(n, step) * LDPC_UNCOR_ROW_BOUND(nc)));
+            {
+                py::gil_scoped_release nogil;
+                for (int64_t r0 = 0; r0 < n; r0 += step) {
+                    const int64_t k = std::min(step, n - r0);
+                    int64_t len = 0;
+                    check(ldpc_format_uncor_rows(rows.data() + r0 * nc, k, nc, buf.data(),
+                                                 (int64_t)buf.size(), &len),
+                          "ldpc_format_uncor_rows");
+                    out.append(buf.data(), (size_t)len);
+                }
+            }
+            return py::bytes(out);
+        },
+        py::arg("rows"));
 }

@@ -289,6 +289,11 @@ class NMSDecoder:
                                   rows[s0:].data_ptr(), stream.cuda_stream)
         return rows.cpu().numpy()
 
+    def format_uncor_rows(self, rows):
+        """``write_uncor_file``'s text for float32 LLR rows [n, N*z] as bytes, formatted by the
+        native ``ldpc_format_uncor_rows`` (byte-identical to np.savetxt with "%.1f")."""
+        return self._ext.format_uncor_rows(rows)
+
     def awgn(self, B: int, sigma: float, seed: int, offset: int = 0, punct=None, short=None,
              out=None, stream=None):
         """On-GPU AWGN LLRs [B, N*z] for the all-zero word (Philox, see ldpc_channel.hip).

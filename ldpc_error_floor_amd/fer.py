@@ -307,7 +307,7 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
                 if flags is not None:
                     rows = decoder.collect_uncorrected(flags[:b], llr[:b])
                     if rows.shape[0]:
-                        append_uncor_rows(rows, upath)
+                        append_uncor_rows(rows, upath, formatter=decoder.format_uncor_rows)
             pos += b
             nb += 1
             if ck is not None and checkpoint_every > 0 and nb % checkpoint_every == 0 and pos < end:
@@ -461,7 +461,7 @@ def collect_uncor_inputs(decoder, sigma, filename, counts=(10000, 5000, 5000), o
             rows = decoder.collect_uncorrected(flags, llr)
             if rows.shape[0]:
                 rows = rows[:need - have]
-                append_uncor_rows(rows, path)
+                append_uncor_rows(rows, path, formatter=decoder.format_uncor_rows)
                 have += rows.shape[0]
             pos += batch
         if need == 0:

@@ -1,10 +1,35 @@
 """Test-only helpers: host counters from APP, and an oracle-backed stand-in decoder used to
 exercise the host logic (Session, FER loops, sharding) on CPU.  Never used by the product."""
+import ctypes
+import os
 from types import SimpleNamespace
 
 import numpy as np
 
 from oracle import nms_oracle
+
+
+_LIB = None
+
+
+def native_format_uncor_rows(rows):
+    """``ldpc_format_uncor_rows`` of the C-ABI library (host code, no GPU) through ctypes."""
+    global _LIB
+    if _LIB is None:
+        _LIB = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "ldpc_error_floor_amd", "libldpc_nms.so"))
+        _LIB.ldpc_format_uncor_rows.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                                ctypes.c_void_p, ctypes.c_int64,
+                                                ctypes.POINTER(ctypes.c_int64)]
+    rows = np.ascontiguousarray(rows, np.float32)
+    n, nc = rows.shape
+    cap = n * (13 + 48 * nc)
+    buf = ctypes.create_string_buffer(max(cap, 1))
+    ln = ctypes.c_int64()
+    st = _LIB.ldpc_format_uncor_rows(rows.ctypes.data, n, nc, buf, cap, ctypes.byref(ln))
+    if st != 0:
+        raise RuntimeError(f"ldpc_format_uncor_rows: {st}")
+    return buf.raw[:ln.value]
 
 
 def counters_from_app(app):
@@ -57,6 +82,9 @@ class OracleDecoder:
     def collect_uncorrected(self, flags, llr):
         sel = (flags.cpu().numpy() & 1) == 1
         return np.asarray(llr.cpu().numpy(), np.float32).reshape(llr.shape[0], -1)[sel]
+
+    def format_uncor_rows(self, rows):
+        return native_format_uncor_rows(rows)
 
     def awgn(self, B, sigma, seed, offset=0, punct=(0, 0), short=(0, 0), out=None, **kw):
         # deterministic per global codeword index (like the GPU Philox stream)
