@@ -858,7 +858,8 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
         const double n = (double)(hst[16 * w + 15] ? hst[16 * w + 15] : 1);
         fprintf(stderr, "  wave %2d:", w);
         for (const int i : order) fprintf(stderr, " %8.0f", hst[16 * w + i] / n);
-        fprintf(stderr, "\n");
+        fprintf(stderr, "  | SIMD %5.3f %5.3f %5.3f %5.3f\n", (hst[16 * w + 13] & 0xFFFFFFFFull) / n,
+                (hst[16 * w + 13] >> 32) / n, (hst[16 * w + 14] & 0xFFFFFFFFull) / n, (hst[16 * w + 14] >> 32) / n);
     }
     return st;
 #else

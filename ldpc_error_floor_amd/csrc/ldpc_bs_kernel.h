@@ -985,6 +985,13 @@ k_bs(BsArgs a) {
     }
     if (UCN && tid == 0) lds_put(a.off_hdz, 0u);
     if (tid < 8) RED[tid] = (tid == 1) ? 0xFFFFFFFFu : 0u;
+#ifdef BS_STAMP
+    if (tid == 0) {
+        uint32_t hw0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw0));
+        RED[12] = (hw0 >> 4) & 3u;
+    }
+#endif
     if (BS_FLOR && tid < BS_FLORW) RED[flor + tid] = 0u;
     // (the barrier that orders these writes before the channel's flag updates: here when the
     // channel is generated from the sampler's tables; else after the first variable's LLR loads
@@ -1907,6 +1914,12 @@ k_bs(BsArgs a) {
 #pragma unroll
         for (int i = 0; i < 13; ++i) atomicAdd(a.stamps + 16 * wave + i, (unsigned long long)sacc[i]);
         atomicAdd(a.stamps + 16 * wave + 15, 1ull);
+        // the SIMD this wave ran on (HW_ID bits 5:4) relative to wave 0's (RED[12]): counts in
+        // 32-bit fields, offsets 0-1 in word 13, 2-3 in word 14
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        const uint32_t simd = (((hw >> 4) & 3u) - RED[12]) & 3u;
+        atomicAdd(a.stamps + 16 * wave + 13 + (simd >> 1), 1ull << (32 * (simd & 1)));
     }
 #endif
 #undef BS_ST
