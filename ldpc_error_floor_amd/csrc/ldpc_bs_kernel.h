@@ -54,8 +54,16 @@ constexpr size_t BS_LDS_MAX = 160 * 1024;
 // shortened bits supported, PK = 16-bit packed slot addresses, WPE = waves per SIMD (registers),
 // NW = waves of the multi-chunk instances (VPL / CPL > 1)
 struct BsInst { int D, DV, LPC, VPL, CPL; bool UCN, BIG, PK; int WPE; int NW = 16; };
+// cache policy of the LLR loads (the aux operand of the buffer loads: 2 = nt, streaming: the
+// read-once LLR blocks then leave the graph tables in L2; A/B switch)
+#ifndef BS_LLR_CPOL
+#define BS_LLR_CPOL 0
+#endif
+#ifndef BS_WMAN_WPE
+#define BS_WMAN_WPE 8
+#endif
 constexpr BsInst kBsInst[] = {
-    {15, 6, 4, 1, 1, false, false, true, 8},     // wman (C2), LPC 4 measured 6.31 ms vs 6.73
+    {15, 6, 4, 1, 1, false, false, true, BS_WMAN_WPE},     // wman (C2), LPC 4 measured 6.31 ms vs 6.73
     {16, 8, 4, 1, 1, false, false, true, 8},
     {15, 6, 2, 1, 1, false, false, true, 8},     // LDPC_BS_LPC=2 A/B
     {24, 4, 4, 1, 1, true, true, true, 6},       // 802.11n (C3): degree 22, UCN
@@ -748,9 +756,12 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 
 // first-generation start spread of the one-workgroup-per-CU instances, microseconds (bs_stagger)
 // (bsl's one-workgroup-per-CU instances: 5G BG2 (C4) 13.93 -> 13.78 ms at 100 us, 50 / 200 us
-// in between, same box, r3ze; bsc: no effect, so it passes one_per_cu = false and starts at 0)
+// in between, same box, r3ze; bsc: no effect, so it passes one_per_cu = false and starts at 0).
+// Round 6, with C4's packs at ~82 us: 60 us 10.47 / 10.53 ms against 100 us 10.52 and 0 us 10.56
+// (two boxes, profiles/r6/session_r6l.log, r6m; 30-80 us equal within 0.2 %; C5 no gain at 180 /
+// 360 us)
 #ifndef BS_STAGGER_US
-#define BS_STAGGER_US 100.0
+#define BS_STAGGER_US 60.0
 #endif
 // the check lane's slot base and alpha-table address packed in one register (16-bit-address
 // one-chunk instances; ldpc_bs.hip checks that the tables end below 64 KB)
@@ -1018,7 +1029,7 @@ k_bs(BsArgs a) {
         (void*)(a.llr + b0 * nv), 0, nvalid * nv * 4, 0x00020000);
     auto llr_at = [&](int r, int v) __attribute__((always_inline)) -> float {
         if (BS_BUFLD)
-            return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(llr_rs, 4 * v, 4 * r * nv, 0));
+            return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(llr_rs, 4 * v, 4 * r * nv, BS_LLR_CPOL));
         return a.llr[(b0 + min(r, nvalid - 1)) * nv + v];
     };
     auto var_of = [&](int u) __attribute__((always_inline)) -> int {

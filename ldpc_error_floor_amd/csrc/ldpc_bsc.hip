@@ -208,7 +208,7 @@ k_bsc(BscArgs a) {
             float xv[PACK];
 #pragma unroll
             for (int r = 0; r < PACK; ++r)
-                xv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(llr_rs, 4 * v, 4 * r * nv, 0));
+                xv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(llr_rs, 4 * v, 4 * r * nv, BS_LLR_CPOL));
             if (BS_PACKT) {
                 off |= pack_channel<true>(xv, a.inv, a.qmax, a.cu, valid, cs[u], cm[u], bg[u]);
                 continue;
