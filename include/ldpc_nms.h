@@ -169,6 +169,15 @@ int ldpc_decode_awgn(ldpc_ctx* ctx, int64_t B, const ldpc_decode_params* params,
 int ldpc_awgn_in_kernel(const ldpc_ctx* ctx, const ldpc_decode_params* params, int32_t has_short,
                         int32_t app);
 
+/* The LLR rows ldpc_channel_awgn(B, ..., offset) would write at batch rows idx_dev[0..n) (each
+   index < B, any order), into rows_dev[n][n_vars]: the same values bit for bit, generated for
+   those codewords only -- the uncorrected-word sweep regenerates the few failing frames' rows
+   after a decode whose channel was generated inside the kernel (ldpc_decode_awgn). */
+int ldpc_channel_awgn_rows(float* rows_dev, const int64_t* idx_dev, int64_t n, int32_t n_vars,
+                           double sigma, uint64_t seed, int64_t offset, int32_t decoding_type,
+                           int32_t q_bit, int32_t punct_start, int32_t punct_end,
+                           int32_t short_start, int32_t short_end, float clip_llr, void* stream);
+
 /* Uncorrected-frame collection for the on-device sweep (replaces the host selection in
    compute_results -> write_uncor_file, Print_Functions.py:155-156 and :120-126).
    Writes the indices b < B with (frame_flags[b] & mask) == want into idx_dev[0..cap) (order

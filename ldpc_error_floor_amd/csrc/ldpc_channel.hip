@@ -88,6 +88,32 @@ __global__ void __launch_bounds__(256) k_awgn_qf(float* __restrict__ out, int64_
     }
 }
 
+// the rows of an index list: rows[r] = the LLR row ldpc_channel_awgn writes for batch codeword
+// idx[r] (global index a.offset + idx[r]), one thread per element; for the few frames an
+// uncorrected-word sweep collects after a decode whose channel never left the kernel
+// (QMS: awgn_qms_elem, the level sampler's stream by a linear threshold scan)
+__global__ void __launch_bounds__(256) k_awgn_rows(float* __restrict__ out, const int64_t* __restrict__ idx,
+                                                   int64_t n, int n_vars, AwgnParams a) {
+    const bool qms = a.decoding_type == LDPC_DEC_QMS;
+    const int per = qms ? n_vars : (n_vars + 1) / 2;
+    const int64_t total = n * per;
+    for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
+         id += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = id / per;
+        const int k = (int)(id - r * per);
+        const int64_t b = idx[r];
+        float* row = out + r * n_vars;
+        if (qms) {
+            row[k] = awgn_qms_elem(a, (uint64_t)(a.offset + b), k);
+        } else {
+            float l[2];
+            awgn_pair(a, b, k, l);
+            row[2 * k] = l[0];
+            if (2 * k + 1 < n_vars) row[2 * k + 1] = l[1];
+        }
+    }
+}
+
 void awgn_gen_table(const AwgnParams& a, uint32_t* out) {
     constexpr int NB = 1 << AWGN_KB;
     for (int b = 0; b < NB; ++b) {
@@ -163,3 +189,24 @@ extern "C" int ldpc_channel_awgn(float* llr_dev, int64_t B, int32_t n_vars, doub
     return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
 }
 
+
+extern "C" int ldpc_channel_awgn_rows(float* rows_dev, const int64_t* idx_dev, int64_t n, int32_t n_vars,
+                                      double sigma, uint64_t seed, int64_t offset, int32_t decoding_type,
+                                      int32_t q_bit, int32_t punct_start, int32_t punct_end,
+                                      int32_t short_start, int32_t short_end, float clip_llr,
+                                      void* stream) {
+    if (n < 0 || (n > 0 && (!rows_dev || !idx_dev))) return LDPC_ERR_ARG;
+    const int chk = ldpc::host::check_channel(1, n_vars, sigma, offset, decoding_type, q_bit,
+                                              punct_start, punct_end, short_start, short_end,
+                                              clip_llr);
+    if (chk != LDPC_OK) return chk;
+    if (n == 0) return LDPC_OK;
+    const ldpc::AwgnParams a = ldpc::make_awgn(sigma, seed, offset, decoding_type, q_bit,
+                                               punct_start, punct_end, short_start, short_end,
+                                               clip_llr);
+    const int64_t per = decoding_type == LDPC_DEC_QMS ? n_vars : (n_vars + 1) / 2;
+    const unsigned grid = (unsigned)std::min<int64_t>(8192, (n * per + 255) / 256);
+    hipLaunchKernelGGL(ldpc::k_awgn_rows, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       rows_dev, idx_dev, n, (int)n_vars, a);
+    return hipGetLastError() == hipSuccess ? LDPC_OK : LDPC_ERR_HIP;
+}

@@ -169,6 +169,20 @@ PYBIND11_MODULE(_ldpc_nms, m) {
         py::arg("punct_end"), py::arg("short_start"), py::arg("short_end"), py::arg("clip"),
         py::arg("stream") = 0);
     m.def(
+        "channel_awgn_rows",
+        [](uintptr_t rows, uintptr_t idx, int64_t n, int n_vars, double sigma, uint64_t seed,
+           int64_t offset, int decoding_type, int q_bit, int ps, int pe, int ss, int se, float clip,
+           uintptr_t stream) {
+            check(ldpc_channel_awgn_rows(reinterpret_cast<float*>(rows), reinterpret_cast<const int64_t*>(idx),
+                                         n, n_vars, sigma, seed, offset, decoding_type, q_bit, ps, pe,
+                                         ss, se, clip, reinterpret_cast<void*>(stream)),
+                  "ldpc_channel_awgn_rows");
+        },
+        py::arg("rows"), py::arg("idx"), py::arg("n"), py::arg("n_vars"), py::arg("sigma"),
+        py::arg("seed"), py::arg("offset"), py::arg("decoding_type"), py::arg("q_bit"),
+        py::arg("punct_start"), py::arg("punct_end"), py::arg("short_start"), py::arg("short_end"),
+        py::arg("clip"), py::arg("stream") = 0);
+    m.def(
         "collect_frames",
         [](uintptr_t flags, int64_t B, uint32_t mask, uint32_t want, uintptr_t idx, int64_t cap,
            uintptr_t count, uintptr_t stream) {

@@ -264,13 +264,9 @@ class NMSDecoder:
                               stream.cuda_stream, ptr(res.iter_wrong))
         return res
 
-    def collect_uncorrected(self, flags, llr, stream=None):
-        """LLR rows (host float32 [n, N*z], batch order) of the frames wrong at every iteration
-        (``frame_flags`` bit 0 = the reference's ``uncor_flag``), compacted on the GPU by
-        ``ldpc_collect_frames`` + ``ldpc_gather_rows``; only the n rows cross PCIe."""
+    def _uncorrected_index(self, flags, stream):
+        """Batch indices (sorted, on the device) of the frames wrong at every iteration."""
         torch = self._torch
-        if stream is None:
-            stream = torch.cuda.current_stream(self.device)
         B = int(flags.shape[0])
         idx = torch.empty(max(B, 1), dtype=torch.int64, device=self.device)
         cnt = torch.empty(1, dtype=torch.int64, device=self.device)
@@ -278,15 +274,46 @@ class NMSDecoder:
                                  stream.cuda_stream)
         stream.synchronize()
         n = int(cnt.item())
+        return torch.sort(idx[:n]).values.contiguous()     # batch order, as the reference writes
+
+    def collect_uncorrected(self, flags, llr, stream=None):
+        """LLR rows (host float32 [n, N*z], batch order) of the frames wrong at every iteration
+        (``frame_flags`` bit 0 = the reference's ``uncor_flag``), compacted on the GPU by
+        ``ldpc_collect_frames`` + ``ldpc_gather_rows``; only the n rows cross PCIe."""
+        torch = self._torch
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        sel = self._uncorrected_index(flags, stream)
+        n = int(sel.numel())
         if n == 0:
             return np.zeros((0, self.n_vars), np.float32)
-        sel = torch.sort(idx[:n]).values.contiguous()     # batch order, as the reference writes
         llr = llr.reshape(llr.shape[0], -1)
         rows = torch.empty((n, self.n_vars), dtype=torch.float32, device=self.device)
         for s0 in range(0, n, 65535):
             s1 = min(n, s0 + 65535)
             self._ext.gather_rows(llr.data_ptr(), self.n_vars, sel[s0:].data_ptr(), s1 - s0,
                                   rows[s0:].data_ptr(), stream.cuda_stream)
+        return rows.cpu().numpy()
+
+    def collect_uncorrected_awgn(self, flags, sigma: float, seed: int, offset: int = 0,
+                                 punct=None, short=None, stream=None):
+        """``collect_uncorrected`` after ``decode_awgn``: the failing frames' LLR rows
+        regenerated from the channel (``ldpc_channel_awgn_rows``, the same values ``awgn`` would
+        have written), so the sweep keeps the in-kernel channel while collecting."""
+        torch = self._torch
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        punct = getattr(self, "punct", (0, 0)) if punct is None else punct
+        short = getattr(self, "short", (0, 0)) if short is None else short
+        sel = self._uncorrected_index(flags, stream)
+        n = int(sel.numel())
+        if n == 0:
+            return np.zeros((0, self.n_vars), np.float32)
+        rows = torch.empty((n, self.n_vars), dtype=torch.float32, device=self.device)
+        self._ext.channel_awgn_rows(rows.data_ptr(), sel.data_ptr(), n, self.n_vars, float(sigma),
+                                    int(seed), int(offset), self.decoding_type, self.q_bit,
+                                    int(punct[0]), int(punct[1]), int(short[0]), int(short[1]),
+                                    self.clip, stream.cuda_stream)
         return rows.cpu().numpy()
 
     def format_uncor_rows(self, rows):

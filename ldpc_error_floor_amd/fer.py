@@ -205,7 +205,11 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
     short = tuple(getattr(decoder, "short", (0, 0)) if short is None else short)
     counters = torch.zeros((sigmas.size, 4), dtype=torch.int64, device=dev)
     begin, end = shard_range(int(n_codewords), rank, world)
-    fused_channel = uncor_path is None and hasattr(decoder, "decode_awgn")
+    # the channel generated inside the decoder (ldpc_decode_awgn) unless the decoder cannot;
+    # collecting uncorrected words then regenerates only the failing frames' rows
+    # (collect_uncorrected_awgn: the same values the HBM channel would hold)
+    fused_channel = hasattr(decoder, "decode_awgn") and (
+        uncor_path is None or hasattr(decoder, "collect_uncorrected_awgn"))
     llr = None if fused_channel else torch.empty((batch, decoder.n_vars), dtype=torch.float32,
                                                  device=dev)
     flags = torch.empty(batch, dtype=torch.uint8, device=dev) if uncor_path else None
@@ -265,7 +269,7 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
         # and rows earlier sweeps appended to a shared file stay (Print_Functions.py:122 appends)
         save(si0, pos0)
 
-    if fused_channel and overlap and _pipelines(decoder, T, kernel):
+    if fused_channel and upath is None and overlap and _pipelines(decoder, T, kernel):
         # the channel of batch j + 1 on a second stream while batch j decodes (the decoder reads
         # its LLRs from HBM, so ldpc_decode_awgn would run the two kernels back to back)
         jobs = [(si, pos, min(batch, end - pos)) for si in range(si0, sigmas.size)
@@ -298,7 +302,13 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
             if fused_channel:
                 # LLRs generated inside the decoder (ldpc_decode_awgn): no HBM round trip
                 decoder.decode_awgn(b, float(sigma), point_seeds[si], offset=pos, punct=punct,
-                                    short=short, T=T, counters=counters[si], kernel=kernel)
+                                    short=short, T=T, counters=counters[si], kernel=kernel,
+                                    flags=None if flags is None else flags[:b])
+                if flags is not None:
+                    rows = decoder.collect_uncorrected_awgn(flags[:b], float(sigma), point_seeds[si],
+                                                            offset=pos, punct=punct, short=short)
+                    if rows.shape[0]:
+                        append_uncor_rows(rows, upath, formatter=decoder.format_uncor_rows)
             else:
                 decoder.awgn(b, float(sigma), point_seeds[si], offset=pos, punct=punct,
                              short=short, out=llr[:b])
