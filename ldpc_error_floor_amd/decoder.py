@@ -305,16 +305,17 @@ class NMSDecoder:
             stream = torch.cuda.current_stream(self.device)
         punct = getattr(self, "punct", (0, 0)) if punct is None else punct
         short = getattr(self, "short", (0, 0)) if short is None else short
-        sel = self._uncorrected_index(flags, stream)
-        n = int(sel.numel())
-        if n == 0:
-            return np.zeros((0, self.n_vars), np.float32)
-        rows = torch.empty((n, self.n_vars), dtype=torch.float32, device=self.device)
-        self._ext.channel_awgn_rows(rows.data_ptr(), sel.data_ptr(), n, self.n_vars, float(sigma),
-                                    int(seed), int(offset), self.decoding_type, self.q_bit,
-                                    int(punct[0]), int(punct[1]), int(short[0]), int(short[1]),
-                                    self.clip, stream.cuda_stream)
-        return rows.cpu().numpy()
+        with torch.cuda.stream(stream):          # (allocations and the copy on `stream`)
+            sel = self._uncorrected_index(flags, stream)
+            n = int(sel.numel())
+            if n == 0:
+                return np.zeros((0, self.n_vars), np.float32)
+            rows = torch.empty((n, self.n_vars), dtype=torch.float32, device=self.device)
+            self._ext.channel_awgn_rows(rows.data_ptr(), sel.data_ptr(), n, self.n_vars, float(sigma),
+                                        int(seed), int(offset), self.decoding_type, self.q_bit,
+                                        int(punct[0]), int(punct[1]), int(short[0]), int(short[1]),
+                                        self.clip, stream.cuda_stream)
+            return rows.cpu().numpy()
 
     def format_uncor_rows(self, rows):
         """``write_uncor_file``'s text for float32 LLR rows [n, N*z] as bytes, formatted by the

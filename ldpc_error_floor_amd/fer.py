@@ -292,6 +292,22 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
             if ck is not None and si not in nbs:
                 save(si + 1, begin, done=(si + 1 == sigmas.size))
         si0 = sigmas.size
+    # the collection on the in-kernel channel: batch j's failing rows are regenerated, copied and
+    # written (side stream, host) while batch j + 1 decodes; two frame-flag buffers
+    side, flag_bufs, pending = None, None, []
+    if fused_channel and flags is not None:
+        side = torch.cuda.Stream(dev)
+        flag_bufs = [flags, torch.empty_like(flags)]
+
+    def flush():
+        while pending:
+            fb, sg, ps, p0, ev = pending.pop(0)
+            side.wait_event(ev)
+            rows = decoder.collect_uncorrected_awgn(fb, sg, ps, offset=p0, punct=punct, short=short,
+                                                    stream=side)
+            if rows.shape[0]:
+                append_uncor_rows(rows, upath, formatter=decoder.format_uncor_rows)
+
     for si, sigma in enumerate(sigmas):
         if si < si0:
             continue
@@ -301,14 +317,14 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
             b = min(batch, end - pos)
             if fused_channel:
                 # LLRs generated inside the decoder (ldpc_decode_awgn): no HBM round trip
+                fb = None if flag_bufs is None else flag_bufs[nb % 2][:b]
                 decoder.decode_awgn(b, float(sigma), point_seeds[si], offset=pos, punct=punct,
-                                    short=short, T=T, counters=counters[si], kernel=kernel,
-                                    flags=None if flags is None else flags[:b])
-                if flags is not None:
-                    rows = decoder.collect_uncorrected_awgn(flags[:b], float(sigma), point_seeds[si],
-                                                            offset=pos, punct=punct, short=short)
-                    if rows.shape[0]:
-                        append_uncor_rows(rows, upath, formatter=decoder.format_uncor_rows)
+                                    short=short, T=T, counters=counters[si], kernel=kernel, flags=fb)
+                if fb is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream(dev))
+                    flush()                       # the previous batch, while this one decodes
+                    pending.append((fb, float(sigma), point_seeds[si], pos, ev))
             else:
                 decoder.awgn(b, float(sigma), point_seeds[si], offset=pos, punct=punct,
                              short=short, out=llr[:b])
@@ -321,9 +337,11 @@ def fer_sweep(decoder, sigmas, n_codewords: int, batch: int, seed: int = 1076, T
             pos += b
             nb += 1
             if ck is not None and checkpoint_every > 0 and nb % checkpoint_every == 0 and pos < end:
+                flush()                           # (the file holds every batch up to pos)
                 save(si, pos)
             if progress:
                 progress(si, pos - begin, end - begin)
+        flush()
         if upath is not None:
             marks[si + 1] = fsize(upath)
         if ck is not None:

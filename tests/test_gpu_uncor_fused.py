@@ -94,3 +94,20 @@ def test_sweep_file_equals_hbm_channel_file(cuda_device, tmp_path):
                 append_uncor_rows(rows, str(exp), formatter=dec.format_uncor_rows)
     assert path.read_bytes() == exp.read_bytes()
     assert sum(x.frame_err_all for x in res) == path.read_bytes().count(b"\n") > 0
+
+
+def test_sweep_checkpointed_and_resumed_file(cuda_device, tmp_path):
+    """With a checkpoint after every batch (the deferred collection flushed before each save) and
+    a resume of the finished sweep, the file and the counters equal the uninterrupted run's."""
+    from ldpc_error_floor_amd.fer import fer_sweep
+    dec, cp, punct, short = _decoder("wman_qms", cuda_device)
+    sigmas = [float(cp.sigma(1.5))]
+    a, b = tmp_path / "a.txt", tmp_path / "b.txt"
+    ra = fer_sweep(dec, sigmas, 4500, 1024, seed=9, uncor_path=str(a))
+    rb = fer_sweep(dec, sigmas, 4500, 1024, seed=9, uncor_path=str(b),
+                   checkpoint=str(tmp_path / "ck.json"), checkpoint_every=1)
+    assert a.read_bytes() == b.read_bytes() and a.stat().st_size > 0
+    rc = fer_sweep(dec, sigmas, 4500, 1024, seed=9, uncor_path=str(b),
+                   checkpoint=str(tmp_path / "ck.json"), checkpoint_every=1, resume=True)
+    assert a.read_bytes() == b.read_bytes()
+    assert [x.frame_err_all for x in ra] == [x.frame_err_all for x in rb] == [x.frame_err_all for x in rc]
