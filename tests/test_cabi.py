@@ -71,3 +71,29 @@ def test_argument_validation_without_gpu(lib):
                                       ctypes.c_double, ctypes.c_uint64, ctypes.c_int64] + \
         [ctypes.c_int32] * 6 + [ctypes.c_float, ctypes.c_void_p]
     assert lib.ldpc_channel_awgn(None, 4, 10, 0.5, 1, 0, 2, 5, 0, 0, 0, 0, 20.0, None) == -1
+
+
+def test_row_writer_and_row_channel_validation_without_gpu(lib):
+    """ldpc_format_uncor_rows checks its capacity and arguments; ldpc_channel_awgn_rows rejects
+    bad arguments before any launch (and n = 0 is a no-op)."""
+    import numpy as np
+    f = lib.ldpc_format_uncor_rows
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                  ctypes.POINTER(ctypes.c_int64)]
+    rows = np.zeros((2, 3), np.float32)
+    ln = ctypes.c_int64(-5)
+    small = ctypes.create_string_buffer(10)
+    assert f(rows.ctypes.data, 2, 3, small, 10, ctypes.byref(ln)) == -1 and ln.value == 0
+    assert f(rows.ctypes.data, 2, 0, small, 10, ctypes.byref(ln)) == -1
+    assert f(rows.ctypes.data, 2, 3, small, 10, None) == -1
+    cap = 2 * (13 + 48 * 3)
+    buf = ctypes.create_string_buffer(cap)
+    assert f(rows.ctypes.data, 2, 3, buf, cap, ctypes.byref(ln)) == 0
+    assert buf.raw[:ln.value] == b"0.0\t0.0\t0.0\t-0.0\t-0.0\t-0.0\n" * 2
+    g = lib.ldpc_channel_awgn_rows
+    g.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double,
+                  ctypes.c_uint64, ctypes.c_int64] + [ctypes.c_int32] * 6 + [ctypes.c_float, ctypes.c_void_p]
+    assert g(None, None, 4, 10, 0.5, 1, 0, 2, 5, 0, 0, 0, 0, 20.0, None) == -1   # no buffers
+    assert g(None, None, -1, 10, 0.5, 1, 0, 2, 5, 0, 0, 0, 0, 20.0, None) == -1  # n < 0
+    assert g(None, None, 0, 10, -0.5, 1, 0, 2, 5, 0, 0, 0, 0, 20.0, None) == -1  # sigma <= 0
+    assert g(None, None, 0, 10, 0.5, 1, 0, 2, 5, 0, 0, 0, 0, 20.0, None) == 0    # nothing to do
