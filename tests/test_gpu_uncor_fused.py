@@ -111,3 +111,25 @@ def test_sweep_checkpointed_and_resumed_file(cuda_device, tmp_path):
                    checkpoint=str(tmp_path / "ck.json"), checkpoint_every=1, resume=True)
     assert a.read_bytes() == b.read_bytes()
     assert [x.frame_err_all for x in ra] == [x.frame_err_all for x in rb] == [x.frame_err_all for x in rc]
+
+
+@pytest.mark.parametrize("q_bit", [6, -5, 4, 3])
+def test_channel_rows_every_quantizer(cuda_device, q_bit):
+    """The rows of the index list on every QMS grid (the level sampler's thresholds differ per
+    q_bit), MS fp32 included (q = 5 decoder, decoding type 1)."""
+    import torch
+    from ldpc_error_floor_amd.decoder import NMSDecoder
+    dec0, cp, punct, short = _decoder("wman_qms", cuda_device)
+    for dt, q in ((2, q_bit), (1, 5)):
+        dec = NMSDecoder(dec0.graph.proto, 24, dec0.weights, dt, q, device=cuda_device)
+        B, off, seed = 777, 12345, 5
+        sigma = float(cp.sigma(1.0))
+        llr = dec.awgn(B, sigma, seed, offset=off)
+        idx_h = np.arange(B - 1, -1, -7, dtype=np.int64)
+        idx = torch.from_numpy(idx_h).to(cuda_device)
+        rows = torch.empty((idx_h.size, dec.n_vars), dtype=torch.float32, device=cuda_device)
+        dec._ext.channel_awgn_rows(rows.data_ptr(), idx.data_ptr(), idx_h.size, dec.n_vars, sigma,
+                                   seed, off, dec.decoding_type, dec.q_bit, 0, 0, 0, 0, dec.clip,
+                                   torch.cuda.current_stream(cuda_device).cuda_stream)
+        torch.cuda.synchronize(cuda_device)
+        assert torch.equal(rows, llr[idx]), (dt, q)
