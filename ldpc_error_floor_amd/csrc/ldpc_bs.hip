@@ -89,7 +89,7 @@ struct BsPlan {
     bool ok = false;
     int inst = -1, nw = 0, cn_lanes = 0, arows = 1, bcols = 1;
     uint32_t off_slots = 0, off_pad = 0, off_zero = 0, off_red = 0, off_alut = 0, off_blut = 0, off_hdz = 0,
-             off_btid = 0, off_ch = 0, off_hdl = 0;
+             off_btid = 0, off_ch = 0, off_hdl = 0, off_preb = 0;
     int cn_dmin = 0;
     bool ucn = false;
     bool colalign = false;         // variable lanes: each column on a half-wave of its own
@@ -235,6 +235,15 @@ static BsPlan plan_inst(const DevGraph& g, int i, bool ucn, float clip, int min_
         const int EPL = (k.D + k.LPC - 1) / k.LPC, HDW = (EPL + 1) / 2;
         p.off_hdl = (uint32_t)o;
         o += (size_t)4 * HDW * 64 * p.nw;
+    }
+    // the check-idle waves' next channel tables (PREB, ldpc_bs_kernel.h): 16 B per lane of the
+    // waves past cn_lanes
+    const bool preb = (BS_PREB < 0 ? (k.UCN && k.VPL == 1 && k.CPL == 1) : BS_PREB != 0) && k.VPL == 1 &&
+                      k.CPL == 1 && !BS_BTID_LDS;
+    if (preb && p.nw * 64 > p.cn_lanes) {
+        o = (o + 15) & ~(size_t)15;
+        p.off_preb = (uint32_t)o;
+        o += (size_t)16 * (64 * p.nw - p.cn_lanes);
     }
     p.lds = (o + 15) & ~(size_t)15;
     if (p.lds > BS_LDS_MAX) return p;
@@ -832,6 +841,7 @@ int bs_decode(const DevGraph& g, const Bufs& b, FusedWorkspace& ws, const float*
     a.off_hdz = p.off_hdz;
     a.off_btid = p.off_btid;
     a.off_hdl = p.off_hdl;
+    a.off_preb = p.off_preb;
     a.off_ch = p.off_ch;
     if (const char* e = getenv("LDPC_DIAG_ABLATE")) a.ablate = atoi(e);   // -DBS_DIAG builds
     const int nblocks = (int)((b.B + PACK - 1) / PACK);
@@ -919,12 +929,19 @@ static int bs_bounds_check(const DevGraph& g, const BsPlan& p, const BsHostTable
     const int HWA = (EPL + 1) / 2;
     const int GW = (GBL && k.PK && BS_ALDS) ? ((1 + HWA) | 1) : 1;
     // the allocations
+    if (getenv("LDPC_BOUNDS_VERBOSE"))
+        fprintf(stderr, "bs plan: inst %d nw %d ucn %d lds %lld (slots %u..%u, alut %u, blut %u, ch %u, hdl %u)\n",
+                p.inst, p.nw, (int)p.ucn, lds, p.off_slots, p.off_pad, p.off_alut, p.off_blut, p.off_ch, p.off_hdl);
     r.in("lds size", lds, (long long)BS_LDS_MAX + 1);
     if ((long long)t.vn.size() != (long long)VPL * NT * VNW) r.fail("vn_tab size", (long long)t.vn.size(), (long long)VPL * NT * VNW);
     r.lds("RED", p.off_red, 4LL * (16 + ((T + 3) & ~3) + BS_FLORW), 0, p.off_alut);
     r.lds("ALUT", p.off_alut, 4 * 2 * AL, 0, p.off_blut);
     r.lds("BLUT", p.off_blut, 4 * 2 * BL, 0, lds);
     r.lds("PAD+ZERO", p.off_pad, 2 * SLOT_B, p.off_slots, p.off_red);
+    // (PREB) the check-idle waves' lanes, 16 B each
+    if (p.off_preb)
+        for (int w = p.cn_lanes / 64; w < nwv; ++w)
+            r.lds("PREB", p.off_preb + 16LL * (64 * w - p.cn_lanes), 16LL * 64, p.off_preb, lds);
     if (UCN) r.lds("HD", 0, 4LL * (nv + 1), 0, p.off_slots);
     // the in-prologue channel's sampler tables (Q8 builds, gen.lds = off_slots): inside the slot
     // region, which the kernel writes only after the prologue, and clear of PAD / ZERO / RED /

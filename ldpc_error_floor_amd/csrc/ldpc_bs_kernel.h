@@ -141,7 +141,8 @@ struct BsArgs {
                                  // check phase needs the syndromes); iterations >= 64: on
     uint32_t off_hdl;            // BS_HDLDS (one-chunk UCN instances): the check lanes' packed
                                  // hard-decision addresses, [HDW][lane] words
-    uint32_t pad_;
+    uint32_t off_preb;           // (PREB) |Q(beta ch)| of the check-idle waves' variables, 16 B per
+                                 // lane from wave cn_lanes / 64 on; 0: none
     BsGen gen;                   // Q8 builds: the in-prologue channel
     unsigned long long* stamps;  // -DBS_STAMP builds only: [16 waves][16] shader-clock sums per
                                  // phase (0 check, 1 check barrier, 2 variable, 3 variable barrier,
@@ -839,6 +840,14 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 // iteration, whose result the table jump waits for) loaded before the check phase instead of
 // at their use: 1 for the multi-chunk instances (one workgroup per CU, so nothing else hides a
 // wave's L2 round trip after the barrier), 2 for every instance, 0 off (A/B switch)
+// (PREB) the check-idle waves' next channel tables evaluated in the check phase: -1 the one-chunk
+// UCN instance, 0 off, 1 every one-chunk instance.  Off: on 802.11n (C3) it cost 2 % (same box,
+// profiles/r6/session_r6w.log: 12.67 against 12.41 ms, counters equal) -- the second inlined
+// copy of the table code doubled the loop's SGPR spills (30 -> 56) for ~12 % of five waves'
+// variable phase
+#ifndef BS_PREB
+#define BS_PREB 0
+#endif
 #ifndef BS_BKPF
 #define BS_BKPF 1
 #endif
@@ -1140,9 +1149,92 @@ k_bs(BsArgs a) {
     //          Tv = clamp(Q(beta_{t+1} ch) + S) and V->C_e = clamp(Tv - C->V_e, +-15) per edge
     //   UCN:   the hard decision (APP_t >= 0; first: lw_0 >= 0) to HD[v] for the next check phase
     constexpr bool BKPF = !XP && BS_BFIX && !BS_BTID_LDS && (BS_BKPF == 2 || (BS_BKPF == 1 && VPL > 1));
+    // the one-chunk UCN instance (802.11n: 108 checks x 4 lanes fill 7 of 12 waves): the
+    // check-idle waves evaluate the next variable phase's channel tables during the check phase
+    constexpr bool PREB = (BS_PREB < 0 ? (UCN && VPL == 1 && CPL == 1) : BS_PREB != 0) && VPL == 1 &&
+                          CPL == 1 && !XP && !BS_BTID_LDS;
     int bkp[VPL];                        // (BKPF) the ids of iteration tb's tables, loaded early
 #pragma unroll
     for (int u = 0; u < VPL; ++u) bkp[u] = -1;
+    // |Q(beta_tb ch)| (4 planes) of the lane's variable u: the identity table, one of the fixed
+    // set (wave-uniform id: a jump into immediate truth tables), the iteration's table in
+    // constant memory (one beta per iteration) or the LDS table words (bslice).  pre: evaluated
+    // ahead, in the check phase, where the LDS tables of iteration tb may still be in flight:
+    // returns false (nothing done) for the paths that read them
+    auto beta_lw = [&](const int u, const uint32_t bslice, const int tb, const uint32_t (&cmu)[4],
+                       uint32_t (&lw)[4], const bool use_bk, const bool pre, const bool nobig)
+                       __attribute__((always_inline)) -> bool {
+        int bk = -1;
+        if constexpr (!XP && BS_BFIX) {
+            if (use_bk && a.btid) {
+                const int col = (a.bcols == 1) ? 0 : pcol[u];
+                if (BKPF) bk = __builtin_amdgcn_readfirstlane(bkp[u]);
+                else if (col >= 0)   // (BS_BTID_S: a scalar load, through the constant address space)
+                    bk = __builtin_amdgcn_readfirstlane(
+                        BS_BTID_LDS ? (int)lds_w(a.off_btid + 4u * (uint32_t)col)
+                        : BS_BTID_S ? (int)((const ConstW*)a.btid)[(size_t)tb * a.btid_n + col]
+                                    : a.btid[(size_t)tb * a.btid_n + col]);
+            }
+        }
+        // identity table: |Q(beta ch)| = |ch| (the mask covers iterations 0..63)
+        if (ABL(2) || (tb < 64 && ((a.beta_id >> tb) & 1))) {
+            PH("vn_beta_id", u);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lw[i] = cmu[i];
+        } else if (bk >= 0 && bk < kNBetaTab) {   // a table of the fixed set
+            if (pre && BIG && a.bcols > 1 && !nobig) return false;
+            PH("vn_beta_fix", u);
+            beta_asm(lw, cmu, bk);
+            if constexpr (BIG) {            // shortened bits: |Q(beta cu)| from the table words
+                if (a.bcols == 1) {
+                    const ConstW* tg = (const ConstW*)(a.blut) + (size_t)tb * BLUT_W;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) lw[i] = mux(bg[u], tg[LUT_W + i], lw[i]);
+                } else if (!pre) {          // (pre: no shortened bit in the wave)
+                    const v4u gb = lds_q(bslice + tab_b[u] + LUT_W * 4);
+                    lw[0] = mux(bg[u], gb.x, lw[0]);
+                    lw[1] = mux(bg[u], gb.y, lw[1]);
+                    lw[2] = mux(bg[u], gb.z, lw[2]);
+                    lw[3] = mux(bg[u], gb.w, lw[3]);
+                }
+            }
+        } else if (a.bcols == 1) {          // one beta per iteration: table in SGPRs
+            PH("vn_beta_sg", u);
+            const ConstW* tg = (const ConstW*)(a.blut) + (size_t)tb * BLUT_W;
+            lut_s(lw, cmu, tg);
+            if constexpr (BIG) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) lw[i] = mux(bg[u], tg[LUT_W + i], lw[i]);
+            }
+        } else {
+            if (pre) return false;
+            PH("vn_beta_lds", u);
+            const uint32_t btab = bslice + tab_b[u];
+            const uint32_t cmi[1][4] = {{cmu[0], cmu[1], cmu[2], cmu[3]}};
+            uint32_t lo[1][4];
+            lut<1>(lo, cmi, btab);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lw[i] = lo[0][i];
+            if constexpr (BIG) {
+                const v4u gb = lds_q(btab + LUT_W * 4);
+                lw[0] = mux(bg[u], gb.x, lw[0]);
+                lw[1] = mux(bg[u], gb.y, lw[1]);
+                lw[2] = mux(bg[u], gb.z, lw[2]);
+                lw[3] = mux(bg[u], gb.w, lw[3]);
+            }
+        }
+        return true;
+    };
+    // (PREB) the check-idle waves' |Q(beta_{t+1} ch)|, evaluated during the check phase of
+    // iteration t (their lanes hold no check), read back by the variable phase
+    bool preb_done = false;
+    // (no shortened bit in any lane of the wave: the fixed tables' shortened-bit planes unneeded)
+    const bool nobig = !BIG || __builtin_amdgcn_ballot_w64(bg[0] != 0u) == 0ull;
+    // (the lane's 16 B, recomputed at each use from the lane id: no address held through the loop)
+    auto pre_addr = [&]() __attribute__((always_inline)) -> uint32_t {
+        const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        return a.off_preb + 16u * ((uint32_t)(wave * 64 - a.cn_lanes) + ln);
+    };
     auto vn_phase = [&](const bool first, const bool last, const uint32_t bslice, const int tb)
                         __attribute__((always_inline)) {
         uint32_t wr = 0u, apos = 0u, nb = 0u;
@@ -1178,62 +1270,16 @@ k_bs(BsArgs a) {
             }
             const bool counted = v >= 0 && v < a.target_bits;
             uint32_t lw[1][4];                   // |Q(beta_{t+1} ch)| (before the C->V: fewer live registers)
-            // the table's index in the fixed set (wave-uniform; -1: evaluate the table words)
-            int bk = -1;
-            if constexpr (!XP && BS_BFIX) {
-                if (!first && !last && a.btid) {
-                    const int col = (a.bcols == 1) ? 0 : pcol[u];
-                    if (BKPF) bk = __builtin_amdgcn_readfirstlane(bkp[u]);
-                    else if (col >= 0)   // (BS_BTID_S: a scalar load, through the constant address space)
-                        bk = __builtin_amdgcn_readfirstlane(
-                            BS_BTID_LDS ? (int)lds_w(a.off_btid + 4u * (uint32_t)col)
-                            : BS_BTID_S ? (int)((const ConstW*)a.btid)[(size_t)tb * a.btid_n + col]
-                                        : a.btid[(size_t)tb * a.btid_n + col]);
-                }
-            }
             PH("vn_beta", (last ? 100 : 0) + u);
             if (!last) {
-                // identity table: |Q(beta ch)| = |ch| (the mask covers iterations 0..63)
-                if (ABL(2) || (tb < 64 && ((a.beta_id >> tb) & 1))) {
-                    PH("vn_beta_id", u);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) lw[0][i] = cmu[i];
-                } else if (bk >= 0 && bk < kNBetaTab) {   // a table of the fixed set
-                    PH("vn_beta_fix", u);
-                    beta_asm(lw[0], cmu, bk);
-                    if constexpr (BIG) {            // shortened bits: |Q(beta cu)| from the table words
-                        if (a.bcols == 1) {
-                            const ConstW* tg = (const ConstW*)(a.blut) + (size_t)tb * BLUT_W;
-#pragma unroll
-                            for (int i = 0; i < 4; ++i) lw[0][i] = mux(bg[u], tg[LUT_W + i], lw[0][i]);
-                        } else {
-                            const v4u gb = lds_q(bslice + tab_b[u] + LUT_W * 4);
-                            lw[0][0] = mux(bg[u], gb.x, lw[0][0]);
-                            lw[0][1] = mux(bg[u], gb.y, lw[0][1]);
-                            lw[0][2] = mux(bg[u], gb.z, lw[0][2]);
-                            lw[0][3] = mux(bg[u], gb.w, lw[0][3]);
-                        }
-                    }
-                } else if (a.bcols == 1) {          // one beta per iteration: table in SGPRs
-                    PH("vn_beta_sg", u);
-                    const ConstW* tg = (const ConstW*)(a.blut) + (size_t)tb * BLUT_W;
-                    lut_s(lw[0], cmu, tg);
-                    if constexpr (BIG) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) lw[0][i] = mux(bg[u], tg[LUT_W + i], lw[0][i]);
-                    }
+                if (PREB && !first && preb_done) {          // (evaluated in the check phase)
+                    const v4u q = lds_q(pre_addr());
+                    lw[0][0] = q.x;
+                    lw[0][1] = q.y;
+                    lw[0][2] = q.z;
+                    lw[0][3] = q.w;
                 } else {
-                    PH("vn_beta_lds", u);
-                    const uint32_t btab = bslice + tab_b[u];
-                    const uint32_t cmi[1][4] = {{cmu[0], cmu[1], cmu[2], cmu[3]}};
-                    lut<1>(lw, cmi, btab);
-                    if constexpr (BIG) {
-                        const v4u gb = lds_q(btab + LUT_W * 4);
-                        lw[0][0] = mux(bg[u], gb.x, lw[0][0]);
-                        lw[0][1] = mux(bg[u], gb.y, lw[0][1]);
-                        lw[0][2] = mux(bg[u], gb.z, lw[0][2]);
-                        lw[0][3] = mux(bg[u], gb.w, lw[0][3]);
-                    }
+                    (void)beta_lw(u, bslice, tb, cmu, lw[0], !first, false, false);
                 }
             }
             // C->V of the first KEEP edges stay in registers for the V->C pass, the others are read
@@ -1591,6 +1637,31 @@ k_bs(BsArgs a) {
         if (PRIO == 9) {
             if (heavy_c) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
+        }
+        if constexpr (PREB) {
+            preb_done = false;
+            if (a.off_preb && wave * 64 >= a.cn_lanes && t + 1 < a.T) {
+                uint32_t cmu[4] = {cm[0][0], cm[0][1], cm[0][2], cm[0][3]};
+                if (BS_CH_LDS) {
+                    int tl = tid;
+                    asm volatile("" : "+v"(tl));
+                    const v4u c4 = lds_q(a.off_ch + 16u * (uint32_t)tl);
+                    cmu[0] = c4.x;
+                    cmu[1] = c4.y;
+                    cmu[2] = c4.z;
+                    cmu[3] = c4.w;
+                }
+                uint32_t lwp[4];
+                if (beta_lw(0, 0u, t + 1, cmu, lwp, true, true, nobig)) {
+                    v4u q;
+                    q.x = lwp[0];
+                    q.y = lwp[1];
+                    q.z = lwp[2];
+                    q.w = lwp[3];
+                    *reinterpret_cast<LdsQ*>(pre_addr()) = q;
+                    preb_done = true;
+                }
+            }
         }
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
