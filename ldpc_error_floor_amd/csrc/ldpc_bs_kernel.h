@@ -840,6 +840,12 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 // iteration, whose result the table jump waits for) loaded before the check phase instead of
 // at their use: 1 for the multi-chunk instances (one workgroup per CU, so nothing else hides a
 // wave's L2 round trip after the barrier), 2 for every instance, 0 off (A/B switch)
+// loop-top table copies with opaque bounds (hoisted, their compares were 64-bit lane masks held
+// through the loop and spilled: C2's in-loop v_readlane 35 -> 24 static; same box,
+// profiles/r6/session_r6x.log: C2 4.427 -> 4.406 ms, C4 10.542 -> 10.447, C3 12.451 -> 12.378)
+#ifndef BS_TOPO
+#define BS_TOPO 1
+#endif
 // (PREB) the check-idle waves' next channel tables evaluated in the check phase: -1 the one-chunk
 // UCN instance, 0 off, 1 every one-chunk instance.  Off: on 802.11n (C3) it cost 2 % (same box,
 // profiles/r6/session_r6w.log: 12.67 against 12.41 ms, counters equal) -- the second inlined
@@ -1603,9 +1609,13 @@ k_bs(BsArgs a) {
                     asm volatile("" : "+v"(tl));
                     cw = __builtin_amdgcn_readfirstlane(tl >> 6);
                 }
-                copy_async(a.off_alut + 4u * (uint32_t)(nx * AL), a.alut + (size_t)(t + 1) * AL, AL, cw, NT);
-                if (a.bcols > 1)
-                    copy_async(a.off_blut + 4u * (uint32_t)(nx * BL), a.blut + (size_t)(t + 1) * BL, BL, cw, NT);
+                // (BS_TOPO: the copies' wave-uniform bounds made opaque per iteration, so their
+                // compares are redone here instead of held through the loop as 64-bit lane masks)
+                int al = AL, bl = BL, bcl = a.bcols;
+                if (BS_TOPO) asm volatile("" : "+s"(cw), "+s"(al), "+s"(bl), "+s"(bcl));
+                copy_async(a.off_alut + 4u * (uint32_t)(nx * al), a.alut + (size_t)(t + 1) * al, al, cw, NT);
+                if (bcl > 1)
+                    copy_async(a.off_blut + 4u * (uint32_t)(nx * bl), a.blut + (size_t)(t + 1) * bl, bl, cw, NT);
                 if (!XP && BS_BFIX && BS_BTID_LDS && a.btid)   // this iteration's variable phase: ids of row t + 1
                     copy_async(a.off_btid, reinterpret_cast<const uint32_t*>(a.btid) + (size_t)(t + 1) * a.btid_n,
                                a.bcols == 1 ? 1 : a.btid_n, cw, NT);
