@@ -26,6 +26,10 @@
 
 // the variable places' edge words not made opaque per use (bsl's BS_VAO; A/B switch, off: the C5
 // build then spills 16-17 VGPRs instead of 7)
+#ifndef BSC_TOPO
+#define BSC_TOPO 0     // the loop-top copies' bounds opaque per iteration (A/B switch: C5 46.37
+                       // against 46.34 ms, profiles/r6/session_r6y.log; off)
+#endif
 #ifndef BSC_VAO
 #define BSC_VAO 0
 #endif
@@ -468,9 +472,12 @@ k_bsc(BscArgs a) {
             // (the lane index made opaque per iteration: the copy addresses are recomputed here
             // rather than hoisted out of the T loop into registers the loop body spills)
             if (BS_GLDS) {            // (async global -> LDS, retired by the next barrier: bsl)
-                copy_async(a.off_alut + 4u * (uint32_t)(nx * AL), a.alut + (size_t)(t + 1) * AL, AL, wave, NT);
-                if (a.bcols > 1)
-                    copy_async(a.off_blut + 4u * (uint32_t)(nx * BL), a.blut + (size_t)(t + 1) * BL, BL, wave, NT);
+                // (BSC_TOPO: the bounds opaque per iteration, as bsl's BS_TOPO)
+                int cw = wave, al = AL, bl = BL, bcl = a.bcols;
+                if (BSC_TOPO) asm volatile("" : "+s"(cw), "+s"(al), "+s"(bl), "+s"(bcl));
+                copy_async(a.off_alut + 4u * (uint32_t)(nx * al), a.alut + (size_t)(t + 1) * al, al, cw, NT);
+                if (bcl > 1)
+                    copy_async(a.off_blut + 4u * (uint32_t)(nx * bl), a.blut + (size_t)(t + 1) * bl, bl, cw, NT);
             } else {
                 int tl = tid;
                 asm volatile("" : "+v"(tl));
