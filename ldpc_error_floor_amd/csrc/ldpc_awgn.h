@@ -35,12 +35,25 @@
 
 namespace ldpc {
 
+// Philox products as separate high / low multiplies (A/B switch; off: the v_mad_u64_u32 form
+// is faster in the prologue channel despite valu_rate's per-instruction figures -- C2 sweep step
+// 4.652 against 4.733 ms, C4 10.960 against 11.130, profiles/r6/session_r6aa.log)
+#ifndef AWGN_MULHL
+#define AWGN_MULHL 0
+#endif
+
 struct Philox {
     static __device__ __forceinline__ void round(uint32_t (&c)[4], const uint32_t (&k)[2]) {
+#if AWGN_MULHL
+        // (v_mul_hi_u32 + v_mul_lo_u32 instead of the one v_mad_u64_u32 of the 64-bit product)
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+#else
         const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
         const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#endif
         // (three-input xors as one v_bitop3 each)
         c[0] = __builtin_amdgcn_bitop3_b32(hi1, c[1], k[0], 0x96);
         c[1] = lo1;

@@ -25,7 +25,7 @@ cp $L $OUT/.lib_default.so
 restore() { cp $OUT/.lib_default.so $L; }
 bench_ms() {   # config, extra args -> prints "ms kernel value"
   timeout -k 10 300 python bench.py --config $1 --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-companions $2 > $OUT/.ab.json 2> $OUT/.ab.err || { tail -5 $OUT/.ab.err; return 1; }
-  python -c "import json;d=json.load(open('$OUT/.ab.json'));print(d['ms_per_step'], d['config']['kernel'], d['value'], d['counters']['frame_err_last'])"
+  python -c "import json;d=json.load(open('$OUT/.ab.json'));print(d['ms_per_step'], d['config']['kernel'], d['value'], d['counters']['frame_err_last'], 'e2e', d['e2e_with_rng']['ms_per_step'])"
 }
 for step in "$@"; do
   echo "== $step $(date +%T)"
