@@ -842,7 +842,9 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 // wave's L2 round trip after the barrier), 2 for every instance, 0 off (A/B switch)
 // loop-top table copies with opaque bounds (hoisted, their compares were 64-bit lane masks held
 // through the loop and spilled: C2's in-loop v_readlane 35 -> 24 static; same box,
-// profiles/r6/session_r6x.log: C2 4.427 -> 4.406 ms, C4 10.542 -> 10.447, C3 12.451 -> 12.378)
+// profiles/r6/session_r6x.log: C2 4.427 -> 4.406 ms, C4 10.542 -> 10.447, C3 12.451 -> 12.378).
+// Not in the in-prologue channel builds (Q8): there it cost the sweep step 1.1 % (4.651 against
+// 4.599 ms, session_r6ac.log)
 #ifndef BS_TOPO
 #define BS_TOPO 1
 #endif
@@ -1612,7 +1614,7 @@ k_bs(BsArgs a) {
                 // (BS_TOPO: the copies' wave-uniform bounds made opaque per iteration, so their
                 // compares are redone here instead of held through the loop as 64-bit lane masks)
                 int al = AL, bl = BL, bcl = a.bcols;
-                if (BS_TOPO) asm volatile("" : "+s"(cw), "+s"(al), "+s"(bl), "+s"(bcl));
+                if (BS_TOPO && !Q8) asm volatile("" : "+s"(cw), "+s"(al), "+s"(bl), "+s"(bcl));
                 copy_async(a.off_alut + 4u * (uint32_t)(nx * al), a.alut + (size_t)(t + 1) * al, al, cw, NT);
                 if (bcl > 1)
                     copy_async(a.off_blut + 4u * (uint32_t)(nx * bl), a.blut + (size_t)(t + 1) * bl, bl, cw, NT);
