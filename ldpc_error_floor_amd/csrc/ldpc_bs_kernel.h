@@ -843,8 +843,9 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 // loop-top table copies with opaque bounds (hoisted, their compares were 64-bit lane masks held
 // through the loop and spilled: C2's in-loop v_readlane 35 -> 24 static; same box,
 // profiles/r6/session_r6x.log: C2 4.427 -> 4.406 ms, C4 10.542 -> 10.447, C3 12.451 -> 12.378).
-// Not in the in-prologue channel builds (Q8): there it cost the sweep step 1.1 % (4.651 against
-// 4.599 ms, session_r6ac.log)
+// Not in wman's in-prologue channel build (Q8): there it cost the sweep step 1.1 % (4.651
+// against 4.599 ms, session_r6ac.log), where the other Q8 builds gained (sweep step without /
+// with it, two boxes each: C3 80.5 / 83.1 M cw/s, C4 94.5 / 96.0 M; session_r6ad, r6z, r6ab)
 #ifndef BS_TOPO
 #define BS_TOPO 1
 #endif
@@ -1614,7 +1615,8 @@ k_bs(BsArgs a) {
                 // (BS_TOPO: the copies' wave-uniform bounds made opaque per iteration, so their
                 // compares are redone here instead of held through the loop as 64-bit lane masks)
                 int al = AL, bl = BL, bcl = a.bcols;
-                if (BS_TOPO && !Q8) asm volatile("" : "+s"(cw), "+s"(al), "+s"(bl), "+s"(bcl));
+                if (BS_TOPO && !(Q8 && VPL == 1 && CPL == 1 && !UCN))
+                    asm volatile("" : "+s"(cw), "+s"(al), "+s"(bl), "+s"(bcl));
                 copy_async(a.off_alut + 4u * (uint32_t)(nx * al), a.alut + (size_t)(t + 1) * al, al, cw, NT);
                 if (bcl > 1)
                     copy_async(a.off_blut + 4u * (uint32_t)(nx * bl), a.blut + (size_t)(t + 1) * bl, bl, cw, NT);
