@@ -849,6 +849,13 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 #ifndef BS_TOPO
 #define BS_TOPO 1
 #endif
+// loop-top table addresses reloaded from the kernel arguments per iteration (scalar loads from
+// the kernarg segment, whose pointer stays in its SGPRs) instead of held through the T loop:
+// C3's loop spill reloads 16 -> 0, C2's 8 -> 3; same box, profiles/r6/session_r6ah.log: C2
+// 4.406 -> 4.322 ms, C3 12.361 -> 12.157 (sweep step 12.628 -> 12.464)
+#ifndef BS_KARG
+#define BS_KARG 1
+#endif
 // (PREB) the check-idle waves' next channel tables evaluated in the check phase: -1 the one-chunk
 // UCN instance, 0 off, 1 every one-chunk instance.  Off: on 802.11n (C3) it cost 2 % (same box,
 // profiles/r6/session_r6w.log: 12.67 against 12.41 ms, counters equal) -- the second inlined
@@ -1617,9 +1624,26 @@ k_bs(BsArgs a) {
                 int al = AL, bl = BL, bcl = a.bcols;
                 if (BS_TOPO && !(Q8 && VPL == 1 && CPL == 1 && !UCN))
                     asm volatile("" : "+s"(cw), "+s"(al), "+s"(bl), "+s"(bcl));
-                copy_async(a.off_alut + 4u * (uint32_t)(nx * al), a.alut + (size_t)(t + 1) * al, al, cw, NT);
+                // (BS_KARG: the tables' addresses loaded again from the kernel arguments each
+                // iteration (scalar loads) instead of held through the loop, where they were
+                // spilled to VGPR lanes and reloaded by v_readlane)
+                const uint32_t* alut_p = a.alut;
+                const uint32_t* blut_p = a.blut;
+                uint32_t off_al = a.off_alut, off_bl = a.off_blut;
+                // (one-chunk instances: the multi-chunk build spilled more with it, C4's loop
+                // reloads 4 -> 44; wman's in-prologue channel build: its sweep step 0.4 % slower)
+                if constexpr (BS_KARG && VPL == 1 && CPL == 1 && !(Q8 && !UCN)) {
+                    typedef __attribute__((address_space(4))) const BsArgs ConstArgs;
+                    ConstArgs* ka = (ConstArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+                    asm volatile("" : "+s"(ka));
+                    alut_p = ka->alut;
+                    blut_p = ka->blut;
+                    off_al = ka->off_alut;
+                    off_bl = ka->off_blut;
+                }
+                copy_async(off_al + 4u * (uint32_t)(nx * al), alut_p + (size_t)(t + 1) * al, al, cw, NT);
                 if (bcl > 1)
-                    copy_async(a.off_blut + 4u * (uint32_t)(nx * bl), a.blut + (size_t)(t + 1) * bl, bl, cw, NT);
+                    copy_async(off_bl + 4u * (uint32_t)(nx * bl), blut_p + (size_t)(t + 1) * bl, bl, cw, NT);
                 if (!XP && BS_BFIX && BS_BTID_LDS && a.btid)   // this iteration's variable phase: ids of row t + 1
                     copy_async(a.off_btid, reinterpret_cast<const uint32_t*>(a.btid) + (size_t)(t + 1) * a.btid_n,
                                a.bcols == 1 ? 1 : a.btid_n, cw, NT);
