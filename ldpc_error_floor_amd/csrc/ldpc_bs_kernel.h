@@ -856,6 +856,13 @@ __device__ __forceinline__ void gen_tables(const BsGen& g, int tid, int NT) {
 #ifndef BS_KARG
 #define BS_KARG 1
 #endif
+// the epilogue's output pointers loaded from the kernel arguments after the T loop, so the
+// loop does not hold them from the kernel's entry (C2's channel-build loop reloads 20 -> 11;
+// same box, profiles/r6/session_r6ak.log: C3 12.124 -> 12.052 ms, sweep steps C2 4.604 ->
+// 4.561, C3 12.44 -> 12.34)
+#ifndef BS_KEPI
+#define BS_KEPI 1
+#endif
 // (PREB) the check-idle waves' next channel tables evaluated in the check phase: -1 the one-chunk
 // UCN instance, 0 off, 1 every one-chunk instance.  Off: on 802.11n (C3) it cost 2 % (same box,
 // profiles/r6/session_r6w.log: 12.67 against 12.41 ms, counters equal) -- the second inlined
@@ -2003,13 +2010,29 @@ k_bs(BsArgs a) {
         __syncthreads();
         BS_ST(3);
     }
+    // the epilogue's output pointers (BS_KEPI: loaded from the kernel arguments here, not held
+    // through the T loop from the kernel's entry)
+    int64_t* e_counters = a.counters;
+    uint8_t* e_flags = a.flags;
+    uint32_t* e_iter_wrong = a.iter_wrong;
+    int64_t e_B = a.B;
+    // (not C4's decode build: more loop spills; not wman's decode build: 0.5 % slower)
+    if constexpr (BS_KEPI && (Q8 || (VPL == 1 && CPL == 1 && UCN))) {
+        typedef __attribute__((address_space(4))) const BsArgs ConstArgs;
+        ConstArgs* ka = (ConstArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka));
+        e_counters = ka->counters;
+        e_flags = ka->flags;
+        e_iter_wrong = ka->iter_wrong;
+        e_B = ka->B;
+    }
     if (tid == 0) {
         const uint32_t wl = RED[0] & valid;
         const uint32_t all = RED[1] & RED[0] & valid;
         const uint32_t ap = RED[2] & valid;
         RED[16 + a.T - 1] = RED[0];
-        if (a.counters) {
-            unsigned long long* cc = reinterpret_cast<unsigned long long*>(a.counters);
+        if (e_counters) {
+            unsigned long long* cc = reinterpret_cast<unsigned long long*>(e_counters);
             const unsigned long long c0 = RED[3], c1 = __popc(wl), c2 = __popc(all),
                                      c3 = 2ull * __popc(ap) + __popc(wl & ~ap);
             if (c0) atomicAdd(cc + 0, c0);
@@ -2020,13 +2043,13 @@ k_bs(BsArgs a) {
         RED[5] = all;
         RED[6] = wl;
     }
-    if (a.flags || a.iter_wrong) {
+    if (e_flags || e_iter_wrong) {
         __syncthreads();
-        if (a.flags && tid < nvalid)
-            a.flags[b0 + tid] = (uint8_t)(((RED[5] >> tid) & 1) | (((RED[6] >> tid) & 1) << 1));
-        if (a.iter_wrong)                   // [T][packs]: iteration t's frame-error word
+        if (e_flags && tid < nvalid)
+            e_flags[b0 + tid] = (uint8_t)(((RED[5] >> tid) & 1) | (((RED[6] >> tid) & 1) << 1));
+        if (e_iter_wrong)                   // [T][packs]: iteration t's frame-error word
             for (int t = tid; t < a.T; t += NT)
-                a.iter_wrong[(size_t)t * (size_t)((a.B + 31) >> 5) + blockIdx.x] = RED[16 + t] & valid;
+                e_iter_wrong[(size_t)t * (size_t)((e_B + 31) >> 5) + blockIdx.x] = RED[16 + t] & valid;
     }
 #ifdef BS_STAMP
     BS_ST(5);
